@@ -1,0 +1,216 @@
+/*
+ * stc.h — the C ABI of libstc.so, the MI355X-native text-clustering hot path.
+ *
+ * This is the drop-in boundary: the entry points a JNI shim binds so that
+ * the reference's Spark pipeline can route its hot path to HIP kernels on gfx950.  Plain C
+ * types only (pointers + sizes); no torch, no C++ in the signatures.
+ *
+ * Which reference interface each entry point replaces ([U] = upstream spark-mllib 2.4.3,
+ * TextClustering/build.sbt:10; paths relative to /root/reference/TextClustering/src/main/scala):
+ *
+ *   stc_hashing_tf[_dev]        [U] mllib.feature.HashingTF.transform / murmur3Hash — the slot of
+ *                               the vocab-indexed counting at LDAClustering.scala:154-167
+ *   stc_idf_fit                 IDF(minDocFreq).fit(tf).idf — LDAClustering.scala:177
+ *   stc_idf_transform           tf × idf (+ the 0 → 1e-4 floor) — LDAClustering.scala:180-192
+ *   stc_lda_create / set_corpus new LDA().setOptimizer(online)...setK... — LDAClustering.scala:37-54
+ *                               ([U] OnlineLDAOptimizer.initialize)
+ *   stc_lda_next / stc_lda_step one OnlineLDAOptimizer.next() / submitMiniBatch inside
+ *                               lda.run(corpus) — LDAClustering.scala:61
+ *   stc_lda_get_topics          [U] LocalLDAModel.topicsMatrix (getLDAModel)
+ *   stc_lda_describe            ldaModel.describeTopics(maxTermsPerTopic) — LDAClustering.scala:81,
+ *                               LDALoader.scala:66
+ *   stc_lda_topic_distribution  toLocal.topicDistribution(tf) — LDALoader.scala:108
+ *   stc_lda_bound               [U] LocalLDAModel.logLikelihood / logPerplexity
+ *   stc_comm_*                  the role of Spark's broadcast + treeReduce inside lda.run
+ *                               (one RCCL all-reduce of k×V sstats per minibatch over xGMI)
+ *
+ * Conventions
+ *   - Every function returns STC_OK (0) or an STC_ERR_* code; the message of the last failure on
+ *     the calling thread is returned by stc_last_error().  The library never aborts.
+ *   - The caller owns every host array; output arrays are caller-allocated with the sizes given
+ *     in each comment.  The library owns all device memory behind the opaque handles.
+ *   - A handle is not thread-safe: serialise calls per handle.  One stc_ctx = one GPU; for
+ *     several GPUs run one process (or thread) per GPU and connect them with stc_comm_init.
+ *   - Matrices are row-major.  The topics matrix crosses the boundary as V×k (Spark's
+ *     topicsMatrix orientation, element (v, t) at [v*k + t]) unless a KV layout flag is given.
+ */
+#ifndef STC_H_
+#define STC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define STC_ABI_VERSION 1
+
+enum stc_status {
+  STC_OK = 0,
+  STC_ERR_INVALID_ARG = 1, /* maps to IllegalArgumentException on the JVM side */
+  STC_ERR_HIP = 2,         /* HIP runtime error (IllegalStateException) */
+  STC_ERR_RCCL = 3,        /* RCCL error */
+  STC_ERR_OOM = 4,         /* device allocation failed */
+  STC_ERR_STATE = 5        /* call not valid in the handle's current state */
+};
+
+enum stc_hash_variant {
+  STC_HASH_STANDARD = 0, /* MurmurHash3_x86_32 (Spark 3.x hashUnsafeBytes2) */
+  STC_HASH_SPARK24 = 1   /* Spark 2.4.x hashUnsafeBytes: per-byte sign-extended tail */
+};
+
+enum stc_dtype { STC_F32 = 0, STC_F64 = 1 };
+
+enum stc_layout {
+  STC_LAYOUT_VK = 0, /* V×k row-major: topicsMatrix(v, t) at [v*k + t] */
+  STC_LAYOUT_KV = 1  /* k×V row-major: Spark's internal λ / a column-major topicsMatrix */
+};
+
+typedef struct stc_ctx stc_ctx;   /* one device (+ optional RCCL communicator) */
+typedef struct stc_dcsr stc_dcsr; /* device-resident CSR matrix (rows = documents) */
+typedef struct stc_lda stc_lda;   /* online-LDA optimizer state / LocalLDAModel */
+
+/* ---- library / device ------------------------------------------------------------------ */
+const char* stc_last_error(void);
+int stc_abi_version(void);
+int stc_device_count(int* n_out);
+int stc_init(int device, stc_ctx** out);
+int stc_destroy(stc_ctx* ctx);
+int stc_synchronize(stc_ctx* ctx);
+
+/* ---- RCCL: one process per GPU ---------------------------------------------------------
+ * Rank 0 calls stc_comm_unique_id and ships the 128 bytes to the other ranks out of band
+ * (the Spark driver broadcast, or torch.distributed's store); every rank then calls
+ * stc_comm_init.  Once connected, stc_idf_fit, stc_lda_step/next and stc_lda_bound reduce
+ * their partial results over all ranks (RCCL all-reduce over xGMI).                        */
+int stc_comm_unique_id(uint8_t id_out[128]);
+int stc_comm_init(stc_ctx* ctx, const uint8_t id[128], int n_ranks, int rank);
+int stc_comm_allreduce_f64(stc_ctx* ctx, double* host_inout, int64_t n); /* host scalars */
+
+/* ---- device CSR ------------------------------------------------------------------------- */
+/* values are stored on device as `value_dtype` (STC_F32 or STC_F64) */
+int stc_dcsr_upload(stc_ctx* ctx, int64_t n_rows, int64_t n_cols, const int64_t* indptr,
+                    const int32_t* indices, const double* values, int value_dtype,
+                    stc_dcsr** out);
+int stc_dcsr_shape(const stc_dcsr* m, int64_t* n_rows, int64_t* n_cols, int64_t* nnz);
+/* indptr[n_rows+1], indices[nnz], values[nnz] (any may be NULL to skip) */
+int stc_dcsr_download(stc_ctx* ctx, const stc_dcsr* m, int64_t* indptr, int32_t* indices,
+                      double* values);
+int stc_dcsr_free(stc_dcsr* m);
+
+/* ---- HashingTF (K1 murmur3 + nonNegativeMod, K2 per-doc count → sorted CSR) -----------
+ * Tokens are given as one UTF-8 byte blob: token t is utf8[tok_off[t] .. tok_off[t+1]),
+ * document d owns tokens [doc_off[d], doc_off[d+1]).  Output row d holds the sorted distinct
+ * bucket indices nonNegativeMod(murmur3_x86_32(token, seed 42), num_features) and their
+ * counts (1.0 when binary).  Bit-exact with [U] HashingTF.transform.                      */
+int stc_hashing_tf_dev(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes,
+                       const int64_t* tok_off /* n_tok+1 */, int64_t n_tok,
+                       const int64_t* doc_off /* n_docs+1 */, int64_t n_docs,
+                       int32_t num_features, int binary, int hash_variant, int value_dtype,
+                       stc_dcsr** out);
+/* host-in/host-out convenience: indices_out/values_out need capacity n_tok */
+int stc_hashing_tf(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int64_t* tok_off,
+                   int64_t n_tok, const int64_t* doc_off, int64_t n_docs, int32_t num_features,
+                   int binary, int hash_variant, int64_t* indptr_out /* n_docs+1 */,
+                   int32_t* indices_out, double* values_out);
+/* raw per-token bucket indices (test hook for K1): idx_out[n_tok] */
+int stc_hash_tokens(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int64_t* tok_off,
+                    int64_t n_tok, int32_t num_features, int hash_variant, int32_t* idx_out);
+
+/* ---- IDF (K3 df count, K4 idf, K5 transform) ---------------------------------------------
+ * df_j = #rows with value_j > 0, m = #rows (summed over all ranks when connected);
+ * idf_j = df_j >= min_doc_freq ? ln((m+1)/(df_j+1)) : 0.                                  */
+int stc_idf_fit(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq,
+                double* idf_out /* n_cols */, int64_t* df_out /* n_cols, may be NULL */,
+                int64_t* m_out /* may be NULL */);
+/* values[e] *= idf[indices[e]]; when zero_floor > 0 an idf of exactly 0 is replaced by
+ * zero_floor (the reference's LDAClustering.scala:184-187 quirk; 0 = stock Spark)          */
+int stc_idf_transform(stc_ctx* ctx, stc_dcsr* tf, const double* idf /* n_cols */,
+                      double zero_floor);
+
+/* ---- online LDA ----------------------------------------------------------------------- */
+typedef struct stc_lda_config {
+  int32_t k;                     /* number of topics */
+  int64_t vocab_size;            /* V (= numFeatures) */
+  const double* doc_concentration; /* α: 1 value (−1 ⇒ 1/k) or k values */
+  int32_t doc_concentration_len;
+  double topic_concentration;    /* η (−1 ⇒ 1/k) */
+  double tau0;                   /* learningOffset, default 1024 */
+  double kappa;                  /* learningDecay, default 0.51 */
+  double mini_batch_fraction;    /* subsamplingRate, default 0.05 */
+  double gamma_shape;            /* default 100 */
+  int32_t optimize_doc_concentration; /* ml.LDA default 1, mllib default 0 */
+  int32_t sample_with_replacement;    /* mllib default 1 */
+  uint64_t seed;                 /* λ₀ / membership / γ₀ counter-RNG seed */
+  int32_t dtype;                 /* STC_F32 (default, fp32 E-step) or STC_F64 */
+  int32_t max_inner_iter;        /* E-step safety cap (upstream has none); 0 ⇒ 100000 */
+} stc_lda_config;
+
+/* fills the upstream defaults (ml.clustering.LDA) */
+void stc_lda_config_default(stc_lda_config* cfg);
+
+typedef struct stc_step_stats {
+  int64_t batch_docs;        /* docs in the minibatch on this rank */
+  int64_t nonempty_docs;     /* all ranks */
+  int64_t batch_entries;     /* (doc, term) entries on this rank */
+  int64_t inner_iters;       /* Σ E-step iterations on this rank */
+  int32_t inner_iters_max;
+  int32_t cap_hits;          /* docs stopped by max_inner_iter */
+  double rho;                /* learning rate used */
+} stc_step_stats;
+
+int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out);
+int stc_lda_destroy(stc_lda* lda);
+/* the documents of THIS rank; corpus_size_total = Σ over ranks (Spark's corpusSize).
+ * The CSR values are read in the LDA's dtype; the handle keeps a reference to `corpus`.    */
+int stc_lda_set_corpus(stc_lda* lda, const stc_dcsr* corpus, int64_t corpus_size_total);
+/* λ₀ ~ Gamma(gamma_shape, 1/gamma_shape) i.i.d. from the counter RNG (seed) — identical on
+ * every rank, so no broadcast is needed                                                    */
+int stc_lda_init_random(stc_lda* lda, uint64_t seed);
+int stc_lda_set_topics(stc_lda* lda, const double* topics, int layout);
+int stc_lda_get_topics(stc_lda* lda, double* topics_out, int layout);
+int stc_lda_set_alpha(stc_lda* lda, const double* alpha /* k */);
+int stc_lda_get_alpha(stc_lda* lda, double* alpha_out /* k */);
+int stc_lda_get_eta(stc_lda* lda, double* eta_out);
+int stc_lda_get_iteration(stc_lda* lda, int64_t* iteration_out);
+
+/* One submitMiniBatch over an injected membership: batch_doc_ids are row indices of this
+ * rank's corpus (duplicates allowed = sampling with replacement).  gamma0 (n×k, may be NULL)
+ * injects γ₀; otherwise γ₀ comes from the counter RNG keyed (seed, iteration, rank, pos).
+ * stats may be NULL (then the call does not wait for the GPU).                              */
+int stc_lda_step(stc_lda* lda, const int64_t* batch_doc_ids, int64_t n, const double* gamma0,
+                 stc_step_stats* stats);
+/* One OnlineLDAOptimizer.next(): device-side Poisson/Bernoulli membership sampling with
+ * fraction mini_batch_fraction, then the same step.                                        */
+int stc_lda_next(stc_lda* lda, stc_step_stats* stats);
+/* E-step only (no model update), for tests: gamma_out n×k; stat_out (k×V as V×k layout,
+ * may be NULL) receives the summed sufficient statistics Σ_d eθ_d ⊗ (cts/φ) scattered to
+ * their terms (Spark's `stat` before ⊙ expElogβ); iters_out n (may be NULL).              */
+int stc_lda_estep(stc_lda* lda, const int64_t* batch_doc_ids, int64_t n, const double* gamma0,
+                  double* gamma_out, double* stat_out, int32_t* iters_out);
+
+/* LocalLDAModel.logLikelihood over `docs` (any CSR with V columns, this rank's part):
+ * bound = corpusPart (Σ over all ranks) + topicsPart.  γ₀ per doc: gamma0 (rows×k) if given,
+ * else counter RNG keyed (gamma_seed, doc_id_base + row).  token_count = Σ values.          */
+int stc_lda_bound(stc_lda* lda, const stc_dcsr* docs, uint64_t gamma_seed, int64_t doc_id_base,
+                  const double* gamma0, double* bound_out, double* corpus_part_out,
+                  double* topics_part_out, double* token_count_out);
+/* LocalLDAModel.topicDistribution for every row of `docs`: out rows×k (zeros for empty rows) */
+int stc_lda_topic_distribution(stc_lda* lda, const stc_dcsr* docs, uint64_t gamma_seed,
+                               int64_t doc_id_base, const double* gamma0, double* out);
+/* LocalLDAModel.describeTopics(max_terms): idx_out k×N, weight_out k×N (N = min(max,V)) */
+int stc_lda_describe(stc_lda* lda, int32_t max_terms, int32_t* idx_out, double* weight_out);
+
+/* Average device time (ms, HIP events) of the last step's phases, for the bench:
+ * [0] sample+scan, [1] E-step kernel, [2] sstats (sort + segmented SpMM), [3] all-reduce,
+ * [4] M-step (λ update + expElogβ).  Requires stc_lda_enable_timing(lda, 1) beforehand.    */
+int stc_lda_enable_timing(stc_lda* lda, int on);
+/* cumulative since creation: [0] batch docs, [1] batch entries, [2] Σ inner E-step iterations,
+ * [3] docs stopped by max_inner_iter                                                         */
+int stc_lda_counters(stc_lda* lda, int64_t out[4]);
+int stc_lda_phase_times(stc_lda* lda, double* ms_out /* 5 */, int64_t* steps_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STC_H_ */

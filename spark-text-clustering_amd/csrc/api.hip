@@ -1,0 +1,1110 @@
+// api.hip — the C ABI of libstc.so (include/stc.h): contexts, device CSR, HashingTF/IDF entry
+// points, and the online-LDA driver (one submitMiniBatch per stc_lda_step / stc_lda_next).
+//
+// Host-side control flow mirrors [U] OnlineLDAOptimizer.submitMiniBatch (spark-mllib 2.4.3):
+//   iteration += 1 → E-step over the batch (K6) → stat (K sstats) → treeReduce ≙ RCCL all-reduce
+//   → batchResult = stat ⊙ expElogβ, updateLambda (K7) → expElogβ (K8) → updateAlpha.
+// One host sync per step (to size the sort for the batch's entry count); everything else is
+// stream-ordered on the context's HIP stream.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <memory>
+
+#include "lda_kernels.h"
+
+namespace stc {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+
+}  // namespace stc
+
+using namespace stc;
+
+struct stc_ctx : Ctx {};
+struct stc_dcsr : DCsr {};
+
+// ---------------------------------------------------------------------------------------
+// LDA state
+// ---------------------------------------------------------------------------------------
+struct stc_lda {
+  Ctx* ctx = nullptr;
+  stc_lda_config cfg{};
+  int k = 0, kp = 0, P = 0, lds_rows = 0;
+  int64_t V = 0;
+  int dtype = STC_F32;
+  size_t tsize = 4;
+  double eta = 0.0;
+  int64_t iteration = 0;
+  const DCsr* corpus = nullptr;
+  int64_t corpus_total = 0;
+  bool has_topics = false;
+  int64_t nblocks_m = 0;
+
+  DevBuf lam, Bp, logscale, colsum, colpart, alpha, small, scal;
+  DevBuf batch, bptr, bnnz, g0, gamma, eth, elogth, iters, nonempty, r, keys, vals, skeys, svals,
+      edoc, stat, headbuf, tailbuf, sort_tmp, scan_tmp, stats4, cum2, bound, dtmp;
+  DevBuf s_counts, s_weights, s_cincl, s_wincl;
+
+  bool timing = false;
+  hipEvent_t ev[2][6] = {};
+  int ev_set = 0;
+  bool ev_pending[2] = {false, false};
+  double acc_ms[5] = {0, 0, 0, 0, 0};
+  int64_t timed_steps = 0;
+  int64_t cum_docs = 0, cum_entries = 0;
+
+  ~stc_lda() {
+    for (auto& s : ev)
+      for (auto& e : s)
+        if (e) (void)hipEventDestroy(e);
+  }
+};
+
+namespace {
+
+template <typename T>
+struct RcclType;
+template <>
+struct RcclType<float> {
+  static constexpr ncclDataType_t v = ncclFloat32;
+};
+template <>
+struct RcclType<double> {
+  static constexpr ncclDataType_t v = ncclFloat64;
+};
+
+inline int bits_for(int64_t n) {
+  int b = 1;
+  while ((int64_t(1) << b) < n) ++b;
+  return b;
+}
+
+void record(stc_lda& L, int slot) {
+  if (L.timing) HIP_CHECK(hipEventRecord(L.ev[L.ev_set][slot], L.ctx->stream));
+}
+
+// add the phase times of an event set whose step is known to have completed
+void harvest(stc_lda& L, int set) {
+  if (!L.ev_pending[set]) return;
+  for (int p = 0; p < 5; ++p) {
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, L.ev[set][p], L.ev[set][p + 1]));
+    L.acc_ms[p] += ms;
+  }
+  L.timed_steps += 1;
+  L.ev_pending[set] = false;
+}
+
+template <typename T>
+void refresh_model(stc_lda& L) {
+  hipStream_t s = L.ctx->stream;
+  lda::launch_colsum_lambda(s, L.lam.as<double>(), L.V, L.k, L.colpart.as<double>(), L.nblocks_m);
+  lda::launch_colsum_reduce(s, L.colpart.as<double>(), L.nblocks_m, L.k, nullptr, L.colsum.as<double>());
+  lda::launch_expelogbeta<T>(s, L.lam.as<double>(), L.colsum.as<double>(), L.V, L.k, L.kp, nullptr,
+                             L.Bp.as<T>(), L.logscale.as<double>());
+  L.has_topics = true;
+}
+
+void refresh(stc_lda& L) {
+  if (L.dtype == STC_F32) refresh_model<float>(L);
+  else refresh_model<double>(L);
+}
+
+template <typename T>
+void ensure_batch(stc_lda& L, int64_t n, int64_t E) {
+  const size_t ts = sizeof(T);
+  L.batch.reserve(4 * (n + 1));
+  L.bptr.reserve(8 * (n + 1));
+  L.bnnz.reserve(8 * (n + 1));
+  L.gamma.reserve(ts * n * L.k);
+  L.eth.reserve(ts * n * L.kp);
+  L.elogth.reserve(ts * n * L.k);
+  L.iters.reserve(4 * n);
+  L.nonempty.reserve(4 * n);
+  L.r.reserve(ts * E);
+  L.keys.reserve(4 * E);
+  L.vals.reserve(4 * E);
+  L.skeys.reserve(4 * E);
+  L.svals.reserve(4 * E);
+  L.edoc.reserve(4 * E);
+  const int64_t nchunks = ceil_div(E, lda::kChunk) + 1;
+  L.headbuf.reserve(ts * nchunks * L.kp);
+  L.tailbuf.reserve(ts * nchunks * L.kp);
+  size_t tb = 0;
+  HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, L.keys.as<uint32_t>(), L.skeys.as<uint32_t>(),
+                                               L.vals.as<uint32_t>(), L.svals.as<uint32_t>(),
+                                               (int)std::max<int64_t>(E, 1), 0, bits_for(L.V),
+                                               L.ctx->stream));
+  L.sort_tmp.reserve(tb);
+  size_t sb = 0;
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, sb, L.bnnz.as<int64_t>(), L.bptr.as<int64_t>() + 1,
+                                             (int)std::max<int64_t>(n, 1), L.ctx->stream));
+  L.scan_tmp.reserve(sb);
+}
+
+// entry offsets of the batch members: bptr[0] = 0, bptr[i+1] = Σ nnz; returns E (syncs)
+int64_t batch_offsets(stc_lda& L, int64_t n) {
+  hipStream_t s = L.ctx->stream;
+  HIP_CHECK(hipMemsetAsync(L.bptr.p, 0, sizeof(int64_t), s));
+  if (n == 0) return 0;
+  lda::launch_batch_nnz(s, L.corpus->indptr.as<int64_t>(), L.batch.as<int32_t>(), n, L.bnnz.as<int64_t>());
+  size_t sb = 0;
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, sb, L.bnnz.as<int64_t>(), L.bptr.as<int64_t>() + 1,
+                                             (int)n, s));
+  L.scan_tmp.reserve(sb);
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(L.scan_tmp.p, sb, L.bnnz.as<int64_t>(),
+                                             L.bptr.as<int64_t>() + 1, (int)n, s));
+  int64_t E = 0;
+  HIP_CHECK(hipMemcpyAsync(&E, L.bptr.as<int64_t>() + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return E;
+}
+
+template <typename T>
+lda::EStepArgs<T> estep_args(stc_lda& L) {
+  lda::EStepArgs<T> a;
+  a.k = L.k;
+  a.kp = L.kp;
+  a.P = L.P;
+  a.lds_rows = L.lds_rows;
+  a.Bp = L.Bp.as<T>();
+  a.logscale = L.logscale.as<double>();
+  a.alpha = L.alpha.as<double>();
+  a.seed = L.cfg.seed;
+  a.rank = L.ctx->rank;
+  a.gamma_shape = L.cfg.gamma_shape;
+  a.max_iter = L.cfg.max_inner_iter;
+  return a;
+}
+
+template <typename T>
+const T* upload_gamma0(stc_lda& L, const double* gamma0, int64_t n) {
+  if (!gamma0 || n == 0) return nullptr;
+  std::vector<T> h((size_t)(n * L.k));
+  for (size_t j = 0; j < h.size(); ++j) {
+    STC_REQUIRE(gamma0[j] > 0.0, "gamma0 entries must be > 0");
+    h[j] = (T)gamma0[j];
+  }
+  L.g0.reserve(sizeof(T) * h.size());
+  HIP_CHECK(hipMemcpyAsync(L.g0.p, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice, L.ctx->stream));
+  HIP_CHECK(hipStreamSynchronize(L.ctx->stream));  // h dies at scope exit
+  return L.g0.as<T>();
+}
+
+// E-step over the n batch members already in L.batch / L.bptr, then the term-sorted sstats SpMM
+// into L.stat (V×kp, row-scaled) and logphat/non-empty count into L.small.
+template <typename T>
+void estep_and_stats(stc_lda& L, int64_t n, int64_t E, const T* g0, int64_t iteration) {
+  hipStream_t s = L.ctx->stream;
+  lda::EStepArgs<T> a = estep_args<T>(L);
+  a.indptr = L.corpus->indptr.as<int64_t>();
+  a.indices = L.corpus->indices.as<int32_t>();
+  a.values = L.corpus->values.as<T>();
+  a.batch = L.batch.as<int32_t>();
+  a.n = n;
+  a.bptr = L.bptr.as<int64_t>();
+  a.gamma0 = g0;
+  a.iteration = iteration;
+  a.key_mode = 0;
+  a.gamma = L.gamma.as<T>();
+  a.eth = L.eth.as<T>();
+  a.elogth = L.elogth.as<T>();
+  a.r = L.r.as<T>();
+  a.keys = L.keys.as<uint32_t>();
+  a.vals = L.vals.as<uint32_t>();
+  a.edoc = L.edoc.as<int32_t>();
+  a.iters = L.iters.as<int32_t>();
+  a.nonempty = L.nonempty.as<int32_t>();
+  record(L, 1);
+  lda::launch_estep<T>(s, a, true, false);
+  record(L, 2);
+  HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.V * L.kp, s));
+  if (E > 0) {
+    size_t tb = L.sort_tmp.bytes;
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(L.sort_tmp.p, tb, L.keys.as<uint32_t>(),
+                                                 L.skeys.as<uint32_t>(), L.vals.as<uint32_t>(),
+                                                 L.svals.as<uint32_t>(), (int)E, 0, bits_for(L.V), s));
+    lda::launch_sstats<T>(s, L.skeys.as<uint32_t>(), L.svals.as<uint32_t>(), E, L.r.as<T>(),
+                          L.edoc.as<int32_t>(), L.eth.as<T>(), L.kp, L.stat.as<T>(),
+                          L.headbuf.as<T>(), L.tailbuf.as<T>());
+  }
+  if (n > 0) {
+    lda::launch_logphat<T>(s, L.elogth.as<T>(), L.nonempty.as<int32_t>(), n, L.k, L.small.as<double>());
+    lda::launch_iter_stats(s, L.iters.as<int32_t>(), L.nonempty.as<int32_t>(), n, L.cfg.max_inner_iter,
+                           L.stats4.as<int64_t>(), L.cum2.as<int64_t>());
+  } else {
+    HIP_CHECK(hipMemsetAsync(L.small.p, 0, sizeof(double) * (L.k + 1), s));
+    HIP_CHECK(hipMemsetAsync(L.stats4.p, 0, sizeof(int64_t) * 4, s));
+  }
+  record(L, 3);
+}
+
+template <typename T>
+void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
+  Ctx& c = *L.ctx;
+  hipStream_t s = c.stream;
+  if (c.comm) {  // treeReduce(elementWiseSum) ≙ one grouped RCCL all-reduce over xGMI
+    RCCL_CHECK(ncclGroupStart());
+    RCCL_CHECK(ncclAllReduce(L.stat.p, L.stat.p, (size_t)(L.V * L.kp), RcclType<T>::v, ncclSum, c.comm, s));
+    RCCL_CHECK(ncclAllReduce(L.small.p, L.small.p, (size_t)(L.k + 1), ncclFloat64, ncclSum, c.comm, s));
+    RCCL_CHECK(ncclGroupEnd());
+  }
+  record(L, 4);
+  L.iteration += 1;
+  const double rho = std::pow(L.cfg.tau0 + (double)L.iteration, -L.cfg.kappa);
+  const double batch_size = std::ceil(L.cfg.mini_batch_fraction * (double)L.corpus_total);
+  const double scale = (double)L.corpus_total / batch_size;
+  const double* gate = L.small.as<double>() + L.k;
+  lda::launch_lambda_update<T>(s, L.lam.as<double>(), L.stat.as<T>(), L.Bp.as<T>(), L.V, L.k, L.kp,
+                               rho, scale, L.eta, gate, L.colpart.as<double>(), L.nblocks_m);
+  lda::launch_colsum_reduce(s, L.colpart.as<double>(), L.nblocks_m, L.k, gate, L.colsum.as<double>());
+  lda::launch_expelogbeta<T>(s, L.lam.as<double>(), L.colsum.as<double>(), L.V, L.k, L.kp, gate,
+                             L.Bp.as<T>(), L.logscale.as<double>());
+  if (L.cfg.optimize_doc_concentration)
+    lda::launch_update_alpha(s, L.alpha.as<double>(), L.small.as<double>(), L.k, rho);
+  record(L, 5);
+  if (L.timing) {
+    L.ev_pending[L.ev_set] = true;
+    L.ev_set ^= 1;
+  }
+  L.cum_docs += n;
+  L.cum_entries += E;
+  if (st) {
+    int64_t h4[4] = {0, 0, 0, 0};
+    double ne = 0.0;
+    HIP_CHECK(hipMemcpyAsync(h4, L.stats4.p, sizeof(h4), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(&ne, L.small.as<double>() + L.k, sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    st->batch_docs = n;
+    st->batch_entries = E;
+    st->inner_iters = h4[0];
+    st->inner_iters_max = (int32_t)h4[1];
+    st->cap_hits = (int32_t)h4[2];
+    st->nonempty_docs = (int64_t)ne;
+    st->rho = rho;
+  }
+}
+
+void require_ready(stc_lda& L) {
+  if (!L.corpus) throw Error(STC_ERR_STATE, "no corpus: call stc_lda_set_corpus first");
+  if (!L.has_topics) throw Error(STC_ERR_STATE, "no topics: call stc_lda_init_random or stc_lda_set_topics");
+}
+
+template <typename T>
+void step_ids(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, stc_step_stats* st) {
+  require_ready(L);
+  Ctx& c = *L.ctx;
+  std::vector<int32_t> h((size_t)n);
+  for (int64_t i = 0; i < n; ++i) {
+    STC_REQUIRE(ids[i] >= 0 && ids[i] < L.corpus->rows, "batch doc id out of range");
+    h[(size_t)i] = (int32_t)ids[i];
+  }
+  ensure_batch<T>(L, n, 0);
+  record(L, 0);
+  if (n > 0)
+    HIP_CHECK(hipMemcpyAsync(L.batch.p, h.data(), 4 * n, hipMemcpyHostToDevice, c.stream));
+  const int64_t E = batch_offsets(L, n);  // syncs (h may die after)
+  if (L.timing) harvest(L, L.ev_set ^ 1);  // the previous step has completed (stream order)
+  ensure_batch<T>(L, n, E);
+  const T* g0 = upload_gamma0<T>(L, gamma0, n);
+  estep_and_stats<T>(L, n, E, g0, L.iteration + 1);
+  train_tail<T>(L, n, E, st);
+}
+
+template <typename T>
+void next_impl(stc_lda& L, stc_step_stats* st) {
+  require_ready(L);
+  Ctx& c = *L.ctx;
+  hipStream_t s = c.stream;
+  const int64_t D = L.corpus->rows;
+  L.s_counts.reserve(4 * D);
+  L.s_weights.reserve(8 * D);
+  L.s_cincl.reserve(4 * D);
+  L.s_wincl.reserve(8 * D);
+  const int64_t it = L.iteration + 1;
+  record(L, 0);
+  lda::launch_sample(s, L.corpus->indptr.as<int64_t>(), D, L.cfg.mini_batch_fraction,
+                     L.cfg.sample_with_replacement, L.cfg.seed, it, c.rank, L.s_counts.as<int32_t>(),
+                     L.s_weights.as<int64_t>());
+  size_t b1 = 0, b2 = 0;
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, b1, L.s_counts.as<int32_t>(), L.s_cincl.as<int32_t>(), (int)D, s));
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, b2, L.s_weights.as<int64_t>(), L.s_wincl.as<int64_t>(), (int)D, s));
+  L.scan_tmp.reserve(std::max(b1, b2));
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(L.scan_tmp.p, b1, L.s_counts.as<int32_t>(), L.s_cincl.as<int32_t>(), (int)D, s));
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(L.scan_tmp.p, b2, L.s_weights.as<int64_t>(), L.s_wincl.as<int64_t>(), (int)D, s));
+  int32_t n32 = 0;
+  int64_t E = 0;
+  HIP_CHECK(hipMemcpyAsync(&n32, L.s_cincl.as<int32_t>() + (D - 1), 4, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(&E, L.s_wincl.as<int64_t>() + (D - 1), 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  if (L.timing) {  // the previous step's events have completed (stream order)
+    harvest(L, L.ev_set ^ 1);
+  }
+  const int64_t n = n32;
+  ensure_batch<T>(L, n, E);
+  if (n > 0)
+    lda::launch_fill_batch(s, L.corpus->indptr.as<int64_t>(), D, L.s_counts.as<int32_t>(),
+                           L.s_cincl.as<int32_t>(), L.s_wincl.as<int64_t>(), L.batch.as<int32_t>(),
+                           L.bptr.as<int64_t>());
+  HIP_CHECK(hipMemcpyAsync(L.bptr.as<int64_t>() + n, &E, 8, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipStreamSynchronize(s));  // &E is a stack value
+  // Spark's next(): `if (batch.isEmpty()) return this` — no iteration increment
+  if (n == 0) {
+    if (st) *st = stc_step_stats{};
+    return;
+  }
+  estep_and_stats<T>(L, n, E, nullptr, it);
+  train_tail<T>(L, n, E, st);
+}
+
+template <typename T>
+void estep_only(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, double* gamma_out,
+                double* stat_out, int32_t* iters_out) {
+  require_ready(L);
+  Ctx& c = *L.ctx;
+  hipStream_t s = c.stream;
+  std::vector<int32_t> h((size_t)n);
+  for (int64_t i = 0; i < n; ++i) {
+    STC_REQUIRE(ids[i] >= 0 && ids[i] < L.corpus->rows, "batch doc id out of range");
+    h[(size_t)i] = (int32_t)ids[i];
+  }
+  ensure_batch<T>(L, n, 0);
+  if (n > 0) HIP_CHECK(hipMemcpyAsync(L.batch.p, h.data(), 4 * n, hipMemcpyHostToDevice, s));
+  const int64_t E = batch_offsets(L, n);
+  ensure_batch<T>(L, n, E);
+  const T* g0 = upload_gamma0<T>(L, gamma0, n);
+  const bool t = L.timing;
+  L.timing = false;
+  estep_and_stats<T>(L, n, E, g0, L.iteration + 1);
+  L.timing = t;
+  if (gamma_out && n > 0) {
+    std::vector<T> g((size_t)(n * L.k));
+    HIP_CHECK(hipMemcpyAsync(g.data(), L.gamma.p, sizeof(T) * g.size(), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    for (size_t j = 0; j < g.size(); ++j) gamma_out[j] = (double)g[j];
+  }
+  if (iters_out && n > 0) {
+    HIP_CHECK(hipMemcpyAsync(iters_out, L.iters.p, 4 * n, hipMemcpyDeviceToHost, s));
+  }
+  if (stat_out) {
+    L.dtmp.reserve(sizeof(double) * L.V * L.k);
+    lda::launch_unscale_stat<T>(s, L.stat.as<T>(), L.logscale.as<double>(), L.V, L.k, L.kp, L.dtmp.as<double>());
+    HIP_CHECK(hipMemcpyAsync(stat_out, L.dtmp.p, sizeof(double) * L.V * L.k, hipMemcpyDeviceToHost, s));
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+}
+
+template <typename T>
+void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const double* gamma0,
+                bool bound, double* gamma_out, double* out4 /* corpus, tokens */) {
+  if (!L.has_topics) throw Error(STC_ERR_STATE, "no topics: call stc_lda_init_random or stc_lda_set_topics");
+  STC_REQUIRE(docs.cols == L.V, "document vectors must have vocab_size columns");
+  STC_REQUIRE(docs.dtype == L.dtype, "document CSR dtype must match the LDA dtype");
+  hipStream_t s = L.ctx->stream;
+  const int64_t n = docs.rows;
+  L.r.reserve(sizeof(T) * std::max<int64_t>(docs.nnz, 1));
+  L.gamma.reserve(sizeof(T) * n * L.k);
+  L.bound.reserve(sizeof(double) * std::max<int64_t>(n, 1));
+  L.iters.reserve(4 * n);
+  L.scal.reserve(sizeof(double) * 8);
+  const T* g0 = upload_gamma0<T>(L, gamma0, n);
+  lda::EStepArgs<T> a = estep_args<T>(L);
+  a.indptr = docs.indptr.as<int64_t>();
+  a.indices = docs.indices.as<int32_t>();
+  a.values = docs.values.as<T>();
+  a.batch = nullptr;
+  a.n = n;
+  a.bptr = docs.indptr.as<int64_t>();
+  a.gamma0 = g0;
+  a.seed = seed;
+  a.key_mode = 1;
+  a.doc_id_base = base;
+  a.r = L.r.as<T>();
+  a.gamma = gamma_out ? L.gamma.as<T>() : nullptr;
+  a.iters = L.iters.as<int32_t>();
+  a.bound = bound ? L.bound.as<double>() : nullptr;
+  lda::launch_estep<T>(s, a, false, bound);
+  if (gamma_out && n > 0) {
+    std::vector<T> g((size_t)(n * L.k));
+    HIP_CHECK(hipMemcpyAsync(g.data(), L.gamma.p, sizeof(T) * g.size(), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    for (size_t j = 0; j < g.size(); ++j) gamma_out[j] = (double)g[j];
+  }
+  if (bound) {
+    double h[3] = {0, 0, 0};
+    HIP_CHECK(hipMemsetAsync(L.scal.p, 0, sizeof(double) * 3, s));
+    if (n > 0) lda::launch_sum_f64(s, L.bound.as<double>(), n, L.scal.as<double>());
+    if (docs.nnz > 0) lda::launch_sum_vals<T>(s, docs.values.as<T>(), docs.nnz, L.scal.as<double>() + 1);
+    HIP_CHECK(hipMemcpyAsync(h, L.scal.p, sizeof(double) * 2, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    out4[0] = h[0];
+    out4[1] = h[1];
+  }
+}
+
+template <typename T>
+double topics_part(stc_lda& L) {
+  hipStream_t s = L.ctx->stream;
+  const int64_t nb = 1024;
+  L.dtmp.reserve(sizeof(double) * (nb + 1));
+  L.scal.reserve(sizeof(double) * 8);
+  lda::launch_topics_bound<T>(s, L.lam.as<double>(), L.colsum.as<double>(), L.V, L.k, L.eta,
+                              L.dtmp.as<double>(), nb);
+  lda::launch_sum_f64(s, L.dtmp.as<double>(), nb, L.scal.as<double>() + 3);
+  double part = 0.0;
+  std::vector<double> cs((size_t)L.k);
+  HIP_CHECK(hipMemcpyAsync(&part, L.scal.as<double>() + 3, sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(cs.data(), L.colsum.p, sizeof(double) * L.k, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  const double lg_sum_eta = std::lgamma(L.eta * (double)L.V);
+  for (int t = 0; t < L.k; ++t) part += std::lgamma(cs[(size_t)t]) - lg_sum_eta;
+  return part;
+}
+
+void allreduce_host(Ctx& c, double* x, int64_t n) {
+  if (!c.comm || n == 0) return;
+  DevBuf d;
+  d.reserve(sizeof(double) * n);
+  HIP_CHECK(hipMemcpyAsync(d.p, x, sizeof(double) * n, hipMemcpyHostToDevice, c.stream));
+  RCCL_CHECK(ncclAllReduce(d.p, d.p, (size_t)n, ncclFloat64, ncclSum, c.comm, c.stream));
+  HIP_CHECK(hipMemcpyAsync(x, d.p, sizeof(double) * n, hipMemcpyDeviceToHost, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+}
+
+void check_csr_host(int64_t rows, int64_t cols, const int64_t* indptr, const int32_t* indices) {
+  STC_REQUIRE(rows >= 0 && cols > 0, "csr: rows >= 0 and cols > 0");
+  STC_REQUIRE(cols <= (int64_t(1) << 31), "csr: at most 2^31 columns");
+  STC_REQUIRE(indptr[0] == 0, "csr: indptr[0] must be 0");
+  for (int64_t r = 0; r < rows; ++r) STC_REQUIRE(indptr[r + 1] >= indptr[r], "csr: indptr must be non-decreasing");
+  const int64_t nnz = indptr[rows];
+  for (int64_t e = 0; e < nnz; ++e)
+    STC_REQUIRE(indices[e] >= 0 && (int64_t)indices[e] < cols, "csr: column index out of range");
+}
+
+}  // namespace
+
+// =======================================================================================
+// C ABI
+// =======================================================================================
+extern "C" {
+
+const char* stc_last_error(void) { return stc::g_last_error.c_str(); }
+int stc_abi_version(void) { return STC_ABI_VERSION; }
+
+int stc_device_count(int* n_out) {
+  return guard([&] {
+    STC_REQUIRE(n_out, "n_out");
+    int n = 0;
+    HIP_CHECK(hipGetDeviceCount(&n));
+    *n_out = n;
+  });
+}
+
+int stc_init(int device, stc_ctx** out) {
+  return guard([&] {
+    STC_REQUIRE(out, "out");
+    int n = 0;
+    HIP_CHECK(hipGetDeviceCount(&n));
+    STC_REQUIRE(device >= 0 && device < n, "device index out of range");
+    auto c = std::make_unique<stc_ctx>();
+    c->device = device;
+    HIP_CHECK(hipSetDevice(device));
+    HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    *out = c.release();
+  });
+}
+
+int stc_destroy(stc_ctx* ctx) {
+  return guard([&] {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+  });
+}
+
+int stc_synchronize(stc_ctx* ctx) {
+  return guard([&] {
+    STC_REQUIRE(ctx, "ctx");
+    ctx->use();
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int stc_comm_unique_id(uint8_t id_out[128]) {
+  return guard([&] {
+    STC_REQUIRE(id_out, "id_out");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    RCCL_CHECK(ncclGetUniqueId(&id));
+    std::memcpy(id_out, &id, 128);
+  });
+}
+
+int stc_comm_init(stc_ctx* ctx, const uint8_t id[128], int n_ranks, int rank) {
+  return guard([&] {
+    STC_REQUIRE(ctx && id, "ctx/id");
+    STC_REQUIRE(n_ranks >= 1 && rank >= 0 && rank < n_ranks, "rank / n_ranks");
+    STC_REQUIRE(!ctx->comm, "communicator already initialised");
+    ctx->use();
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, 128);
+    RCCL_CHECK(ncclCommInitRank(&ctx->comm, n_ranks, uid, rank));
+    ctx->n_ranks = n_ranks;
+    ctx->rank = rank;
+  });
+}
+
+int stc_comm_allreduce_f64(stc_ctx* ctx, double* host_inout, int64_t n) {
+  return guard([&] {
+    STC_REQUIRE(ctx && (host_inout || n == 0), "ctx/host_inout");
+    ctx->use();
+    allreduce_host(*ctx, host_inout, n);
+  });
+}
+
+int stc_dcsr_upload(stc_ctx* ctx, int64_t n_rows, int64_t n_cols, const int64_t* indptr,
+                    const int32_t* indices, const double* values, int value_dtype, stc_dcsr** out) {
+  return guard([&] {
+    STC_REQUIRE(ctx && indptr && out, "ctx/indptr/out");
+    STC_REQUIRE(value_dtype == STC_F32 || value_dtype == STC_F64, "value_dtype");
+    const int64_t nnz = indptr[n_rows];
+    STC_REQUIRE(nnz == 0 || (indices && values), "indices/values");
+    check_csr_host(n_rows, n_cols, indptr, indices);
+    ctx->use();
+    auto m = std::make_unique<stc_dcsr>();
+    m->ctx = ctx;
+    m->rows = n_rows;
+    m->cols = n_cols;
+    m->nnz = nnz;
+    m->dtype = value_dtype;
+    m->indptr.reserve(8 * (n_rows + 1));
+    m->indices.reserve(4 * std::max<int64_t>(nnz, 1));
+    m->values.reserve((value_dtype == STC_F32 ? 4 : 8) * std::max<int64_t>(nnz, 1));
+    HIP_CHECK(hipMemcpyAsync(m->indptr.p, indptr, 8 * (n_rows + 1), hipMemcpyHostToDevice, ctx->stream));
+    if (nnz > 0) {
+      HIP_CHECK(hipMemcpyAsync(m->indices.p, indices, 4 * nnz, hipMemcpyHostToDevice, ctx->stream));
+      if (value_dtype == STC_F64) {
+        HIP_CHECK(hipMemcpyAsync(m->values.p, values, 8 * nnz, hipMemcpyHostToDevice, ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      } else {
+        std::vector<float> f((size_t)nnz);
+        for (int64_t e = 0; e < nnz; ++e) f[(size_t)e] = (float)values[e];
+        HIP_CHECK(hipMemcpyAsync(m->values.p, f.data(), 4 * nnz, hipMemcpyHostToDevice, ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      }
+    }
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    *out = m.release();
+  });
+}
+
+int stc_dcsr_shape(const stc_dcsr* m, int64_t* n_rows, int64_t* n_cols, int64_t* nnz) {
+  return guard([&] {
+    STC_REQUIRE(m, "m");
+    if (n_rows) *n_rows = m->rows;
+    if (n_cols) *n_cols = m->cols;
+    if (nnz) *nnz = m->nnz;
+  });
+}
+
+int stc_dcsr_download(stc_ctx* ctx, const stc_dcsr* m, int64_t* indptr, int32_t* indices, double* values) {
+  return guard([&] {
+    STC_REQUIRE(ctx && m, "ctx/m");
+    ctx->use();
+    hipStream_t s = ctx->stream;
+    if (indptr) HIP_CHECK(hipMemcpyAsync(indptr, m->indptr.p, 8 * (m->rows + 1), hipMemcpyDeviceToHost, s));
+    if (indices && m->nnz) HIP_CHECK(hipMemcpyAsync(indices, m->indices.p, 4 * m->nnz, hipMemcpyDeviceToHost, s));
+    if (values && m->nnz) {
+      if (m->dtype == STC_F64) {
+        HIP_CHECK(hipMemcpyAsync(values, m->values.p, 8 * m->nnz, hipMemcpyDeviceToHost, s));
+      } else {
+        std::vector<float> f((size_t)m->nnz);
+        HIP_CHECK(hipMemcpyAsync(f.data(), m->values.p, 4 * m->nnz, hipMemcpyDeviceToHost, s));
+        HIP_CHECK(hipStreamSynchronize(s));
+        for (int64_t e = 0; e < m->nnz; ++e) values[e] = f[(size_t)e];
+      }
+    }
+    HIP_CHECK(hipStreamSynchronize(s));
+  });
+}
+
+int stc_dcsr_free(stc_dcsr* m) {
+  return guard([&] {
+    if (!m) return;
+    if (m->ctx) (void)hipSetDevice(m->ctx->device);
+    delete m;
+  });
+}
+
+// ---- HashingTF ------------------------------------------------------------------------
+namespace {
+struct TokenUpload {
+  DevBuf utf8, tok_off, doc_off;
+};
+void upload_tokens(Ctx& c, TokenUpload& u, const uint8_t* utf8, int64_t n_bytes, const int64_t* tok_off,
+                   int64_t n_tok, const int64_t* doc_off, int64_t n_docs) {
+  STC_REQUIRE(n_bytes >= 0 && n_tok >= 0 && n_docs >= 0, "sizes must be >= 0");
+  STC_REQUIRE(tok_off && (n_bytes == 0 || utf8), "utf8/tok_off");
+  STC_REQUIRE(tok_off[0] == 0 && tok_off[n_tok] <= n_bytes, "tok_off must start at 0 and stay within n_bytes");
+  for (int64_t t = 0; t < n_tok; ++t) STC_REQUIRE(tok_off[t + 1] >= tok_off[t], "tok_off must be non-decreasing");
+  if (doc_off) {
+    STC_REQUIRE(doc_off[0] == 0 && doc_off[n_docs] == n_tok, "doc_off must span [0, n_tok]");
+    for (int64_t d = 0; d < n_docs; ++d) STC_REQUIRE(doc_off[d + 1] >= doc_off[d], "doc_off must be non-decreasing");
+  }
+  u.utf8.reserve(std::max<int64_t>(n_bytes, 1));
+  u.tok_off.reserve(8 * (n_tok + 1));
+  if (n_bytes) HIP_CHECK(hipMemcpyAsync(u.utf8.p, utf8, n_bytes, hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemcpyAsync(u.tok_off.p, tok_off, 8 * (n_tok + 1), hipMemcpyHostToDevice, c.stream));
+  if (doc_off) {
+    u.doc_off.reserve(8 * (n_docs + 1));
+    HIP_CHECK(hipMemcpyAsync(u.doc_off.p, doc_off, 8 * (n_docs + 1), hipMemcpyHostToDevice, c.stream));
+  }
+}
+}  // namespace
+
+int stc_hash_tokens(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int64_t* tok_off,
+                    int64_t n_tok, int32_t num_features, int hash_variant, int32_t* idx_out) {
+  return guard([&] {
+    STC_REQUIRE(ctx && (idx_out || n_tok == 0), "ctx/idx_out");
+    STC_REQUIRE(num_features > 0, "numFeatures must be > 0");
+    STC_REQUIRE(hash_variant == STC_HASH_STANDARD || hash_variant == STC_HASH_SPARK24, "hash_variant");
+    ctx->use();
+    TokenUpload u;
+    upload_tokens(*ctx, u, utf8, n_bytes, tok_off, n_tok, nullptr, 0);
+    DevBuf out;
+    out.reserve(4 * std::max<int64_t>(n_tok, 1));
+    hashing::hash_tokens(*ctx, u.utf8.as<uint8_t>(), u.tok_off.as<int64_t>(), n_tok, num_features,
+                         hash_variant, out.as<int32_t>());
+    if (n_tok) HIP_CHECK(hipMemcpyAsync(idx_out, out.p, 4 * n_tok, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int stc_hashing_tf_dev(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int64_t* tok_off,
+                       int64_t n_tok, const int64_t* doc_off, int64_t n_docs, int32_t num_features,
+                       int binary, int hash_variant, int value_dtype, stc_dcsr** out) {
+  return guard([&] {
+    STC_REQUIRE(ctx && doc_off && out, "ctx/doc_off/out");
+    STC_REQUIRE(num_features > 0, "numFeatures must be > 0");
+    STC_REQUIRE(hash_variant == STC_HASH_STANDARD || hash_variant == STC_HASH_SPARK24, "hash_variant");
+    STC_REQUIRE(value_dtype == STC_F32 || value_dtype == STC_F64, "value_dtype");
+    ctx->use();
+    TokenUpload u;
+    upload_tokens(*ctx, u, utf8, n_bytes, tok_off, n_tok, doc_off, n_docs);
+    auto m = std::make_unique<stc_dcsr>();
+    m->ctx = ctx;
+    hashing::build_csr(*ctx, u.utf8.as<uint8_t>(), u.tok_off.as<int64_t>(), n_tok, u.doc_off.as<int64_t>(),
+                       n_docs, num_features, binary, hash_variant, value_dtype, *m);
+    *out = m.release();
+  });
+}
+
+int stc_hashing_tf(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int64_t* tok_off,
+                   int64_t n_tok, const int64_t* doc_off, int64_t n_docs, int32_t num_features,
+                   int binary, int hash_variant, int64_t* indptr_out, int32_t* indices_out,
+                   double* values_out) {
+  stc_dcsr* m = nullptr;
+  int rc = stc_hashing_tf_dev(ctx, utf8, n_bytes, tok_off, n_tok, doc_off, n_docs, num_features,
+                              binary, hash_variant, STC_F64, &m);
+  if (rc != STC_OK) return rc;
+  rc = stc_dcsr_download(ctx, m, indptr_out, indices_out, values_out);
+  stc_dcsr_free(m);
+  return rc;
+}
+
+// ---- IDF --------------------------------------------------------------------------------
+int stc_idf_fit(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, double* idf_out,
+                int64_t* df_out, int64_t* m_out) {
+  return guard([&] {
+    STC_REQUIRE(ctx && tf && idf_out, "ctx/tf/idf_out");
+    STC_REQUIRE(min_doc_freq >= 0, "minDocFreq must be >= 0");
+    ctx->use();
+    hipStream_t s = ctx->stream;
+    DevBuf df, idf;
+    df.reserve(8 * tf->cols);
+    idf.reserve(8 * tf->cols);
+    idf::doc_freq(*ctx, *tf, df.as<int64_t>());
+    int64_t m = tf->rows;
+    if (ctx->comm) {  // DocumentFrequencyAggregator.merge over ranks
+      DevBuf mm;
+      mm.reserve(8);
+      HIP_CHECK(hipMemcpyAsync(mm.p, &m, 8, hipMemcpyHostToDevice, s));
+      RCCL_CHECK(ncclGroupStart());
+      RCCL_CHECK(ncclAllReduce(df.p, df.p, (size_t)tf->cols, ncclInt64, ncclSum, ctx->comm, s));
+      RCCL_CHECK(ncclAllReduce(mm.p, mm.p, 1, ncclInt64, ncclSum, ctx->comm, s));
+      RCCL_CHECK(ncclGroupEnd());
+      HIP_CHECK(hipMemcpyAsync(&m, mm.p, 8, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipStreamSynchronize(s));
+    }
+    idf::finalize(*ctx, df.as<int64_t>(), tf->cols, m, min_doc_freq, idf.as<double>());
+    HIP_CHECK(hipMemcpyAsync(idf_out, idf.p, 8 * tf->cols, hipMemcpyDeviceToHost, s));
+    if (df_out) HIP_CHECK(hipMemcpyAsync(df_out, df.p, 8 * tf->cols, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (m_out) *m_out = m;
+  });
+}
+
+int stc_idf_transform(stc_ctx* ctx, stc_dcsr* tf, const double* idf, double zero_floor) {
+  return guard([&] {
+    STC_REQUIRE(ctx && tf && idf, "ctx/tf/idf");
+    STC_REQUIRE(zero_floor >= 0.0, "zero_floor must be >= 0");
+    ctx->use();
+    DevBuf d;
+    d.reserve(8 * tf->cols);
+    HIP_CHECK(hipMemcpyAsync(d.p, idf, 8 * tf->cols, hipMemcpyHostToDevice, ctx->stream));
+    idf::transform(*ctx, *tf, d.as<double>(), zero_floor);
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+// ---- LDA ----------------------------------------------------------------------------------
+void stc_lda_config_default(stc_lda_config* c) {
+  if (!c) return;
+  *c = stc_lda_config{};
+  c->k = 10;
+  c->vocab_size = 1 << 18;
+  c->doc_concentration = nullptr;
+  c->doc_concentration_len = 0;
+  c->topic_concentration = -1.0;
+  c->tau0 = 1024.0;
+  c->kappa = 0.51;
+  c->mini_batch_fraction = 0.05;
+  c->gamma_shape = 100.0;
+  c->optimize_doc_concentration = 1;
+  c->sample_with_replacement = 1;
+  c->seed = 0;
+  c->dtype = STC_F32;
+  c->max_inner_iter = 0;
+}
+
+int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
+  return guard([&] {
+    STC_REQUIRE(ctx && cfg && out, "ctx/cfg/out");
+    // [U] LDA / OnlineLDAOptimizer setter validation
+    STC_REQUIRE(cfg->k > 1, "LDA k (number of clusters) must be > 1");
+    STC_REQUIRE(cfg->k <= 4096, "k <= 4096");
+    STC_REQUIRE(cfg->vocab_size > 0 && cfg->vocab_size <= (int64_t(1) << 31), "vocab_size in (0, 2^31]");
+    STC_REQUIRE(cfg->tau0 > 0, "LDA tau0 must be positive");
+    STC_REQUIRE(cfg->kappa > 0, "LDA kappa must be positive");
+    STC_REQUIRE(cfg->mini_batch_fraction > 0.0 && cfg->mini_batch_fraction <= 1.0,
+                "miniBatchFraction must be in range (0,1]");
+    STC_REQUIRE(cfg->gamma_shape > 1.0 / 3.0, "gammaShape must be > 1/3");
+    STC_REQUIRE(cfg->dtype == STC_F32 || cfg->dtype == STC_F64, "dtype");
+    STC_REQUIRE(cfg->max_inner_iter >= 0, "max_inner_iter must be >= 0");
+    ctx->use();
+    auto L = std::make_unique<stc_lda>();
+    L->ctx = ctx;
+    L->cfg = *cfg;
+    if (L->cfg.max_inner_iter == 0) L->cfg.max_inner_iter = 100000;
+    L->k = cfg->k;
+    L->V = cfg->vocab_size;
+    L->dtype = cfg->dtype;
+    L->tsize = cfg->dtype == STC_F32 ? 4 : 8;
+    const int W = cfg->dtype == STC_F32 ? 4 : 2;
+    L->kp = (int)ceil_div(L->k, W) * W;
+    L->P = ((L->kp / W) % 2 == 1) ? L->kp : L->kp + W;  // P/W odd: conflict-free b128 rows
+    L->lds_rows = cfg->dtype == STC_F32 ? lda::estep_lds_rows<float>(L->k, L->kp, L->P)
+                                        : lda::estep_lds_rows<double>(L->k, L->kp, L->P);
+    // α / η resolution ([U] OnlineLDAOptimizer.initialize)
+    std::vector<double> alpha((size_t)L->k);
+    const int alen = cfg->doc_concentration ? cfg->doc_concentration_len : 0;
+    if (alen == 0 || (alen == 1 && cfg->doc_concentration[0] == -1.0)) {
+      std::fill(alpha.begin(), alpha.end(), 1.0 / L->k);
+    } else if (alen == 1) {
+      STC_REQUIRE(cfg->doc_concentration[0] >= 0, "docConcentration must be >= 0");
+      std::fill(alpha.begin(), alpha.end(), cfg->doc_concentration[0]);
+    } else {
+      STC_REQUIRE(alen == L->k, "docConcentration must have length 1 or k");
+      for (int t = 0; t < L->k; ++t) {
+        STC_REQUIRE(cfg->doc_concentration[t] >= 0, "docConcentration entries must be >= 0");
+        alpha[(size_t)t] = cfg->doc_concentration[t];
+      }
+    }
+    if (cfg->topic_concentration == -1.0) L->eta = 1.0 / L->k;
+    else {
+      STC_REQUIRE(cfg->topic_concentration >= 0, "topicConcentration must be >= 0");
+      L->eta = cfg->topic_concentration;
+    }
+    L->cfg.doc_concentration = nullptr;
+    L->cfg.doc_concentration_len = 0;
+    L->nblocks_m = ceil_div(L->V, lda::kRowsPerBlock);
+    L->lam.reserve(8 * L->V * L->k);
+    L->Bp.reserve(L->tsize * L->V * L->kp);
+    L->stat.reserve(L->tsize * L->V * L->kp);
+    L->logscale.reserve(8 * L->V);
+    L->colsum.reserve(8 * L->k);
+    L->colpart.reserve(8 * L->nblocks_m * L->k);
+    L->alpha.reserve(8 * L->k);
+    L->small.reserve(8 * (L->k + 1));
+    L->stats4.reserve(8 * 4);
+    L->cum2.reserve(8 * 2);
+    HIP_CHECK(hipMemsetAsync(L->cum2.p, 0, 16, ctx->stream));
+    HIP_CHECK(hipMemcpyAsync(L->alpha.p, alpha.data(), 8 * L->k, hipMemcpyHostToDevice, ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    for (auto& s : L->ev)
+      for (auto& e : s) HIP_CHECK(hipEventCreate(&e));
+    *out = L.release();
+  });
+}
+
+int stc_lda_destroy(stc_lda* lda) {
+  return guard([&] {
+    if (!lda) return;
+    (void)hipSetDevice(lda->ctx->device);
+    (void)hipStreamSynchronize(lda->ctx->stream);
+    delete lda;
+  });
+}
+
+int stc_lda_set_corpus(stc_lda* L, const stc_dcsr* corpus, int64_t corpus_size_total) {
+  return guard([&] {
+    STC_REQUIRE(L && corpus, "lda/corpus");
+    STC_REQUIRE(corpus->cols == L->V, "corpus must have vocab_size columns");
+    STC_REQUIRE(corpus->dtype == L->dtype, "corpus value dtype must match the LDA dtype");
+    STC_REQUIRE(corpus->rows < (int64_t(1) << 31), "at most 2^31-1 documents per rank");
+    STC_REQUIRE(corpus_size_total >= corpus->rows && corpus_size_total > 0,
+                "corpus_size_total must be >= this rank's rows and > 0");
+    L->corpus = corpus;
+    L->corpus_total = corpus_size_total;
+  });
+}
+
+int stc_lda_init_random(stc_lda* L, uint64_t seed) {
+  return guard([&] {
+    STC_REQUIRE(L, "lda");
+    L->ctx->use();
+    lda::launch_init_lambda(L->ctx->stream, L->lam.as<double>(), L->V, L->k, seed, L->cfg.gamma_shape);
+    refresh(*L);
+    L->iteration = 0;
+    HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+  });
+}
+
+int stc_lda_set_topics(stc_lda* L, const double* topics, int layout) {
+  return guard([&] {
+    STC_REQUIRE(L && topics, "lda/topics");
+    STC_REQUIRE(layout == STC_LAYOUT_VK || layout == STC_LAYOUT_KV, "layout");
+    L->ctx->use();
+    const int64_t n = L->V * L->k;
+    std::vector<double> h((size_t)n);
+    for (int64_t v = 0; v < L->V; ++v)
+      for (int t = 0; t < L->k; ++t) {
+        const double x = layout == STC_LAYOUT_VK ? topics[v * L->k + t] : topics[(int64_t)t * L->V + v];
+        STC_REQUIRE(x > 0.0 && std::isfinite(x), "topics entries must be finite and > 0");
+        h[(size_t)(v * L->k + t)] = x;
+      }
+    HIP_CHECK(hipMemcpyAsync(L->lam.p, h.data(), 8 * n, hipMemcpyHostToDevice, L->ctx->stream));
+    refresh(*L);
+    HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+  });
+}
+
+int stc_lda_get_topics(stc_lda* L, double* out, int layout) {
+  return guard([&] {
+    STC_REQUIRE(L && out, "lda/out");
+    STC_REQUIRE(layout == STC_LAYOUT_VK || layout == STC_LAYOUT_KV, "layout");
+    STC_REQUIRE(L->has_topics, "no topics yet");
+    L->ctx->use();
+    const int64_t n = L->V * L->k;
+    if (layout == STC_LAYOUT_VK) {
+      HIP_CHECK(hipMemcpyAsync(out, L->lam.p, 8 * n, hipMemcpyDeviceToHost, L->ctx->stream));
+      HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+    } else {
+      std::vector<double> h((size_t)n);
+      HIP_CHECK(hipMemcpyAsync(h.data(), L->lam.p, 8 * n, hipMemcpyDeviceToHost, L->ctx->stream));
+      HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+      for (int64_t v = 0; v < L->V; ++v)
+        for (int t = 0; t < L->k; ++t) out[(int64_t)t * L->V + v] = h[(size_t)(v * L->k + t)];
+    }
+  });
+}
+
+int stc_lda_set_alpha(stc_lda* L, const double* alpha) {
+  return guard([&] {
+    STC_REQUIRE(L && alpha, "lda/alpha");
+    for (int t = 0; t < L->k; ++t) STC_REQUIRE(alpha[t] >= 0, "alpha entries must be >= 0");
+    L->ctx->use();
+    HIP_CHECK(hipMemcpyAsync(L->alpha.p, alpha, 8 * L->k, hipMemcpyHostToDevice, L->ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+  });
+}
+
+int stc_lda_get_alpha(stc_lda* L, double* alpha_out) {
+  return guard([&] {
+    STC_REQUIRE(L && alpha_out, "lda/alpha_out");
+    L->ctx->use();
+    HIP_CHECK(hipMemcpyAsync(alpha_out, L->alpha.p, 8 * L->k, hipMemcpyDeviceToHost, L->ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+  });
+}
+
+int stc_lda_get_eta(stc_lda* L, double* eta_out) {
+  return guard([&] {
+    STC_REQUIRE(L && eta_out, "lda/eta_out");
+    *eta_out = L->eta;
+  });
+}
+
+int stc_lda_get_iteration(stc_lda* L, int64_t* it) {
+  return guard([&] {
+    STC_REQUIRE(L && it, "lda/it");
+    *it = L->iteration;
+  });
+}
+
+int stc_lda_step(stc_lda* L, const int64_t* ids, int64_t n, const double* gamma0, stc_step_stats* st) {
+  return guard([&] {
+    STC_REQUIRE(L && (ids || n == 0) && n >= 0, "lda/ids");
+    L->ctx->use();
+    if (L->dtype == STC_F32) step_ids<float>(*L, ids, n, gamma0, st);
+    else step_ids<double>(*L, ids, n, gamma0, st);
+  });
+}
+
+int stc_lda_next(stc_lda* L, stc_step_stats* st) {
+  return guard([&] {
+    STC_REQUIRE(L, "lda");
+    L->ctx->use();
+    if (L->dtype == STC_F32) next_impl<float>(*L, st);
+    else next_impl<double>(*L, st);
+  });
+}
+
+int stc_lda_estep(stc_lda* L, const int64_t* ids, int64_t n, const double* gamma0, double* gamma_out,
+                  double* stat_out, int32_t* iters_out) {
+  return guard([&] {
+    STC_REQUIRE(L && (ids || n == 0) && n >= 0, "lda/ids");
+    L->ctx->use();
+    if (L->dtype == STC_F32) estep_only<float>(*L, ids, n, gamma0, gamma_out, stat_out, iters_out);
+    else estep_only<double>(*L, ids, n, gamma0, gamma_out, stat_out, iters_out);
+  });
+}
+
+int stc_lda_bound(stc_lda* L, const stc_dcsr* docs, uint64_t gamma_seed, int64_t doc_id_base,
+                  const double* gamma0, double* bound_out, double* corpus_part_out,
+                  double* topics_part_out, double* token_count_out) {
+  return guard([&] {
+    STC_REQUIRE(L && docs, "lda/docs");
+    L->ctx->use();
+    double h[2] = {0, 0};
+    double tp = 0;
+    if (L->dtype == STC_F32) {
+      infer_impl<float>(*L, *docs, gamma_seed, doc_id_base, gamma0, true, nullptr, h);
+      tp = topics_part<float>(*L);
+    } else {
+      infer_impl<double>(*L, *docs, gamma_seed, doc_id_base, gamma0, true, nullptr, h);
+      tp = topics_part<double>(*L);
+    }
+    allreduce_host(*L->ctx, h, 2);  // corpusPart and token count are sums over all ranks
+    if (bound_out) *bound_out = h[0] + tp;
+    if (corpus_part_out) *corpus_part_out = h[0];
+    if (topics_part_out) *topics_part_out = tp;
+    if (token_count_out) *token_count_out = h[1];
+  });
+}
+
+int stc_lda_topic_distribution(stc_lda* L, const stc_dcsr* docs, uint64_t gamma_seed,
+                               int64_t doc_id_base, const double* gamma0, double* out) {
+  return guard([&] {
+    STC_REQUIRE(L && docs && (out || docs->rows == 0), "lda/docs/out");
+    L->ctx->use();
+    if (L->dtype == STC_F32)
+      infer_impl<float>(*L, *docs, gamma_seed, doc_id_base, gamma0, false, out, nullptr);
+    else
+      infer_impl<double>(*L, *docs, gamma_seed, doc_id_base, gamma0, false, out, nullptr);
+    for (int64_t i = 0; i < docs->rows; ++i) {  // normalize(gamma, 1.0); zeros for empty docs
+      double* g = out + i * L->k;
+      double sum = 0.0;
+      for (int t = 0; t < L->k; ++t) sum += std::fabs(g[t]);
+      if (sum > 0.0)
+        for (int t = 0; t < L->k; ++t) g[t] /= sum;
+    }
+  });
+}
+
+int stc_lda_describe(stc_lda* L, int32_t max_terms, int32_t* idx_out, double* weight_out) {
+  return guard([&] {
+    STC_REQUIRE(L && idx_out && weight_out, "lda/idx_out/weight_out");
+    STC_REQUIRE(max_terms > 0, "maxTermsPerTopic must be > 0");
+    STC_REQUIRE(L->has_topics, "no topics yet");
+    STC_REQUIRE(L->V * L->k < (int64_t(1) << 31), "describe: V*k must be < 2^31");
+    L->ctx->use();
+    hipStream_t s = L->ctx->stream;
+    const int64_t n = L->V * L->k;
+    const int N = (int)std::min<int64_t>(max_terms, L->V);
+    DevBuf kv, kv_s, ix, ix_s, off, tmp;
+    kv.reserve(8 * n);
+    kv_s.reserve(8 * n);
+    ix.reserve(4 * n);
+    ix_s.reserve(4 * n);
+    off.reserve(8 * (L->k + 1));
+    std::vector<int64_t> ho((size_t)L->k + 1);
+    for (int t = 0; t <= L->k; ++t) ho[(size_t)t] = (int64_t)t * L->V;
+    HIP_CHECK(hipMemcpyAsync(off.p, ho.data(), 8 * (L->k + 1), hipMemcpyHostToDevice, s));
+    lda::launch_transpose_kv(s, L->lam.as<double>(), L->V, L->k, kv.as<double>(), ix.as<int32_t>());
+    size_t tb = 0;
+    // stable descending sort per topic ⇒ ties keep ascending term index (Scala's sortBy(-w))
+    HIP_CHECK(hipcub::DeviceSegmentedRadixSort::SortPairsDescending(
+        nullptr, tb, kv.as<double>(), kv_s.as<double>(), ix.as<int32_t>(), ix_s.as<int32_t>(), (int)n,
+        L->k, off.as<int64_t>(), off.as<int64_t>() + 1, 0, 64, s));
+    tmp.reserve(tb);
+    HIP_CHECK(hipcub::DeviceSegmentedRadixSort::SortPairsDescending(
+        tmp.p, tb, kv.as<double>(), kv_s.as<double>(), ix.as<int32_t>(), ix_s.as<int32_t>(), (int)n,
+        L->k, off.as<int64_t>(), off.as<int64_t>() + 1, 0, 64, s));
+    std::vector<double> cs((size_t)L->k);
+    HIP_CHECK(hipMemcpyAsync(cs.data(), L->colsum.p, 8 * L->k, hipMemcpyDeviceToHost, s));
+    std::vector<double> w((size_t)N);
+    for (int t = 0; t < L->k; ++t) {
+      HIP_CHECK(hipMemcpyAsync(idx_out + (int64_t)t * N, ix_s.as<int32_t>() + (int64_t)t * L->V, 4 * N,
+                               hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipMemcpyAsync(weight_out + (int64_t)t * N, kv_s.as<double>() + (int64_t)t * L->V, 8 * N,
+                               hipMemcpyDeviceToHost, s));
+    }
+    HIP_CHECK(hipStreamSynchronize(s));
+    for (int t = 0; t < L->k; ++t)  // normalize(topic, 1.0): v / ‖v‖₁ (λ > 0)
+      for (int j = 0; j < N; ++j) weight_out[(int64_t)t * N + j] /= cs[(size_t)t];
+  });
+}
+
+int stc_lda_enable_timing(stc_lda* L, int on) {
+  return guard([&] {
+    STC_REQUIRE(L, "lda");
+    L->timing = on != 0;
+    for (double& a : L->acc_ms) a = 0.0;
+    L->timed_steps = 0;
+    L->ev_pending[0] = L->ev_pending[1] = false;
+  });
+}
+
+int stc_lda_phase_times(stc_lda* L, double* ms_out, int64_t* steps_out) {
+  return guard([&] {
+    STC_REQUIRE(L && ms_out, "lda/ms_out");
+    L->ctx->use();
+    HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+    harvest(*L, 0);
+    harvest(*L, 1);
+    for (int p = 0; p < 5; ++p) ms_out[p] = L->timed_steps ? L->acc_ms[p] / (double)L->timed_steps : 0.0;
+    if (steps_out) *steps_out = L->timed_steps;
+  });
+}
+
+int stc_lda_counters(stc_lda* L, int64_t out[4]) {
+  return guard([&] {
+    STC_REQUIRE(L && out, "lda/out");
+    L->ctx->use();
+    int64_t c2[2] = {0, 0};
+    HIP_CHECK(hipMemcpyAsync(c2, L->cum2.p, 16, hipMemcpyDeviceToHost, L->ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+    out[0] = L->cum_docs;
+    out[1] = L->cum_entries;
+    out[2] = c2[0];
+    out[3] = c2[1];
+  });
+}
+
+}  // extern "C"

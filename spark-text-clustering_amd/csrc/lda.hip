@@ -1,0 +1,910 @@
+// lda.hip — online variational-Bayes LDA kernels for gfx950 (K6–K12 of SURVEY.md §7).
+//
+// Each kernel restates one upstream function of spark-mllib 2.4.3 (TextClustering/build.sbt:10),
+// reached from lda.run(corpus) at LDAClustering.scala:61 and toLocal.topicDistribution at
+// LDALoader.scala:108:
+//   k_estep          [U] OnlineLDAOptimizer.variationalTopicInference (+ LocalLDAModel
+//                    logLikelihoodBound corpusPart when BOUND)
+//   k_sstats/k_fixup [U] submitMiniBatch `stat(::, ids) += sstats` + treeReduce (per device)
+//   k_lambda_update  [U] submitMiniBatch `statsSum ⊙ expElogβᵀ` + updateLambda
+//   k_expelogbeta    [U] exp(LDAUtils.dirichletExpectation(λ)) (+ .t)
+//   k_update_alpha   [U] updateAlpha (Newton step on α)
+//   k_topics_bound   [U] logLikelihoodBound topicsPart
+//
+// Numerics: expElogβ is stored ROW-SCALED, Bp[v][t] = exp(Elogβ[v][t] − m_v) with
+// m_v = max_t Elogβ[v][t], and the E-step iterates with eθ' = exp(ψ(γ_t) − ψ(max γ)).  Both
+// factors cancel exactly in γ ← eθ ⊙ Bᵀ(cts/(B·eθ)) + α and in batchResult = stat ⊙ expElogβ, so
+// the recursion is Spark's, but nothing underflows in fp32 (Spark's unscaled exp(Elogβ) reaches
+// 1e-50 for rare terms).  The bound adds m_v and max E[log θ] back in fp64.
+#include "lda_kernels.h"
+
+namespace stc {
+namespace lda {
+
+template <typename T>
+struct VecOf;
+template <>
+struct VecOf<float> {
+  typedef float type __attribute__((ext_vector_type(4)));
+  static constexpr int W = 4;
+};
+template <>
+struct VecOf<double> {
+  typedef double type __attribute__((ext_vector_type(2)));
+  static constexpr int W = 2;
+};
+
+template <typename T>
+__device__ __forceinline__ T eps_phi() { return T(1e-30); }
+template <>
+__device__ __forceinline__ double eps_phi<double>() { return 1e-100; }
+
+template <typename T, typename VT>
+__device__ __forceinline__ T hsum(VT v);
+template <>
+__device__ __forceinline__ float hsum<float, VecOf<float>::type>(VecOf<float>::type v) {
+  return (v.x + v.y) + (v.z + v.w);
+}
+template <>
+__device__ __forceinline__ double hsum<double, VecOf<double>::type>(VecOf<double>::type v) {
+  return v.x + v.y;
+}
+
+__device__ __forceinline__ float exp_t(float x) { return __expf(x); }
+__device__ __forceinline__ double exp_t(double x) { return exp(x); }
+
+// ---------------------------------------------------------------------------------------
+// Block (256 threads = 4 waves) reduction of (sum, sum, max) in a fixed order: deterministic.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void block_reduce3(double& a, double& b, double& c, double* s_red) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  c = wave_max(c);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_red[w * 4 + 0] = a;
+    s_red[w * 4 + 1] = b;
+    s_red[w * 4 + 2] = c;
+  }
+  __syncthreads();
+  a = (s_red[0] + s_red[4]) + (s_red[8] + s_red[12]);
+  b = (s_red[1] + s_red[5]) + (s_red[9] + s_red[13]);
+  c = fmax(fmax(s_red[2], s_red[6]), fmax(s_red[10], s_red[14]));
+  __syncthreads();
+}
+
+template <typename T>
+__host__ __device__ constexpr int part_elems(int kp) {
+  return (256 * VecOf<T>::W > kp) ? 256 * VecOf<T>::W : kp;
+}
+
+template <typename T>
+size_t estep_lds_bytes(int kp, int lds_rows, int P) {
+  size_t b = 0;
+  b += 2 * (size_t)kp * sizeof(T);                 // eth, gam
+  b += (size_t)part_elems<T>(kp) * sizeof(T);      // partial column sums
+  b += 16 * sizeof(double);                        // reduction scratch
+  b += (size_t)lds_rows * sizeof(int32_t);         // ids   (lds_rows % 4 == 0)
+  b += 2 * (size_t)lds_rows * sizeof(T);           // cts, r
+  b += (size_t)lds_rows * P * sizeof(T);           // the document block B
+  return b;
+}
+
+template <typename T>
+int estep_lds_rows(int k, int kp, int P) {
+  (void)k;
+  const size_t fixed = estep_lds_bytes<T>(kp, 0, P);
+  const size_t per_row = sizeof(int32_t) + 2 * sizeof(T) + (size_t)P * sizeof(T);
+  if (fixed >= (size_t)kLdsBudget) return 0;
+  int rows = (int)(((size_t)kLdsBudget - fixed) / per_row);
+  return rows & ~3;
+}
+
+// ---------------------------------------------------------------------------------------
+// K6: the E-step.  One 256-thread workgroup per document; the hardware dispatcher balances the
+// data-dependent trip counts.  LDS=true keeps the gathered nnz×k block in LDS (rows padded to
+// P with P/W odd ⇒ conflict-free row-per-lane ds_read_b128); LDS=false streams it from L2.
+// Per inner iteration: φ_n = B_n·eθ' (row per lane), r_n = cts_n/φ_n, s = Bᵀr (column groups ×
+// row subsets, partials in LDS), γ = eθ'⊙s + α, eθ' = exp(ψ(γ) − ψ(max γ)), meanΔγ ≤ 1e-3 stops.
+// ---------------------------------------------------------------------------------------
+template <typename T, bool STATS, bool BOUND, bool LDS>
+__device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* smem, int64_t i,
+                                          int64_t row, int64_t s0, int nnz, int64_t e0) {
+  using VT = typename VecOf<T>::type;
+  constexpr int W = VecOf<T>::W;
+  const int tid = threadIdx.x;
+  const int k = a.k, kp = a.kp, ncg = kp / W, P = a.P;
+  const int rows_cap = a.lds_rows;
+
+  T* s_eth = reinterpret_cast<T*>(smem);
+  T* s_gam = s_eth + kp;
+  T* s_part = s_gam + kp;
+  double* s_red = reinterpret_cast<double*>(s_part + part_elems<T>(kp));
+  int32_t* s_ids = reinterpret_cast<int32_t*>(s_red + 16);
+  T* s_cts = reinterpret_cast<T*>(s_ids + rows_cap);
+  T* s_r = s_cts + rows_cap;
+  T* s_B = s_r + rows_cap;
+
+  const int32_t* ids = LDS ? s_ids : a.indices + s0;
+  const T* cts = LDS ? s_cts : a.values + s0;
+  T* rr = LDS ? s_r : a.r + e0;
+
+  // -- load ids / counts (LDS) and detect an all-zero document (Spark's numNonzeros == 0)
+  int nz = 0;
+  for (int n = tid; n < nnz; n += kBlock) {
+    const int32_t id = a.indices[s0 + n];
+    const T c = a.values[s0 + n];
+    if (LDS) {
+      s_ids[n] = id;
+      s_cts[n] = c;
+    }
+    nz |= (c != T(0));
+  }
+  const bool nonempty = __syncthreads_or(nz) != 0;
+  if (!nonempty) {
+    for (int t = tid; t < k; t += kBlock) {
+      if (a.gamma) a.gamma[i * k + t] = T(0);
+      if (STATS) a.elogth[i * k + t] = T(0);
+    }
+    if (STATS)
+      for (int t = tid; t < kp; t += kBlock) a.eth[i * kp + t] = T(0);
+    for (int n = tid; n < nnz; n += kBlock) {
+      a.r[e0 + n] = T(0);
+      if (STATS) {
+        a.keys[e0 + n] = (uint32_t)a.indices[s0 + n];
+        a.vals[e0 + n] = (uint32_t)(e0 + n);
+        a.edoc[e0 + n] = (int32_t)i;
+      }
+    }
+    if (tid == 0) {
+      if (a.iters) a.iters[i] = 0;
+      if (a.nonempty) a.nonempty[i] = 0;
+      if (BOUND) a.bound[i] = 0.0;
+    }
+    return;
+  }
+
+  // -- gather the document block B[n][:] = Bp[ids[n]][:] into LDS
+  if (LDS) {
+    const int total = nnz * ncg;
+#pragma unroll 4
+    for (int w = tid; w < total; w += kBlock) {
+      const int n = w / ncg;
+      const int c = w - n * ncg;
+      const VT v = *reinterpret_cast<const VT*>(a.Bp + (int64_t)s_ids[n] * kp + c * W);
+      *reinterpret_cast<VT*>(s_B + n * P + c * W) = v;
+    }
+  }
+
+  // -- γ₀ (injected or counter RNG) and eθ'
+  uint64_t stream = 0;
+  if (!a.gamma0) {
+    const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, i)
+                                         : (uint64_t)(a.doc_id_base + row);
+    stream = doc_stream(a.seed, key);
+  }
+  double gsum = 0.0, gmax = -INFINITY, dummy = 0.0;
+  for (int t = tid; t < kp; t += kBlock) {
+    T g = T(0);
+    if (t < k) {
+      g = a.gamma0 ? a.gamma0[i * k + t] : (T)gamma_sample(stream, t, a.gamma_shape);
+      gsum += (double)g;
+      gmax = fmax(gmax, (double)g);
+    }
+    s_gam[t] = g;
+  }
+  block_reduce3(gsum, dummy, gmax, s_red);
+  {
+    const T psimax = digamma_t<T>((T)gmax);
+    for (int t = tid; t < kp; t += kBlock)
+      s_eth[t] = t < k ? exp_t(digamma_t<T>(s_gam[t]) - psimax) : T(0);
+  }
+  __syncthreads();
+
+  const int R = ncg >= kBlock ? 1 : kBlock / ncg;  // row subsets in the Bᵀr product
+  const int nwork = R * ncg;
+  int it = 0;
+  bool done = false;
+  double b_tok = 0.0, c_tok = 0.0;  // BOUND: Σ cts·(log φ'_n + m_v), Σ cts
+  while (true) {
+    // Phase A: φ_n = B_n · eθ', r_n = cts_n / φ_n
+    for (int n = tid; n < nnz; n += kBlock) {
+      const T* Brow = LDS ? s_B + n * P : a.Bp + (int64_t)ids[n] * kp;
+      VT acc = (VT)T(0);
+      for (int c = 0; c < ncg; ++c)
+        acc += *reinterpret_cast<const VT*>(Brow + c * W) * *reinterpret_cast<const VT*>(s_eth + c * W);
+      const T phi = hsum<T, VT>(acc) + eps_phi<T>();
+      const T cn = cts[n];
+      rr[n] = cn / phi;
+      if (BOUND && (done || it >= a.max_iter) && cn != T(0)) {
+        b_tok += (double)cn * ((double)log(phi) + a.logscale[ids[n]]);
+        c_tok += (double)cn;
+      }
+    }
+    __syncthreads();
+    if (done || it >= a.max_iter) break;
+
+    // Phase B: partial column sums s_j[c] = Σ_{n ≡ j mod R} B[n][c]·r_n
+    for (int w = tid; w < nwork; w += kBlock) {
+      const int c = w % ncg;
+      const int j = w / ncg;
+      VT acc = (VT)T(0);
+      for (int n = j; n < nnz; n += R) {
+        const T* Brow = LDS ? s_B + n * P : a.Bp + (int64_t)ids[n] * kp;
+        acc += *reinterpret_cast<const VT*>(Brow + c * W) * rr[n];
+      }
+      *reinterpret_cast<VT*>(s_part + j * kp + c * W) = acc;
+    }
+    __syncthreads();
+
+    // Phase C: γ ← eθ' ⊙ s + α ; Σ|Δγ|, Σγ, max γ
+    double dsum = 0.0;
+    gsum = 0.0;
+    gmax = -INFINITY;
+    for (int t = tid; t < k; t += kBlock) {
+      T s = T(0);
+      for (int j = 0; j < R; ++j) s += s_part[j * kp + t];
+      const T g = s_eth[t] * s + (T)a.alpha[t];
+      dsum += fabs((double)g - (double)s_gam[t]);
+      s_gam[t] = g;
+      gsum += (double)g;
+      gmax = fmax(gmax, (double)g);
+    }
+    block_reduce3(dsum, gsum, gmax, s_red);
+
+    // Phase D: eθ' = exp(ψ(γ) − ψ(max γ)) ; meanGammaChange = Σ|Δγ| / k
+    const T psimax = digamma_t<T>((T)gmax);
+    for (int t = tid; t < k; t += kBlock) s_eth[t] = exp_t(digamma_t<T>(s_gam[t]) - psimax);
+    ++it;
+    done = dsum / (double)k <= 1e-3;
+    __syncthreads();
+  }
+
+  // -- outputs
+  const double psisum = digamma_t<double>(gsum);
+  for (int t = tid; t < k; t += kBlock) {
+    if (a.gamma) a.gamma[i * k + t] = s_gam[t];
+    if (STATS) a.elogth[i * k + t] = (T)(digamma_t<double>((double)s_gam[t]) - psisum);
+  }
+  if (STATS) {
+    for (int t = tid; t < kp; t += kBlock) a.eth[i * kp + t] = s_eth[t];
+    for (int n = tid; n < nnz; n += kBlock) {
+      if (LDS) a.r[e0 + n] = s_r[n];
+      a.keys[e0 + n] = (uint32_t)ids[n];
+      a.vals[e0 + n] = (uint32_t)(e0 + n);
+      a.edoc[e0 + n] = (int32_t)i;
+    }
+  }
+  if (tid == 0) {
+    if (a.iters) a.iters[i] = it;
+    if (a.nonempty) a.nonempty[i] = 1;
+  }
+  if (BOUND) {
+    // E[log p(doc|θ,β)] = Σ_n cts_n (log φ'_n + m_v + max E[log θ]);  E[log p(θ|α) − log q(θ|γ)]
+    const double elog_max = digamma_t<double>(gmax) - psisum;
+    double topic = 0.0, asum = 0.0, dummy2 = -INFINITY;
+    for (int t = tid; t < k; t += kBlock) {
+      const double g = (double)s_gam[t], al = a.alpha[t];
+      const double el = digamma_t<double>(g) - psisum;
+      topic += (al - g) * el + (lgamma(g) - lgamma(al));
+      asum += al;
+    }
+    double tok = b_tok + c_tok * elog_max;
+    block_reduce3(tok, topic, dummy2, s_red);
+    double as2 = asum, z = 0.0, dz = -INFINITY;
+    block_reduce3(as2, z, dz, s_red);
+    if (tid == 0) a.bound[i] = tok + topic + (lgamma(as2) - lgamma(gsum));
+  }
+}
+
+template <typename T, bool STATS, bool BOUND>
+__global__ __launch_bounds__(kBlock) void k_estep(EStepArgs<T> a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int64_t i = blockIdx.x;
+  if (i >= a.n) return;
+  const int64_t row = a.batch ? (int64_t)a.batch[i] : i;
+  const int64_t s0 = a.indptr[row];
+  const int nnz = (int)(a.indptr[row + 1] - s0);
+  const int64_t e0 = a.bptr[i];
+  if (nnz <= a.lds_rows)
+    estep_doc<T, STATS, BOUND, true>(a, smem, i, row, s0, nnz, e0);
+  else
+    estep_doc<T, STATS, BOUND, false>(a, smem, i, row, s0, nnz, e0);
+}
+
+template <typename T>
+void launch_estep(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound) {
+  if (a.n == 0) return;
+  const size_t lds = estep_lds_bytes<T>(a.kp, a.lds_rows, a.P);
+  const dim3 grid((unsigned)a.n);
+  if (stats) {
+    static bool set = false;
+    if (!set) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)k_estep<T, true, false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget));
+      set = true;
+    }
+    k_estep<T, true, false><<<grid, kBlock, lds, s>>>(a);
+  } else if (bound) {
+    static bool set = false;
+    if (!set) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)k_estep<T, false, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget));
+      set = true;
+    }
+    k_estep<T, false, true><<<grid, kBlock, lds, s>>>(a);
+  } else {
+    static bool set = false;
+    if (!set) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)k_estep<T, false, false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBudget));
+      set = true;
+    }
+    k_estep<T, false, false><<<grid, kBlock, lds, s>>>(a);
+  }
+  KERNEL_CHECK();
+}
+
+// ---------------------------------------------------------------------------------------
+// Sufficient statistics: stat[v][:] = Σ_{entries of term v} r_e · eθ'[doc(e)][:]  — a
+// segmented SpMM over the batch's (term, slot) pairs radix-sorted by term.  One wave per chunk of
+// kChunk sorted entries, lanes over topics; runs that cross chunk edges go to head/tail partials
+// that k_fixup adds in chunk order.  Plain stores, no atomics, bitwise reproducible.
+// ---------------------------------------------------------------------------------------
+template <typename T, int Q>
+__global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ skeys,
+                                                const uint32_t* __restrict__ svals, int64_t E,
+                                                const T* __restrict__ r, const int32_t* __restrict__ edoc,
+                                                const T* __restrict__ eth, int kp, T* __restrict__ stat,
+                                                T* __restrict__ headbuf, T* __restrict__ tailbuf,
+                                                int64_t nchunks) {
+  const int lane = threadIdx.x & 63;
+  const int64_t chunk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (chunk >= nchunks) return;
+  const int64_t p0 = chunk * kChunk;
+  const int64_t p1 = (p0 + kChunk < E) ? p0 + kChunk : E;
+  const uint32_t first = skeys[p0], last = skeys[p1 - 1];
+  const bool start_mid = p0 > 0 && skeys[p0 - 1] == first;
+  const bool cont = p1 < E && skeys[p1] == last;
+  T acc[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) acc[q] = T(0);
+  uint32_t cur = first;
+  auto flush = [&](uint32_t v) {
+    T* dst;
+    if (v == first && start_mid) dst = headbuf + chunk * kp;
+    else if (v == last && cont) dst = tailbuf + chunk * kp;
+    else dst = stat + (int64_t)v * kp;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int col = lane + 64 * q;
+      if (col < kp) dst[col] = acc[q];
+      acc[q] = T(0);
+    }
+  };
+  for (int64_t pb = p0; pb < p1; pb += 64) {
+    const int64_t p = pb + lane;
+    uint32_t kv = 0xFFFFFFFFu;
+    T rv = T(0);
+    int32_t dv = 0;
+    if (p < p1) {
+      kv = skeys[p];
+      const uint32_t j = svals[p];
+      rv = r[j];
+      dv = edoc[j];
+    }
+    const int cnt = (int)((p1 - pb) < 64 ? (p1 - pb) : 64);
+    for (int jj = 0; jj < cnt; ++jj) {
+      const uint32_t v = (uint32_t)__shfl((int)kv, jj, 64);
+      const T rj = __shfl(rv, jj, 64);
+      const int32_t d = __shfl(dv, jj, 64);
+      if (v != cur) {
+        flush(cur);
+        cur = v;
+      }
+      const T* er = eth + (int64_t)d * kp;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int col = lane + 64 * q;
+        if (col < kp) acc[q] += rj * er[col];
+      }
+    }
+  }
+  flush(cur);
+}
+
+template <typename T, int Q>
+__global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skeys, int64_t E,
+                                               int kp, T* __restrict__ stat,
+                                               const T* __restrict__ headbuf,
+                                               const T* __restrict__ tailbuf, int64_t nchunks) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= nchunks) return;
+  const int64_t p0 = c * kChunk;
+  const int64_t p1 = (p0 + kChunk < E) ? p0 + kChunk : E;
+  const uint32_t first = skeys[p0], last = skeys[p1 - 1];
+  const bool start_mid = p0 > 0 && skeys[p0 - 1] == first;
+  const bool cont = p1 < E && skeys[p1] == last;
+  if (!cont || (first == last && start_mid)) return;  // owner = chunk where the run starts
+  T acc[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int col = lane + 64 * q;
+    acc[q] = col < kp ? tailbuf[c * kp + col] : T(0);
+  }
+  for (int64_t c2 = c + 1; c2 < nchunks; ++c2) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int col = lane + 64 * q;
+      if (col < kp) acc[q] += headbuf[c2 * kp + col];
+    }
+    const int64_t q0 = c2 * kChunk;
+    const int64_t q1 = (q0 + kChunk < E) ? q0 + kChunk : E;
+    if (!(skeys[q1 - 1] == last && q1 < E && skeys[q1] == last)) break;
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int col = lane + 64 * q;
+    if (col < kp) stat[(int64_t)last * kp + col] = acc[q];
+  }
+}
+
+template <typename T, int Q>
+static void sstats_q(hipStream_t s, const uint32_t* skeys, const uint32_t* svals, int64_t E,
+                     const T* r, const int32_t* edoc, const T* eth, int kp, T* stat, T* headbuf,
+                     T* tailbuf) {
+  const int64_t nchunks = ceil_div(E, kChunk);
+  const dim3 grid((unsigned)ceil_div(nchunks, 4));
+  k_sstats<T, Q><<<grid, 256, 0, s>>>(skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf, nchunks);
+  KERNEL_CHECK();
+  k_fixup<T, Q><<<grid, 256, 0, s>>>(skeys, E, kp, stat, headbuf, tailbuf, nchunks);
+  KERNEL_CHECK();
+}
+
+template <typename T>
+void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint32_t* svals, int64_t E,
+                   const T* r, const int32_t* edoc, const T* eth, int kp, T* stat, T* headbuf,
+                   T* tailbuf) {
+  if (E == 0) return;
+  const int q = (kp + 63) / 64;
+  if (q <= 1) sstats_q<T, 1>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
+  else if (q <= 2) sstats_q<T, 2>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
+  else if (q <= 4) sstats_q<T, 4>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
+  else if (q <= 8) sstats_q<T, 8>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
+  else if (q <= 16) sstats_q<T, 16>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
+  else if (q <= 32) sstats_q<T, 32>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
+  else if (q <= 64) sstats_q<T, 64>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
+  else throw Error(STC_ERR_INVALID_ARG, "k > 4096 topics is not supported");
+}
+
+// ---------------------------------------------------------------------------------------
+// M-step.  λ is fp64 V×k (term-major, Spark's topicsMatrix orientation); rows of RB terms per
+// workgroup, lanes over topics, fixed-order per-topic partial sums (deterministic colsum).
+// ---------------------------------------------------------------------------------------
+
+template <typename T, bool UPDATE>
+__global__ __launch_bounds__(256) void k_lambda_update(double* __restrict__ lam, const T* __restrict__ stat,
+                                                       const T* __restrict__ Bp, int64_t V, int k, int kp,
+                                                       double rho, double scale, double eta,
+                                                       const double* __restrict__ gate,
+                                                       double* __restrict__ colpart) {
+  if (gate && gate[0] == 0.0) return;  // Spark: no non-empty docs ⇒ no update
+  __shared__ double s_acc[256];
+  const int tid = threadIdx.x;
+  const int TW = k < 256 ? k : 256;
+  const int nrl = 256 / TW;
+  const int ti = tid % TW, rl = tid / TW;
+  const int64_t v0 = (int64_t)blockIdx.x * kRowsPerBlock;
+  const int64_t v1 = (v0 + kRowsPerBlock < V) ? v0 + kRowsPerBlock : V;
+  for (int t0 = 0; t0 < k; t0 += TW) {
+    const int t = t0 + ti;
+    double acc = 0.0;
+    if (rl < nrl && t < k) {
+      for (int64_t v = v0 + rl; v < v1; v += nrl) {
+        const int64_t e = v * k + t;
+        double nl = lam[e];
+        if (UPDATE) {
+          const int64_t ev = v * kp + t;
+          nl = (1.0 - rho) * nl + rho * ((double)stat[ev] * (double)Bp[ev] * scale + eta);
+          lam[e] = nl;
+        }
+        acc += nl;
+      }
+    }
+    if (rl < nrl) s_acc[rl * TW + ti] = acc;
+    __syncthreads();
+    if (tid < TW && t0 + tid < k) {
+      double sum = 0.0;
+      for (int j = 0; j < nrl; ++j) sum += s_acc[j * TW + tid];
+      colpart[(int64_t)blockIdx.x * k + t0 + tid] = sum;
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T>
+void launch_lambda_update(hipStream_t s, double* lam, const T* stat, const T* Bp, int64_t V, int k,
+                          int kp, double rho, double scale, double eta, const double* gate,
+                          double* colpart, int64_t nblocks) {
+  k_lambda_update<T, true><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, V, k, kp, rho, scale,
+                                                             eta, gate, colpart);
+  KERNEL_CHECK();
+}
+
+void launch_colsum_lambda(hipStream_t s, const double* lam, int64_t V, int k, double* colpart,
+                          int64_t nblocks) {
+  k_lambda_update<float, false><<<(unsigned)nblocks, 256, 0, s>>>(
+      const_cast<double*>(lam), nullptr, nullptr, V, k, k, 0.0, 0.0, 0.0, nullptr, colpart);
+  KERNEL_CHECK();
+}
+
+__global__ __launch_bounds__(256) void k_colsum_reduce(const double* __restrict__ colpart,
+                                                       int64_t nblocks, int k,
+                                                       const double* __restrict__ gate,
+                                                       double* __restrict__ colsum) {
+  if (gate && gate[0] == 0.0) return;
+  __shared__ double s[256];
+  const int t = blockIdx.x;
+  double acc = 0.0;
+  for (int64_t b = threadIdx.x; b < nblocks; b += 256) acc += colpart[b * k + t];
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) colsum[t] = s[0];
+}
+
+void launch_colsum_reduce(hipStream_t s, const double* colpart, int64_t nblocks, int k,
+                          const double* gate, double* colsum) {
+  k_colsum_reduce<<<k, 256, 0, s>>>(colpart, nblocks, k, gate, colsum);
+  KERNEL_CHECK();
+}
+
+// expElogβ'[v][t] = exp(ψ(λ_vt) − ψ(colsum_t) − m_v), m_v = max_t (ψ(λ_vt) − ψ(colsum_t)); one wave / term
+template <typename T>
+__global__ __launch_bounds__(256) void k_expelogbeta(const double* __restrict__ lam,
+                                                     const double* __restrict__ colsum, int64_t V,
+                                                     int k, int kp, const double* __restrict__ gate,
+                                                     T* __restrict__ Bp, double* __restrict__ logscale) {
+  if (gate && gate[0] == 0.0) return;
+  extern __shared__ double s_psic[];
+  for (int t = threadIdx.x; t < k; t += 256) s_psic[t] = digamma_t<double>(colsum[t]);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (v >= V) return;
+  const double* lr = lam + v * k;
+  double m = -INFINITY;
+  for (int t = lane; t < k; t += 64) m = fmax(m, digamma_t<double>(lr[t]) - s_psic[t]);
+  m = wave_max(m);
+  T* br = Bp + v * kp;
+  for (int t = lane; t < kp; t += 64)
+    br[t] = t < k ? (T)exp(digamma_t<double>(lr[t]) - s_psic[t] - m) : T(0);
+  if (lane == 0) logscale[v] = m;
+}
+
+template <typename T>
+void launch_expelogbeta(hipStream_t s, const double* lam, const double* colsum, int64_t V, int k,
+                        int kp, const double* gate, T* Bp, double* logscale) {
+  k_expelogbeta<T><<<(unsigned)ceil_div(V, 4), 256, sizeof(double) * k, s>>>(lam, colsum, V, k, kp,
+                                                                              gate, Bp, logscale);
+  KERNEL_CHECK();
+}
+
+// logphat = Σ_docs E[log θ_d] (fixed order) ; small[k] = #non-empty docs
+template <typename T>
+__global__ __launch_bounds__(256) void k_logphat(const T* __restrict__ elogth,
+                                                 const int32_t* __restrict__ nonempty, int64_t n,
+                                                 int k, double* __restrict__ small) {
+  __shared__ double s[256];
+  const int t = blockIdx.x;  // t == k: count non-empty docs
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256)
+    acc += t < k ? (double)elogth[i * k + t] : (double)nonempty[i];
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) small[t] = s[0];
+}
+
+template <typename T>
+void launch_logphat(hipStream_t s, const T* elogth, const int32_t* nonempty, int64_t n, int k,
+                    double* small) {
+  k_logphat<T><<<k + 1, 256, 0, s>>>(elogth, nonempty, n, k, small);
+  KERNEL_CHECK();
+}
+
+// updateAlpha: one Newton step; applied only when every α_t + ρ·dα_t > 0
+__global__ __launch_bounds__(256) void k_update_alpha(double* __restrict__ alpha,
+                                                      const double* __restrict__ small, int k,
+                                                      double rho) {
+  extern __shared__ double s_g[];  // gradf[k], q[k]
+  __shared__ double s_r[4 * 4];
+  const double N = small[k];
+  if (N == 0.0) return;
+  double* s_q = s_g + k;
+  double asum = 0.0, z = 0.0, dz = -INFINITY;
+  for (int t = threadIdx.x; t < k; t += 256) asum += alpha[t];
+  block_reduce3(asum, z, dz, s_r);
+  const double psis = digamma_t<double>(asum);
+  double a1 = 0.0, a2 = 0.0;
+  for (int t = threadIdx.x; t < k; t += 256) {
+    const double al = alpha[t];
+    const double g = N * (-(digamma_t<double>(al) - psis) + small[t] / N);
+    const double q = -N * trigamma_d(al);
+    s_g[t] = g;
+    s_q[t] = q;
+    a1 += g / q;
+    a2 += 1.0 / q;
+  }
+  double dz2 = -INFINITY;
+  block_reduce3(a1, a2, dz2, s_r);
+  const double c = N * trigamma_d(asum);
+  const double b = a1 / (1.0 / c + a2);
+  double bad = 0.0, z2 = 0.0, dz3 = -INFINITY;
+  for (int t = threadIdx.x; t < k; t += 256) {
+    const double da = -(s_g[t] - b) / s_q[t];
+    s_g[t] = da;
+    if (!(rho * da + alpha[t] > 0.0)) bad += 1.0;
+  }
+  block_reduce3(bad, z2, dz3, s_r);
+  if (bad == 0.0)
+    for (int t = threadIdx.x; t < k; t += 256) alpha[t] += rho * s_g[t];
+}
+
+void launch_update_alpha(hipStream_t s, double* alpha, const double* small, int k, double rho) {
+  k_update_alpha<<<1, 256, 2 * sizeof(double) * k, s>>>(alpha, small, k, rho);
+  KERNEL_CHECK();
+}
+
+// λ₀ ~ Gamma(shape, 1/shape) i.i.d., keyed by the k×V element index (identical on every rank)
+__global__ __launch_bounds__(256) void k_init_lambda(double* __restrict__ lam, int64_t V, int k,
+                                                     uint64_t seed, double shape) {
+  const int64_t total = V * k;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t v = e / k;
+    const int t = (int)(e - v * k);
+    lam[e] = gamma_sample(doc_stream(seed, (uint64_t)t * (uint64_t)V + (uint64_t)v), 0, shape);
+  }
+}
+
+void launch_init_lambda(hipStream_t s, double* lam, int64_t V, int k, uint64_t seed, double shape) {
+  k_init_lambda<<<2048, 256, 0, s>>>(lam, V, k, seed, shape);
+  KERNEL_CHECK();
+}
+
+// topicsPart of logLikelihoodBound without the per-topic lgamma(Σλ) − lgamma(ηV) term
+template <typename T>
+__global__ __launch_bounds__(256) void k_topics_bound(const double* __restrict__ lam,
+                                                      const double* __restrict__ colsum, int64_t V,
+                                                      int k, double eta, double* __restrict__ partials) {
+  extern __shared__ double s_psic[];
+  __shared__ double s_r[16];
+  for (int t = threadIdx.x; t < k; t += 256) s_psic[t] = digamma_t<double>(colsum[t]);
+  __syncthreads();
+  const int64_t total = V * k;
+  const double lge = lgamma(eta);
+  double acc = 0.0, z = 0.0, dz = -INFINITY;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int t = (int)(e % k);
+    const double l = lam[e];
+    const double eb = digamma_t<double>(l) - s_psic[t];
+    acc += (eta - l) * eb + (lgamma(l) - lge);
+  }
+  block_reduce3(acc, z, dz, s_r);
+  if (threadIdx.x == 0) partials[blockIdx.x] = acc;
+}
+
+template <typename T>
+void launch_topics_bound(hipStream_t s, const double* lam, const double* colsum, int64_t V, int k,
+                         double eta, double* partials, int64_t nblocks) {
+  k_topics_bound<T><<<(unsigned)nblocks, 256, sizeof(double) * k, s>>>(lam, colsum, V, k, eta, partials);
+  KERNEL_CHECK();
+}
+
+template <typename X>
+__global__ __launch_bounds__(256) void k_sum(const X* __restrict__ x, int64_t n, double* __restrict__ out) {
+  __shared__ double s[256];
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) acc += (double)x[i];
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = s[0];
+}
+
+void launch_sum_f64(hipStream_t s, const double* x, int64_t n, double* out) {
+  k_sum<double><<<1, 256, 0, s>>>(x, n, out);
+  KERNEL_CHECK();
+}
+template <typename T>
+void launch_sum_vals(hipStream_t s, const T* x, int64_t n, double* out) {
+  k_sum<T><<<1, 256, 0, s>>>(x, n, out);
+  KERNEL_CHECK();
+}
+
+__global__ __launch_bounds__(256) void k_iter_stats(const int32_t* __restrict__ iters,
+                                                    const int32_t* __restrict__ nonempty, int64_t n,
+                                                    int max_iter, int64_t* __restrict__ out4,
+                                                    int64_t* __restrict__ cum2) {
+  __shared__ int64_t s[4][256];
+  int64_t sum = 0, mx = 0, cap = 0, ne = 0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    const int32_t it = iters[i];
+    sum += it;
+    mx = it > mx ? it : mx;
+    cap += (it >= max_iter) ? 1 : 0;
+    ne += nonempty[i];
+  }
+  s[0][threadIdx.x] = sum;
+  s[1][threadIdx.x] = mx;
+  s[2][threadIdx.x] = cap;
+  s[3][threadIdx.x] = ne;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      s[0][threadIdx.x] += s[0][threadIdx.x + w];
+      s[1][threadIdx.x] = s[1][threadIdx.x] > s[1][threadIdx.x + w] ? s[1][threadIdx.x] : s[1][threadIdx.x + w];
+      s[2][threadIdx.x] += s[2][threadIdx.x + w];
+      s[3][threadIdx.x] += s[3][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) out4[threadIdx.x] = s[threadIdx.x][0];
+  if (threadIdx.x == 0 && cum2) {  // cumulative Σ iterations, cap hits (single block: no race)
+    cum2[0] += s[0][0];
+    cum2[1] += s[2][0];
+  }
+}
+
+void launch_iter_stats(hipStream_t s, const int32_t* iters, const int32_t* nonempty, int64_t n,
+                       int max_iter, int64_t* out4, int64_t* cum2) {
+  k_iter_stats<<<1, 256, 0, s>>>(iters, nonempty, n, max_iter, out4, cum2);
+  KERNEL_CHECK();
+}
+
+__global__ __launch_bounds__(256) void k_batch_nnz(const int64_t* __restrict__ indptr,
+                                                   const int32_t* __restrict__ batch, int64_t n,
+                                                   int64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = batch[i];
+    out[i] = indptr[r + 1] - indptr[r];
+  }
+}
+
+void launch_batch_nnz(hipStream_t s, const int64_t* indptr, const int32_t* batch, int64_t n,
+                      int64_t* nnz_out) {
+  if (n == 0) return;
+  int64_t g = ceil_div(n, 256);
+  k_batch_nnz<<<(unsigned)(g > 4096 ? 4096 : g), 256, 0, s>>>(indptr, batch, n, nnz_out);
+  KERNEL_CHECK();
+}
+
+// RDD.sample(withReplacement, fraction): Poisson(f) (with) or Bernoulli(f) (without) per doc
+__global__ __launch_bounds__(256) void k_sample(const int64_t* __restrict__ indptr, int64_t D,
+                                                double f, int with_repl, uint64_t seed,
+                                                int64_t iteration, int rank,
+                                                int32_t* __restrict__ counts,
+                                                int64_t* __restrict__ weights) {
+  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256) {
+    const uint64_t st = doc_stream(seed ^ 0x5DEECE66Dull, train_doc_key(iteration, rank, d));
+    const double u = rng_uniform(st, 0);
+    int c = 0;
+    if (with_repl) {
+      double p = exp(-f), F = p;
+      while (u > F && c < 64) {
+        ++c;
+        p *= f / c;
+        F += p;
+      }
+    } else {
+      c = u < f ? 1 : 0;
+    }
+    counts[d] = c;
+    weights[d] = (int64_t)c * (indptr[d + 1] - indptr[d]);
+  }
+}
+
+void launch_sample(hipStream_t s, const int64_t* indptr, int64_t D, double fraction, int with_repl,
+                   uint64_t seed, int64_t iteration, int rank, int32_t* counts, int64_t* weights) {
+  int64_t g = ceil_div(D, 256);
+  k_sample<<<(unsigned)(g > 8192 ? 8192 : g), 256, 0, s>>>(indptr, D, fraction, with_repl, seed,
+                                                           iteration, rank, counts, weights);
+  KERNEL_CHECK();
+}
+
+// count_incl / weight_incl are INCLUSIVE scans
+__global__ __launch_bounds__(256) void k_fill_batch(const int64_t* __restrict__ indptr, int64_t D,
+                                                    const int32_t* __restrict__ counts,
+                                                    const int32_t* __restrict__ count_incl,
+                                                    const int64_t* __restrict__ weight_incl,
+                                                    int32_t* __restrict__ batch,
+                                                    int64_t* __restrict__ bptr) {
+  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256) {
+    const int c = counts[d];
+    if (c == 0) continue;
+    const int64_t nnz = indptr[d + 1] - indptr[d];
+    const int64_t pos0 = (int64_t)count_incl[d] - c;
+    const int64_t w0 = weight_incl[d] - (int64_t)c * nnz;
+    for (int j = 0; j < c; ++j) {
+      batch[pos0 + j] = (int32_t)d;
+      bptr[pos0 + j] = w0 + (int64_t)j * nnz;
+    }
+  }
+}
+
+void launch_fill_batch(hipStream_t s, const int64_t* indptr, int64_t D, const int32_t* counts,
+                       const int32_t* count_off, const int64_t* weight_off, int32_t* batch,
+                       int64_t* bptr) {
+  int64_t g = ceil_div(D, 256);
+  k_fill_batch<<<(unsigned)(g > 8192 ? 8192 : g), 256, 0, s>>>(indptr, D, counts, count_off,
+                                                               weight_off, batch, bptr);
+  KERNEL_CHECK();
+}
+
+__global__ __launch_bounds__(256) void k_transpose_kv(const double* __restrict__ lam, int64_t V, int k,
+                                                      double* __restrict__ out, int32_t* __restrict__ idx) {
+  const int64_t total = V * k;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int t = (int)(e / V);
+    const int64_t v = e - (int64_t)t * V;
+    out[e] = lam[v * k + t];
+    idx[e] = (int32_t)v;
+  }
+}
+
+void launch_transpose_kv(hipStream_t s, const double* lam, int64_t V, int k, double* out_kv,
+                         int32_t* idx_kv) {
+  k_transpose_kv<<<4096, 256, 0, s>>>(lam, V, k, out_kv, idx_kv);
+  KERNEL_CHECK();
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_unscale_stat(const T* __restrict__ stat,
+                                                      const double* __restrict__ logscale, int64_t V,
+                                                      int k, int kp, double* __restrict__ out) {
+  const int64_t total = V * k;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t v = e / k;
+    const int t = (int)(e - v * k);
+    out[e] = (double)stat[v * kp + t] * exp(-logscale[v]);
+  }
+}
+
+template <typename T>
+void launch_unscale_stat(hipStream_t s, const T* stat, const double* logscale, int64_t V, int k,
+                         int kp, double* out_vk) {
+  k_unscale_stat<T><<<4096, 256, 0, s>>>(stat, logscale, V, k, kp, out_vk);
+  KERNEL_CHECK();
+}
+
+#define STC_INSTANTIATE(T)                                                                        \
+  template size_t estep_lds_bytes<T>(int, int, int);                                              \
+  template int estep_lds_rows<T>(int, int, int);                                                  \
+  template void launch_estep<T>(hipStream_t, const EStepArgs<T>&, bool, bool);                    \
+  template void launch_sstats<T>(hipStream_t, const uint32_t*, const uint32_t*, int64_t, const T*, \
+                                 const int32_t*, const T*, int, T*, T*, T*);                      \
+  template void launch_lambda_update<T>(hipStream_t, double*, const T*, const T*, int64_t, int, int, \
+                                        double, double, double, const double*, double*, int64_t); \
+  template void launch_expelogbeta<T>(hipStream_t, const double*, const double*, int64_t, int, int, \
+                                      const double*, T*, double*);                               \
+  template void launch_logphat<T>(hipStream_t, const T*, const int32_t*, int64_t, int, double*);  \
+  template void launch_topics_bound<T>(hipStream_t, const double*, const double*, int64_t, int,   \
+                                       double, double*, int64_t);                                 \
+  template void launch_sum_vals<T>(hipStream_t, const T*, int64_t, double*);                      \
+  template void launch_unscale_stat<T>(hipStream_t, const T*, const double*, int64_t, int, int, double*);
+
+STC_INSTANTIATE(float)
+STC_INSTANTIATE(double)
+
+}  // namespace lda
+}  // namespace stc

@@ -1,0 +1,100 @@
+// lda_kernels.h — host-side launch API of the online-LDA kernels (lda.hip).
+#pragma once
+
+#include "stc_internal.h"
+
+namespace stc {
+namespace lda {
+
+constexpr int kBlock = 256;           // threads per E-step workgroup (4 waves of 64)
+constexpr int kLdsBudget = 80 * 1024; // dynamic LDS per E-step workgroup → 2 workgroups / CU
+constexpr int kChunk = 256;           // sorted entries per wave in the sstats segmented SpMM
+constexpr int kRowsPerBlock = 64;     // terms per workgroup in the λ update
+
+// Everything the E-step kernel reads/writes.  T = the E-step arithmetic type (float/double).
+template <typename T>
+struct EStepArgs {
+  int k = 0, kp = 0, P = 0;            // topics, global row pitch of Bp, LDS row pitch
+  int lds_rows = 0;                    // docs with nnz <= lds_rows keep their block in LDS
+  const int64_t* indptr = nullptr;     // documents (CSR rows)
+  const int32_t* indices = nullptr;
+  const T* values = nullptr;
+  const int32_t* batch = nullptr;      // batch member → row (nullptr: member i is row i)
+  int64_t n = 0;                       // members
+  const int64_t* bptr = nullptr;       // member → first entry slot (n+1)
+  const T* Bp = nullptr;               // V×kp  row-scaled expElogβ'
+  const double* logscale = nullptr;    // V     m_v (BOUND)
+  const double* alpha = nullptr;       // k
+  const T* gamma0 = nullptr;           // n×k or nullptr (counter RNG)
+  uint64_t seed = 0;
+  int64_t iteration = 0;
+  int rank = 0;
+  int key_mode = 0;                    // 0: train_doc_key(iteration, rank, i); 1: doc_id_base + row
+  int64_t doc_id_base = 0;
+  double gamma_shape = 100.0;
+  int max_iter = 100000;
+  // outputs
+  T* gamma = nullptr;                  // n×k (optional)
+  T* eth = nullptr;                    // n×kp scaled exp(E[log θ]) (STATS)
+  T* elogth = nullptr;                 // n×k  E[log θ] (STATS: logphat)
+  T* r = nullptr;                      // entry slots: cts/φ' (always)
+  uint32_t* keys = nullptr;            // entry slots: term id (STATS)
+  uint32_t* vals = nullptr;            // entry slots: slot index (STATS)
+  int32_t* edoc = nullptr;             // entry slots: member index (STATS)
+  int32_t* iters = nullptr;            // n (optional)
+  int32_t* nonempty = nullptr;         // n (optional)
+  double* bound = nullptr;             // n (BOUND)
+};
+
+template <typename T>
+size_t estep_lds_bytes(int kp, int lds_rows, int P);
+template <typename T>
+int estep_lds_rows(int k, int kp, int P);
+template <typename T>
+void launch_estep(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound);
+
+template <typename T>
+void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint32_t* svals, int64_t E,
+                   const T* r, const int32_t* edoc, const T* eth, int kp, T* stat, T* headbuf,
+                   T* tailbuf);
+
+template <typename T>
+void launch_lambda_update(hipStream_t s, double* lam, const T* stat, const T* Bp, int64_t V, int k,
+                          int kp, double rho, double scale, double eta, const double* gate,
+                          double* colpart, int64_t nblocks);
+void launch_colsum_lambda(hipStream_t s, const double* lam, int64_t V, int k, double* colpart,
+                          int64_t nblocks);
+void launch_colsum_reduce(hipStream_t s, const double* colpart, int64_t nblocks, int k,
+                          const double* gate, double* colsum);
+template <typename T>
+void launch_expelogbeta(hipStream_t s, const double* lam, const double* colsum, int64_t V, int k,
+                        int kp, const double* gate, T* Bp, double* logscale);
+template <typename T>
+void launch_logphat(hipStream_t s, const T* elogth, const int32_t* nonempty, int64_t n, int k,
+                    double* small /* k+1 */);
+void launch_update_alpha(hipStream_t s, double* alpha, const double* small, int k, double rho);
+void launch_init_lambda(hipStream_t s, double* lam, int64_t V, int k, uint64_t seed, double shape);
+template <typename T>
+void launch_topics_bound(hipStream_t s, const double* lam, const double* colsum, int64_t V, int k,
+                         double eta, double* partials, int64_t nblocks);
+void launch_sum_f64(hipStream_t s, const double* x, int64_t n, double* out);
+template <typename T>
+void launch_sum_vals(hipStream_t s, const T* x, int64_t n, double* out);
+void launch_iter_stats(hipStream_t s, const int32_t* iters, const int32_t* nonempty, int64_t n,
+                       int max_iter, int64_t* out4 /* sum, max, caphits, nonempty */,
+                       int64_t* cum2 /* += Σiters, caphits; may be null */);
+void launch_batch_nnz(hipStream_t s, const int64_t* indptr, const int32_t* batch, int64_t n,
+                      int64_t* nnz_out);
+void launch_sample(hipStream_t s, const int64_t* indptr, int64_t D, double fraction, int with_repl,
+                   uint64_t seed, int64_t iteration, int rank, int32_t* counts, int64_t* weights);
+void launch_fill_batch(hipStream_t s, const int64_t* indptr, int64_t D, const int32_t* counts,
+                       const int32_t* count_off, const int64_t* weight_off, int32_t* batch,
+                       int64_t* bptr);
+void launch_transpose_kv(hipStream_t s, const double* lam, int64_t V, int k, double* out_kv,
+                         int32_t* idx_kv);
+template <typename T>
+void launch_unscale_stat(hipStream_t s, const T* stat, const double* logscale, int64_t V, int k,
+                         int kp, double* out_vk);
+
+}  // namespace lda
+}  // namespace stc

@@ -1,0 +1,218 @@
+// stc_internal.h — internals shared by the libstc.so translation units (gfx950 / HIP only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "stc.h"
+
+namespace stc {
+
+// ---------------------------------------------------------------------------------------
+// Errors: every entry point runs inside guard(); failures throw stc::Error and come back to
+// the caller as a status code + thread-local message (stc_last_error).  Never abort().
+// ---------------------------------------------------------------------------------------
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void set_last_error(const std::string& msg);
+
+template <typename F>
+int guard(F&& f) {
+  try {
+    f();
+    return STC_OK;
+  } catch (const Error& e) {
+    set_last_error(e.what());
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_last_error("host out of memory");
+    return STC_ERR_OOM;
+  } catch (const std::exception& e) {
+    set_last_error(e.what());
+    return STC_ERR_STATE;
+  }
+}
+
+#define STC_REQUIRE(cond, msg)                                                          \
+  do {                                                                                  \
+    if (!(cond)) throw ::stc::Error(STC_ERR_INVALID_ARG, std::string("requirement failed: ") + (msg)); \
+  } while (0)
+
+#define HIP_CHECK(expr)                                                                 \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      int c_ = (e_ == hipErrorOutOfMemory) ? STC_ERR_OOM : STC_ERR_HIP;                 \
+      throw ::stc::Error(c_, std::string(#expr) + ": " + hipGetErrorString(e_) + " @" + \
+                                 __FILE__ + ":" + std::to_string(__LINE__));            \
+    }                                                                                   \
+  } while (0)
+
+#define RCCL_CHECK(expr)                                                                \
+  do {                                                                                  \
+    ncclResult_t r_ = (expr);                                                           \
+    if (r_ != ncclSuccess)                                                              \
+      throw ::stc::Error(STC_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+#define KERNEL_CHECK() HIP_CHECK(hipGetLastError())
+
+// ---------------------------------------------------------------------------------------
+// Device buffer (grow-only scratch).  Allocation happens only outside the launch sequence.
+// ---------------------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  void reserve(size_t n) {
+    if (n <= bytes) return;
+    release();
+    size_t want = n < 256 ? 256 : n;
+    HIP_CHECK(hipMalloc(&p, want));
+    bytes = want;
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+// ---------------------------------------------------------------------------------------
+// Context: one device, one stream, optional RCCL communicator.
+// ---------------------------------------------------------------------------------------
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  int n_ranks = 1;
+  int rank = 0;
+  void use() const { HIP_CHECK(hipSetDevice(device)); }
+};
+
+struct DCsr {
+  Ctx* ctx = nullptr;
+  int64_t rows = 0, cols = 0, nnz = 0;
+  int dtype = STC_F64;
+  DevBuf indptr;   // int64[rows+1]
+  DevBuf indices;  // int32[nnz]
+  DevBuf values;   // float/double[nnz]
+};
+
+// ---------------------------------------------------------------------------------------
+// Counter-based RNG shared bit-for-bit with oracle/oracle.py (splitmix64 streams, uniform
+// in (0,1) from the top 53 bits, Box–Muller normal, Marsaglia–Tsang Gamma(shape, 1/shape)).
+// ---------------------------------------------------------------------------------------
+__host__ __device__ inline uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ inline uint64_t doc_stream(uint64_t seed, uint64_t key) {
+  return splitmix64(seed ^ splitmix64(key));
+}
+__host__ __device__ inline double rng_uniform(uint64_t stream, uint64_t ctr) {
+  uint64_t x = splitmix64(stream + ctr * 0xD1B54A32D192ED03ull);
+  return ((double)(x >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+}
+__host__ __device__ inline double gamma_sample(uint64_t stream, int topic, double shape) {
+  const double d = shape - 1.0 / 3.0;
+  const double c = 1.0 / sqrt(9.0 * d);
+  double v = 1.0;
+  for (int attempt = 0; attempt < 64; ++attempt) {
+    const uint64_t base = ((uint64_t)topic << 8) + 3u * (uint64_t)attempt;
+    const double u1 = rng_uniform(stream, base);
+    const double u2 = rng_uniform(stream, base + 1);
+    const double x = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+    v = 1.0 + c * x;
+    if (v <= 0.0) continue;
+    v = v * v * v;
+    const double u = rng_uniform(stream, base + 2);
+    if (u < 1.0 - 0.0331 * (x * x) * (x * x)) break;
+    if (log(u) < 0.5 * x * x + d * (1.0 - v + log(v))) break;
+  }
+  return d * v / shape;
+}
+// γ₀ key of a training minibatch member (mirrors oracle.train_doc_key)
+__host__ __device__ inline uint64_t train_doc_key(int64_t iteration, int rank, int64_t pos) {
+  return (((uint64_t)iteration & 0xFFFFFFull) << 40) | (((uint64_t)rank & 0xFFull) << 32) |
+         ((uint64_t)pos & 0xFFFFFFFFull);
+}
+
+// ---------------------------------------------------------------------------------------
+// Breeze 0.13.2 digamma / trigamma (recurrence to x > 5 + asymptotic series).
+// ---------------------------------------------------------------------------------------
+template <typename R>
+__host__ __device__ inline R digamma_t(R x) {
+  R r = 0;
+  while (x <= R(5)) {
+    r -= R(1) / x;
+    x += R(1);
+  }
+  const R f = R(1) / (x * x);
+  const R t = f * (R(-1.0 / 12.0) + f * (R(1.0 / 120.0) + f * (R(-1.0 / 252.0) + f * (R(1.0 / 240.0) +
+              f * (R(-1.0 / 132.0) + f * (R(691.0 / 32760.0) + f * (R(-1.0 / 12.0) + f * R(3617.0) / R(8160.0))))))));
+  return r + log(x) - R(0.5) / x + t;
+}
+__host__ __device__ inline double trigamma_d(double x) {
+  double r = 0;
+  while (x <= 5.0) {
+    r += 1.0 / (x * x);
+    x += 1.0;
+  }
+  const double f = 1.0 / (x * x);
+  const double t = f * (1 / 6.0 + f * (-1 / 30.0 + f * (1 / 42.0 + f * (-1 / 30.0 + f * (5 / 66.0 +
+                   f * (-691 / 2730.0 + f * (7 / 6.0 - f * 3617 / 510.0)))))));
+  return r + 1.0 / x + f / 2.0 + t / x;
+}
+
+// ---------------------------------------------------------------------------------------
+// Wave64 / block reductions
+// ---------------------------------------------------------------------------------------
+template <typename R>
+__device__ inline R wave_sum(R v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <typename R>
+__device__ inline R wave_max(R v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// kernels-side entry points (implemented in the .hip files)
+namespace hashing {
+void hash_tokens(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t n_tok,
+                 int32_t num_features, int variant, int32_t* d_idx);
+void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t n_tok,
+               const int64_t* d_doc_off, int64_t n_docs, int32_t num_features, int binary,
+               int variant, int value_dtype, DCsr& out);
+}  // namespace hashing
+namespace idf {
+void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df /* cols */);
+void finalize(Ctx& c, const int64_t* d_df, int64_t cols, int64_t m, int64_t min_df, double* d_idf);
+void transform(Ctx& c, DCsr& m, const double* d_idf, double zero_floor);
+}  // namespace idf
+
+}  // namespace stc

@@ -1,0 +1,18 @@
+"""stc — MI355X-native HashingTF → IDF → online-LDA hot path of borisfoko/Spark-Text-Clustering.
+
+The compute lives in libstc.so (HIP kernels for gfx950 behind the C ABI in include/stc.h); this
+package is the host-side mirror of the Spark ML interface the reference's pipeline uses.
+"""
+from ._lib import (STC_F32, STC_F64, STC_HASH_SPARK24, STC_HASH_STANDARD, STC_LAYOUT_KV,
+                   STC_LAYOUT_VK, StcError, StcIllegalArgument, load)
+from .clustering import (LDA, ML_LDA_DEFAULT_SEED, LdaHandle, LDAModel, MllibLDA, OnlineLDAOptimizer,
+                         reference_mini_batch_fraction)
+from .core import Context, CsrMatrix, DeviceCsr
+from .feature import IDF, HashingTF, IDFModel, encode_tokens
+
+__all__ = [
+    "Context", "CsrMatrix", "DeviceCsr", "HashingTF", "IDF", "IDFModel", "encode_tokens", "LDA",
+    "LDAModel", "LdaHandle", "MllibLDA", "OnlineLDAOptimizer", "ML_LDA_DEFAULT_SEED",
+    "reference_mini_batch_fraction", "StcError", "StcIllegalArgument", "load", "STC_F32", "STC_F64",
+    "STC_HASH_STANDARD", "STC_HASH_SPARK24", "STC_LAYOUT_VK", "STC_LAYOUT_KV",
+]

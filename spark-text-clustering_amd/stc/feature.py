@@ -1,0 +1,169 @@
+"""HashingTF / IDF / IDFModel with the Spark ML surface, backed by the HIP kernels K1–K5.
+
+Mirrors ``org.apache.spark.ml.feature.{HashingTF, IDF, IDFModel}`` ([U] spark 2.4.3, build.sbt:10)
+and the mllib ``IDF(minDocFreq)`` the reference calls at LDAClustering.scala:177.  Parameter names,
+defaults and validation follow Spark (numFeatures = 2^18, binary = false, minDocFreq = 0).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+from .core import Context, CsrMatrix, DeviceCsr
+
+_VARIANTS = {"murmur3": L.STC_HASH_STANDARD, "standard": L.STC_HASH_STANDARD,
+             "spark24": L.STC_HASH_SPARK24, "murmur3-spark24": L.STC_HASH_SPARK24}
+
+
+def encode_tokens(docs):
+    """list[list[str|bytes]] → (utf8 uint8 blob, tok_off int64[n_tok+1], doc_off int64[n_docs+1])."""
+    parts, tok_len, doc_len = [], [], []
+    for toks in docs:
+        doc_len.append(len(toks))
+        for t in toks:
+            b = t.encode("utf-8") if isinstance(t, str) else bytes(t)
+            parts.append(b)
+            tok_len.append(len(b))
+    blob = np.frombuffer(b"".join(parts), np.uint8) if parts else np.zeros(0, np.uint8)
+    tok_off = np.zeros(len(tok_len) + 1, np.int64)
+    np.cumsum(tok_len, out=tok_off[1:])
+    doc_off = np.zeros(len(doc_len) + 1, np.int64)
+    np.cumsum(doc_len, out=doc_off[1:])
+    return np.ascontiguousarray(blob), tok_off, doc_off
+
+
+class HashingTF:
+    """Maps a sequence of terms to their term frequencies using the hashing trick.
+
+    numFeatures (default 2^18) buckets; bucket = nonNegativeMod(murmur3_x86_32(utf8(term), 42),
+    numFeatures).  ``hashAlgorithm="murmur3"`` is the standard MurmurHash3_x86_32 tail (Spark 3.x);
+    ``"murmur3-spark24"`` reproduces Spark 2.4's per-byte tail (the version build.sbt pins).
+    """
+
+    def __init__(self, numFeatures=1 << 18, binary=False, hashAlgorithm="murmur3",
+                 inputCol=None, outputCol=None, ctx: Context | None = None):
+        self.setNumFeatures(numFeatures)
+        self.setBinary(binary)
+        if hashAlgorithm not in _VARIANTS:
+            raise ValueError(f"HashingTF does not support hash function: {hashAlgorithm}")
+        self.hashAlgorithm = hashAlgorithm
+        self.inputCol, self.outputCol = inputCol, outputCol
+        self._ctx = ctx
+
+    @property
+    def ctx(self):
+        return self._ctx or Context.get()
+
+    def setNumFeatures(self, n):
+        if int(n) <= 0:
+            raise ValueError(f"numFeatures must be > 0 but got {n}")
+        self.numFeatures = int(n)
+        return self
+
+    def getNumFeatures(self):
+        return self.numFeatures
+
+    def setBinary(self, b):
+        self.binary = bool(b)
+        return self
+
+    def getBinary(self):
+        return self.binary
+
+    def indexOf(self, term) -> int:
+        """Bucket index of one term (mllib HashingTF.indexOf)."""
+        return int(self.indices_of([term])[0])
+
+    def indices_of(self, terms):
+        blob, tok_off, _ = encode_tokens([list(terms)])
+        out = np.zeros(len(terms), np.int32)
+        L.check(self.ctx.lib.stc_hash_tokens(self.ctx.handle, L.ptr(blob, C.c_uint8), blob.size,
+                                             L.ptr(tok_off, C.c_int64), len(terms), self.numFeatures,
+                                             _VARIANTS[self.hashAlgorithm], L.ptr(out, C.c_int32)))
+        return out
+
+    def transform_device(self, docs, value_dtype=L.STC_F64, encoded=None) -> DeviceCsr:
+        """Term frequencies of every doc, left resident in HBM (for IDF/LDA on the same GPU)."""
+        blob, tok_off, doc_off = encoded if encoded is not None else encode_tokens(docs)
+        h = C.c_void_p()
+        L.check(self.ctx.lib.stc_hashing_tf_dev(
+            self.ctx.handle, L.ptr(blob, C.c_uint8), blob.size, L.ptr(tok_off, C.c_int64),
+            tok_off.size - 1, L.ptr(doc_off, C.c_int64), doc_off.size - 1, self.numFeatures,
+            int(self.binary), _VARIANTS[self.hashAlgorithm], int(value_dtype), C.byref(h)))
+        return DeviceCsr(self.ctx, h)
+
+    def transform(self, docs, encoded=None) -> CsrMatrix:
+        d = self.transform_device(docs, L.STC_F64, encoded)
+        try:
+            return d.download()
+        finally:
+            d.free()
+
+
+class IDFModel:
+    """Fitted IDF: ``idf`` (float64[numFeatures]), ``docFreq`` (int64), ``numDocs``."""
+
+    def __init__(self, idf, docFreq, numDocs, ctx: Context | None = None):
+        self.idf = np.asarray(idf, np.float64)
+        self.docFreq = np.asarray(docFreq, np.int64)
+        self.numDocs = int(numDocs)
+        self._ctx = ctx
+
+    @property
+    def ctx(self):
+        return self._ctx or Context.get()
+
+    def transform_device(self, tf: DeviceCsr, zero_floor=0.0) -> DeviceCsr:
+        """In place on a device CSR.  zero_floor=1e-4 reproduces LDAClustering.scala:184-187."""
+        idf = L.as_f64(self.idf)
+        if tf.num_cols != idf.size:
+            raise ValueError(f"vector size {tf.num_cols} does not match IDF size {idf.size}")
+        L.check(self.ctx.lib.stc_idf_transform(self.ctx.handle, tf.handle, L.ptr(idf, C.c_double),
+                                               float(zero_floor)))
+        return tf
+
+    def transform(self, tf: CsrMatrix, zero_floor=0.0) -> CsrMatrix:
+        d = DeviceCsr.upload(self.ctx, tf, L.STC_F64)
+        try:
+            return self.transform_device(d, zero_floor).download()
+        finally:
+            d.free()
+
+
+class IDF:
+    """Compute the Inverse Document Frequency of a collection of term-frequency vectors."""
+
+    def __init__(self, minDocFreq=0, inputCol=None, outputCol=None, ctx: Context | None = None):
+        self.setMinDocFreq(minDocFreq)
+        self.inputCol, self.outputCol = inputCol, outputCol
+        self._ctx = ctx
+
+    @property
+    def ctx(self):
+        return self._ctx or Context.get()
+
+    def setMinDocFreq(self, v):
+        if int(v) < 0:
+            raise ValueError(f"minDocFreq must be >= 0 but got {v}")
+        self.minDocFreq = int(v)
+        return self
+
+    def getMinDocFreq(self):
+        return self.minDocFreq
+
+    def fit_device(self, tf: DeviceCsr) -> IDFModel:
+        idf = np.zeros(tf.num_cols, np.float64)
+        df = np.zeros(tf.num_cols, np.int64)
+        m = C.c_int64()
+        L.check(self.ctx.lib.stc_idf_fit(self.ctx.handle, tf.handle, self.minDocFreq,
+                                         L.ptr(idf, C.c_double), L.ptr(df, C.c_int64), C.byref(m)))
+        return IDFModel(idf, df, m.value, self._ctx)
+
+    def fit(self, tf: CsrMatrix) -> IDFModel:
+        d = DeviceCsr.upload(self.ctx, tf, L.STC_F64)
+        try:
+            return self.fit_device(d)
+        finally:
+            d.free()

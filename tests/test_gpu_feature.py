@@ -1,0 +1,120 @@
+"""GPU parity: HashingTF (K1/K2, bit-exact) and IDF (K3–K5) through the C ABI vs the oracle and
+the reference's own saved TF·IDF edges (tests/golden/{en,ge}_idf.npz)."""
+import numpy as np
+import pytest
+
+from helpers import golden_npz, random_tokens
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("algo,variant", [("murmur3", 0), ("murmur3-spark24", 1)])
+def test_hash_tokens_bit_exact(ctx, oracle, algo, variant):
+    import stc
+
+    rng = np.random.default_rng(1)
+    docs = random_tokens(rng, 60)
+    terms = [t for d in docs for t in d]
+    for nf in (1 << 18, 1000, 7, 1 << 20):
+        htf = stc.HashingTF(numFeatures=nf, hashAlgorithm=algo, ctx=ctx)
+        got = htf.indices_of(terms)
+        exp = [oracle.non_negative_mod(oracle.murmur3_x86_32(t.encode(), 42, variant), nf) for t in terms]
+        assert np.array_equal(got, np.asarray(exp, np.int32)), nf
+
+
+def test_murmur3_known_answers_on_device(ctx):
+    """Public MurmurHash3_x86_32 vectors (seed 42 is Spark's; use numFeatures = 2^31 - 1 to read
+    the non-negative residue of the signed hash)."""
+    import stc
+
+    from oracle import oracle as O
+
+    htf = stc.HashingTF(numFeatures=(1 << 31) - 1, ctx=ctx)
+    words = ["", "a", "ab", "abc", "abcd", "hello", "The quick brown fox jumps over the lazy dog"]
+    got = htf.indices_of(words)
+    for w, g in zip(words, got):
+        assert g == O.non_negative_mod(O.murmur3_x86_32(w.encode(), 42), (1 << 31) - 1)
+
+
+@pytest.mark.parametrize("binary", [False, True])
+@pytest.mark.parametrize("algo,variant", [("murmur3", 0), ("murmur3-spark24", 1)])
+def test_hashing_tf_csr_bit_exact(ctx, oracle, binary, algo, variant):
+    import stc
+
+    rng = np.random.default_rng(2)
+    docs = random_tokens(rng, 300, max_len=80)
+    docs[5] = []  # empty rows are kept (zero-length sparse vectors)
+    docs[17] = ["same"] * 50
+    for nf in (1 << 18, 97):
+        out = stc.HashingTF(numFeatures=nf, binary=binary, hashAlgorithm=algo, ctx=ctx).transform(docs)
+        ip, ix, vv = oracle.hashing_tf(docs, nf, binary, variant)
+        assert np.array_equal(out.indptr, ip)
+        assert np.array_equal(out.indices, ix)
+        assert np.array_equal(out.values, vv)
+
+
+def test_hashing_tf_all_empty(ctx):
+    import stc
+
+    out = stc.HashingTF(ctx=ctx).transform([[], [], []])
+    assert out.shape == (3, 1 << 18) and out.nnz == 0
+
+
+@pytest.mark.parametrize("tag", ["en", "ge"])
+def test_idf_reference_edges_bit_exact(ctx, oracle, tag):
+    """IDF(2).fit + the 1e-4 floor (LDAClustering.scala:177-188) reproduce every TF·IDF value the
+    reference stored in its saved model, bit for bit."""
+    import stc
+
+    f = golden_npz(f"{tag}_idf.npz")
+    V = int(f["vocab_size"])
+    tf = stc.CsrMatrix(f["indptr"], f["indices"], f["tf"].astype(np.float64), V)
+    model = stc.IDF(minDocFreq=int(f["min_doc_freq"]), ctx=ctx).fit(tf)
+    assert model.numDocs == int(f["num_docs"])
+    idf_o, df_o, m_o = oracle.idf_fit(tf.indptr, tf.indices, tf.values, V, int(f["min_doc_freq"]))
+    assert np.array_equal(model.docFreq, df_o)
+    assert np.max(np.abs(model.idf - idf_o) / np.maximum(np.abs(idf_o), 1e-300)) <= 1e-15
+    out = model.transform(tf, zero_floor=1e-4)
+    assert np.array_equal(out.indices, tf.indices)
+    rel = np.abs(out.values - f["tfidf"]) / f["tfidf"]
+    # device log() vs the JVM's: at most an ulp apart; north star asks for 1e-6 relative
+    assert rel.max() <= 1e-15, rel.max()
+    print(f"{tag}: {np.mean(out.values == f['tfidf']):.6f} of the stored edges reproduced bit for bit")
+
+
+def test_idf_min_doc_freq_and_stock_transform(ctx, oracle):
+    import stc
+
+    rng = np.random.default_rng(3)
+    V = 50
+    rows = []
+    for _ in range(40):
+        ids = np.sort(rng.choice(V, size=int(rng.integers(0, 12)), replace=False))
+        vals = rng.integers(0, 4, ids.size).astype(np.float64)  # explicit zeros don't count
+        rows.append((ids, vals))
+    tf = stc.CsrMatrix.from_rows(rows, V)
+    for mdf in (0, 1, 3, 10):
+        m = stc.IDF(minDocFreq=mdf, ctx=ctx).fit(tf)
+        idf_o, df_o, _ = oracle.idf_fit(tf.indptr, tf.indices, tf.values, V, mdf)
+        assert np.array_equal(m.docFreq, df_o)
+        np.testing.assert_allclose(m.idf, idf_o, rtol=1e-15, atol=0)
+        out = m.transform(tf)
+        np.testing.assert_allclose(out.values, oracle.idf_transform(tf.indices, tf.values, idf_o),
+                                   rtol=1e-15, atol=0)
+
+
+def test_pipeline_hashing_idf_device_resident(ctx, oracle):
+    """HashingTF → IDF with the TF matrix left in HBM (no host round trip between stages)."""
+    import stc
+
+    rng = np.random.default_rng(4)
+    docs = random_tokens(rng, 200, max_len=60)
+    htf = stc.HashingTF(numFeatures=1 << 12, ctx=ctx)
+    d = htf.transform_device(docs)
+    model = stc.IDF(minDocFreq=2, ctx=ctx).fit_device(d)
+    model.transform_device(d)
+    got = d.download()
+    ip, ix, vv = oracle.hashing_tf(docs, 1 << 12)
+    idf_o, _, _ = oracle.idf_fit(ip, ix, vv, 1 << 12, 2)
+    assert np.array_equal(got.indices, ix)
+    np.testing.assert_allclose(got.values, oracle.idf_transform(ix, vv, idf_o), rtol=1e-15, atol=0)
