@@ -1,0 +1,207 @@
+"""Benchmark: online-LDA minibatch steps (E-step + sstats + [RCCL all-reduce] + M-step) on MI355X.
+
+Workload (BASELINE.json configs[1]): synthetic Zipfian corpus, 1M docs × 200 tokens per GPU,
+V = 2^18, online LDA k = 100, subsamplingRate 0.05 (≈50k docs per minibatch per GPU).  A "step" is
+one OnlineLDAOptimizer.next(): device-side membership sampling, the E-step over the minibatch, the
+term-sorted sufficient statistics, the all-reduce (N > 1) and the λ / expElogβ / α update.  The
+corpus is resident in HBM before the timed region.  Weak scaling: every rank owns its own 1M-doc
+shard (corpusSize = N·1M for the λ update), one RCCL all-reduce of k×V sstats per step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--docs D] [--corpus zipf|zipf-lda]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N   (one rank per GPU)
+
+Rank 0 prints ONE JSON line.  value = Σ_ranks minibatch docs in the K timed steps ÷ max-over-ranks
+wall time.  roofline: SURVEY.md §8(d) algorithmic bytes per doc (nnz·(4+4) + 2·nnz·k·4 + 4k) over
+the E-step phase (k_estep + term sort + sstats SpMM kernels, HIP events on the library stream).
+cpu_baseline: the NumPy restatement (oracle/, one core) timed on a bounded sample of the same docs
+at the same model state.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "spark-text-clustering_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--docs", type=int, default=1_000_000, help="documents per GPU")
+    p.add_argument("--tokens", type=int, default=200)
+    p.add_argument("--vocab", type=int, default=1 << 18)
+    p.add_argument("--k", type=int, default=100)
+    p.add_argument("--fraction", type=float, default=0.05)
+    p.add_argument("--corpus", default="zipf", choices=["zipf", "zipf-lda"])
+    p.add_argument("--dtype", default="f32", choices=["f32", "f64"])
+    p.add_argument("--seed", type=int, default=20261015)
+    p.add_argument("--cpu-sample-docs", type=int, default=4000)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def algorithmic_bytes(nnz, k, docs):
+    """ids + counts (4+4 B per nnz), one k-wide fp32 row gathered and one
+    scattered per nnz, γ out (4k B per doc)."""
+    return nnz * 8.0 + 2.0 * nnz * k * 4.0 + docs * 4.0 * k
+
+
+def cpu_baseline(h, corpus, k, n_docs, seed):
+    """Oracle (NumPy, 1 thread) E-step on a bounded sample at the GPU model's current state."""
+    from oracle import oracle as O
+
+    lam = h.topics()                      # V×k
+    alpha = h.alpha()
+    eeb = O.topics_exp_elog_beta(lam)     # Spark's expElogβ (V×k)
+    rng = np.random.default_rng(seed)
+    ids = rng.choice(corpus.num_rows, size=n_docs, replace=False)
+    t0 = time.perf_counter()
+    iters, done = 0, 0
+    for i in ids:  # bounded: stop after ~15 s of CPU work
+        cid, cts = corpus.row(i)
+        g0 = O.gamma_init(seed, int(i), k)
+        _, _, it = O.variational_topic_inference(cid, cts, eeb, alpha, g0)
+        iters += it
+        done += 1
+        if time.perf_counter() - t0 > 15.0:
+            break
+    dt = time.perf_counter() - t0
+    n_docs = done
+    return {"value": n_docs / dt, "unit": "docs/s", "cores": 1, "kind": "port",
+            "sample": f"{n_docs} docs of the same corpus, E-step only (variationalTopicInference), "
+                      f"model state after the timed steps; NumPy oracle/oracle.py, 1 thread; "
+                      f"mean inner iters {iters / n_docs:.1f}; {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        a.gpus = world if world > 1 else a.gpus
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only (uid exchange, barrier, max time)
+
+        dist.init_process_group("gloo")
+    import stc
+    from stc import synth
+
+    ctx = stc.Context(local)
+    if world > 1:
+        obj = [stc.Context.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ctx.comm_init(obj[0], world, rank)
+
+    t0 = time.perf_counter()
+    corpus = synth.make_corpus(a.corpus, a.docs, a.tokens, a.vocab, a.k, a.seed + 7919 * rank)
+    gen_s = time.perf_counter() - t0
+    dcorp = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F32 if a.dtype == "f32" else stc.STC_F64)
+    h = stc.LdaHandle(ctx, a.k, a.vocab, mini_batch_fraction=a.fraction, optimize_doc_concentration=True,
+                      seed=a.seed, dtype=a.dtype)
+    h.set_corpus(dcorp, a.docs * world)
+    h.init_random(a.seed)
+
+    for _ in range(a.warmup):
+        h.next(stats=False)
+    ctx.synchronize()
+    c0 = h.counters()
+    h.enable_timing(True)
+
+    def barrier():
+        ctx.synchronize()
+        try:
+            import torch
+
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+        except Exception:
+            pass
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    t_start = time.perf_counter()
+    for _ in range(a.steps):
+        h.next(stats=False)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    phases = h.phase_times()
+    c1 = h.counters()
+    docs_local = c1["docs"] - c0["docs"]
+    entries_local = c1["entries"] - c0["entries"]
+    iters_local = c1["inner_iters"] - c0["inner_iters"]
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+        s = torch.tensor([docs_local, entries_local, iters_local], dtype=torch.float64)
+        dist.all_reduce(s)
+        docs_all, entries_all, iters_all = (float(x) for x in s)
+    else:
+        docs_all, entries_all, iters_all = float(docs_local), float(entries_local), float(iters_local)
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+        return
+
+    value = docs_all / elapsed
+    estep_ms = phases["estep"] + phases["sstats"]
+    per_step_docs = docs_local / max(1, a.steps)
+    per_step_nnz = entries_local / max(1, a.steps)
+    alg = algorithmic_bytes(per_step_nnz, a.k, per_step_docs)
+    achieved = alg / (estep_ms * 1e-3) / 1e9
+    cpu = None
+    if not a.no_cpu_baseline:
+        cpu = cpu_baseline(h, corpus, a.k, a.cpu_sample_docs, a.seed)
+    line = {
+        "metric": "LDA E-step docs/sec (node) at k=100, V=2^18; % of HBM roofline",
+        "value": value,
+        "unit": "docs/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed * 1e3 / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32" if a.dtype == "f32" else "fp64",
+        "data": f"synthetic {a.corpus} corpus (seeded, generated in {gen_s:.0f} s), resident in HBM",
+        "config": {
+            "workload": f"online LDA minibatch steps: {a.docs} docs x {a.tokens} tokens per GPU, "
+                        f"V={a.vocab}, k={a.k}, subsamplingRate={a.fraction}",
+            "docs_per_gpu": a.docs, "tokens_per_doc": a.tokens, "vocab": a.vocab, "k": a.k,
+            "subsampling_rate": a.fraction, "corpus": a.corpus, "parallelism": f"dp{world}",
+            "mean_nnz_per_doc": entries_all / max(1.0, docs_all),
+            "mean_inner_iters": iters_all / max(1.0, docs_all),
+            "phase_ms": {k: round(v, 4) for k, v in phases.items() if k != "steps"},
+            "estep_only_docs_per_s": per_step_docs * world / (estep_ms * 1e-3),
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "kernel": "E-step phase (k_estep + term radix sort + k_sstats/k_fixup)",
+            "algorithmic_bytes_per_step": alg, "phase_ms_per_step": estep_ms,
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

@@ -34,10 +34,14 @@ struct VecOf<double> {
   static constexpr int W = 2;
 };
 
+// Spark adds 1e-100 to φ = B·eθ (unscaled).  In the row/doc-scaled space that epsilon becomes
+// ε'_n = 1e-100 / (exp(m_v)·exp(max E[log θ])) = exp(LOG_EPS − m_v − lmax): it keeps Spark's
+// behaviour for terms whose unscaled expElogβ underflows (they contribute nothing in Spark).
+constexpr double LOG_EPS = -230.25850929940458;  // ln(1e-100)
 template <typename T>
-__device__ __forceinline__ T eps_phi() { return T(1e-30); }
+__device__ __forceinline__ T eps_floor() { return T(1.17549435e-38); }  // FLT_MIN (f32 only)
 template <>
-__device__ __forceinline__ double eps_phi<double>() { return 1e-100; }
+__device__ __forceinline__ double eps_floor<double>() { return 0.0; }
 
 template <typename T, typename VT>
 __device__ __forceinline__ T hsum(VT v);
@@ -85,7 +89,7 @@ size_t estep_lds_bytes(int kp, int lds_rows, int P) {
   b += (size_t)part_elems<T>(kp) * sizeof(T);      // partial column sums
   b += 16 * sizeof(double);                        // reduction scratch
   b += (size_t)lds_rows * sizeof(int32_t);         // ids   (lds_rows % 4 == 0)
-  b += 2 * (size_t)lds_rows * sizeof(T);           // cts, r
+  b += 3 * (size_t)lds_rows * sizeof(T);           // cts, r, ln(1e-100) − m_v
   b += (size_t)lds_rows * P * sizeof(T);           // the document block B
   return b;
 }
@@ -94,7 +98,7 @@ template <typename T>
 int estep_lds_rows(int k, int kp, int P) {
   (void)k;
   const size_t fixed = estep_lds_bytes<T>(kp, 0, P);
-  const size_t per_row = sizeof(int32_t) + 2 * sizeof(T) + (size_t)P * sizeof(T);
+  const size_t per_row = sizeof(int32_t) + 3 * sizeof(T) + (size_t)P * sizeof(T);
   if (fixed >= (size_t)kLdsBudget) return 0;
   int rows = (int)(((size_t)kLdsBudget - fixed) / per_row);
   return rows & ~3;
@@ -123,7 +127,8 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
   int32_t* s_ids = reinterpret_cast<int32_t*>(s_red + 16);
   T* s_cts = reinterpret_cast<T*>(s_ids + rows_cap);
   T* s_r = s_cts + rows_cap;
-  T* s_B = s_r + rows_cap;
+  T* s_lse = s_r + rows_cap;
+  T* s_B = s_lse + rows_cap;
 
   const int32_t* ids = LDS ? s_ids : a.indices + s0;
   const T* cts = LDS ? s_cts : a.values + s0;
@@ -137,6 +142,7 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
     if (LDS) {
       s_ids[n] = id;
       s_cts[n] = c;
+      s_lse[n] = (T)(LOG_EPS - a.logscale[id]);
     }
     nz |= (c != T(0));
   }
@@ -194,6 +200,7 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
     s_gam[t] = g;
   }
   block_reduce3(gsum, dummy, gmax, s_red);
+  T lmax = digamma_t<T>((T)gmax) - digamma_t<T>((T)gsum);  // max_t E[log θ_t]
   {
     const T psimax = digamma_t<T>((T)gmax);
     for (int t = tid; t < kp; t += kBlock)
@@ -213,11 +220,13 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
       VT acc = (VT)T(0);
       for (int c = 0; c < ncg; ++c)
         acc += *reinterpret_cast<const VT*>(Brow + c * W) * *reinterpret_cast<const VT*>(s_eth + c * W);
-      const T phi = hsum<T, VT>(acc) + eps_phi<T>();
+      const T dot = hsum<T, VT>(acc);
+      const T lse = LDS ? s_lse[n] : (T)(LOG_EPS - a.logscale[ids[n]]);
+      const T phi = dot + fmax(exp_t(lse - lmax), eps_floor<T>());
       const T cn = cts[n];
       rr[n] = cn / phi;
-      if (BOUND && (done || it >= a.max_iter) && cn != T(0)) {
-        b_tok += (double)cn * ((double)log(phi) + a.logscale[ids[n]]);
+      if (BOUND && (done || it >= a.max_iter) && cn != T(0)) {  // logSumExp: no epsilon
+        b_tok += (double)cn * ((double)log(fmax(dot, eps_floor<T>())) + a.logscale[ids[n]]);
         c_tok += (double)cn;
       }
     }
@@ -254,6 +263,7 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
 
     // Phase D: eθ' = exp(ψ(γ) − ψ(max γ)) ; meanGammaChange = Σ|Δγ| / k
     const T psimax = digamma_t<T>((T)gmax);
+    lmax = psimax - digamma_t<T>((T)gsum);
     for (int t = tid; t < k; t += kBlock) s_eth[t] = exp_t(digamma_t<T>(s_gam[t]) - psimax);
     ++it;
     done = dsum / (double)k <= 1e-3;
