@@ -10,7 +10,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <memory>
+#include <type_traits>
 
 #include "lda_kernels.h"
 
@@ -44,9 +46,11 @@ struct stc_lda {
   int64_t nblocks_m = 0;
 
   DevBuf lam, Bp, logscale, colsum, colpart, alpha, small, scal;
-  DevBuf batch, bptr, bnnz, g0, gamma, eth, elogth, iters, nonempty, r, keys, vals, skeys, svals,
-      edoc, stat, headbuf, tailbuf, sort_tmp, scan_tmp, stats4, cum2, bound, dtmp;
-  DevBuf s_counts, s_weights, s_cincl, s_wincl;
+  DevBuf batch_raw, batch, orig, flags, sincl, bptr, bnnz, nnzp, g0, gamma, eth, elogth, iters,
+      nonempty, r, keys, vals, skeys, svals, edoc, stat, headbuf, tailbuf, sort_tmp, scan_tmp,
+      stats4, cum2, bound, dtmp;
+  DevBuf s_counts, s_weights, s_short, s_cincl, s_wincl, s_sincl;
+  int64_t wave_cap = 0;  // docs with nnz <= wave_cap run the wave-per-document E-step
 
   bool timing = false;
   hipEvent_t ev[2][6] = {};
@@ -116,9 +120,14 @@ void refresh(stc_lda& L) {
 template <typename T>
 void ensure_batch(stc_lda& L, int64_t n, int64_t E) {
   const size_t ts = sizeof(T);
+  L.batch_raw.reserve(4 * (n + 1));
   L.batch.reserve(4 * (n + 1));
+  L.orig.reserve(4 * (n + 1));
+  L.flags.reserve(4 * (n + 1));
+  L.sincl.reserve(4 * (n + 1));
   L.bptr.reserve(8 * (n + 1));
   L.bnnz.reserve(8 * (n + 1));
+  L.nnzp.reserve(8 * (n + 1));
   L.gamma.reserve(ts * n * L.k);
   L.eth.reserve(ts * n * L.kp);
   L.elogth.reserve(ts * n * L.k);
@@ -139,28 +148,44 @@ void ensure_batch(stc_lda& L, int64_t n, int64_t E) {
                                                (int)std::max<int64_t>(E, 1), 0, bits_for(L.V),
                                                L.ctx->stream));
   L.sort_tmp.reserve(tb);
-  size_t sb = 0;
-  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, sb, L.bnnz.as<int64_t>(), L.bptr.as<int64_t>() + 1,
-                                             (int)std::max<int64_t>(n, 1), L.ctx->stream));
-  L.scan_tmp.reserve(sb);
 }
 
-// entry offsets of the batch members: bptr[0] = 0, bptr[i+1] = Σ nnz; returns E (syncs)
-int64_t batch_offsets(stc_lda& L, int64_t n) {
-  hipStream_t s = L.ctx->stream;
-  HIP_CHECK(hipMemsetAsync(L.bptr.p, 0, sizeof(int64_t), s));
-  if (n == 0) return 0;
-  lda::launch_batch_nnz(s, L.corpus->indptr.as<int64_t>(), L.batch.as<int32_t>(), n, L.bnnz.as<int64_t>());
+template <typename X>
+void incl_scan(stc_lda& L, const X* in, X* out, int64_t n) {
+  if (n <= 0) return;
   size_t sb = 0;
-  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, sb, L.bnnz.as<int64_t>(), L.bptr.as<int64_t>() + 1,
-                                             (int)n, s));
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, sb, in, out, (int)n, L.ctx->stream));
   L.scan_tmp.reserve(sb);
-  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(L.scan_tmp.p, sb, L.bnnz.as<int64_t>(),
-                                             L.bptr.as<int64_t>() + 1, (int)n, s));
-  int64_t E = 0;
-  HIP_CHECK(hipMemcpyAsync(&E, L.bptr.as<int64_t>() + n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(L.scan_tmp.p, sb, in, out, (int)n, L.ctx->stream));
+}
+
+// bptr[0] = 0, bptr[i+1] = Σ_{j<=i} nnz_p[j]  (entry offsets of the partitioned slots)
+void slot_offsets(stc_lda& L, int64_t n) {
+  HIP_CHECK(hipMemsetAsync(L.bptr.p, 0, sizeof(int64_t), L.ctx->stream));
+  incl_scan<int64_t>(L, L.nnzp.as<int64_t>(), L.bptr.as<int64_t>() + 1, n);
+}
+
+struct Part {
+  int64_t E = 0, n_short = 0;
+};
+
+// Partition members (raw = row ids on device, or nullptr for identity rows) into
+// [nnz <= wave cap | rest] slots: fills L.batch, L.orig, L.nnzp.  One host sync (E, n_short).
+Part partition(stc_lda& L, const int64_t* indptr, const int32_t* raw, int64_t n) {
+  hipStream_t s = L.ctx->stream;
+  Part p;
+  if (n == 0) return p;
+  lda::launch_part_flags(s, indptr, raw, n, L.wave_cap, L.bnnz.as<int64_t>(), L.flags.as<int32_t>());
+  incl_scan<int64_t>(L, L.bnnz.as<int64_t>(), L.bptr.as<int64_t>() + 1, n);  // temp: total E
+  incl_scan<int32_t>(L, L.flags.as<int32_t>(), L.sincl.as<int32_t>(), n);
+  int32_t ns = 0;
+  HIP_CHECK(hipMemcpyAsync(&p.E, L.bptr.as<int64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(&ns, L.sincl.as<int32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  return E;
+  p.n_short = ns;
+  lda::launch_part_scatter(s, raw, L.bnnz.as<int64_t>(), n, L.flags.as<int32_t>(), L.sincl.as<int32_t>(),
+                           L.batch.as<int32_t>(), L.orig.as<int32_t>(), L.nnzp.as<int64_t>());
+  return p;
 }
 
 template <typename T>
@@ -180,6 +205,27 @@ lda::EStepArgs<T> estep_args(stc_lda& L) {
   return a;
 }
 
+// wave kernel on slots [0, n_short), workgroup kernel on [n_short, n)
+template <typename T>
+void launch_split(stc_lda& L, lda::EStepArgs<T> a, int64_t n, int64_t n_short, bool stats, bool bound) {
+  hipStream_t s = L.ctx->stream;
+  if constexpr (std::is_same<T, float>::value) {
+    if (n_short > 0) {
+      lda::EStepArgs<float> w = a;
+      w.slot0 = 0;
+      w.n = n_short;
+      lda::launch_estep_wave(s, w, stats, bound);
+    }
+  } else {
+    STC_REQUIRE(n_short == 0, "wave kernel is fp32-only");
+  }
+  if (n > n_short) {
+    a.slot0 = n_short;
+    a.n = n - n_short;
+    lda::launch_estep<T>(s, a, stats, bound);
+  }
+}
+
 template <typename T>
 const T* upload_gamma0(stc_lda& L, const double* gamma0, int64_t n) {
   if (!gamma0 || n == 0) return nullptr;
@@ -194,17 +240,17 @@ const T* upload_gamma0(stc_lda& L, const double* gamma0, int64_t n) {
   return L.g0.as<T>();
 }
 
-// E-step over the n batch members already in L.batch / L.bptr, then the term-sorted sstats SpMM
-// into L.stat (V×kp, row-scaled) and logphat/non-empty count into L.small.
+// E-step over the n partitioned slots (L.batch / L.orig / L.bptr), then the term-sorted sstats
+// SpMM into L.stat (V×kp, row-scaled) and logphat / non-empty count into L.small.
 template <typename T>
-void estep_and_stats(stc_lda& L, int64_t n, int64_t E, const T* g0, int64_t iteration) {
+void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T* g0, int64_t iteration) {
   hipStream_t s = L.ctx->stream;
   lda::EStepArgs<T> a = estep_args<T>(L);
   a.indptr = L.corpus->indptr.as<int64_t>();
   a.indices = L.corpus->indices.as<int32_t>();
   a.values = L.corpus->values.as<T>();
   a.batch = L.batch.as<int32_t>();
-  a.n = n;
+  a.orig = L.orig.as<int32_t>();
   a.bptr = L.bptr.as<int64_t>();
   a.gamma0 = g0;
   a.iteration = iteration;
@@ -219,7 +265,7 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t E, const T* g0, int64_t iter
   a.iters = L.iters.as<int32_t>();
   a.nonempty = L.nonempty.as<int32_t>();
   record(L, 1);
-  lda::launch_estep<T>(s, a, true, false);
+  launch_split<T>(L, a, n, n_short, true, false);
   record(L, 2);
   HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.V * L.kp, s));
   if (E > 0) {
@@ -293,25 +339,32 @@ void require_ready(stc_lda& L) {
   if (!L.has_topics) throw Error(STC_ERR_STATE, "no topics: call stc_lda_init_random or stc_lda_set_topics");
 }
 
+// host-injected membership → partitioned slots on the device; returns the partition
 template <typename T>
-void step_ids(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, stc_step_stats* st) {
-  require_ready(L);
-  Ctx& c = *L.ctx;
+Part upload_members(stc_lda& L, const int64_t* ids, int64_t n) {
   std::vector<int32_t> h((size_t)n);
   for (int64_t i = 0; i < n; ++i) {
     STC_REQUIRE(ids[i] >= 0 && ids[i] < L.corpus->rows, "batch doc id out of range");
     h[(size_t)i] = (int32_t)ids[i];
   }
   ensure_batch<T>(L, n, 0);
-  record(L, 0);
   if (n > 0)
-    HIP_CHECK(hipMemcpyAsync(L.batch.p, h.data(), 4 * n, hipMemcpyHostToDevice, c.stream));
-  const int64_t E = batch_offsets(L, n);  // syncs (h may die after)
+    HIP_CHECK(hipMemcpyAsync(L.batch_raw.p, h.data(), 4 * n, hipMemcpyHostToDevice, L.ctx->stream));
+  Part p = partition(L, L.corpus->indptr.as<int64_t>(), L.batch_raw.as<int32_t>(), n);  // syncs
+  ensure_batch<T>(L, n, p.E);
+  slot_offsets(L, n);
+  return p;
+}
+
+template <typename T>
+void step_ids(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, stc_step_stats* st) {
+  require_ready(L);
+  record(L, 0);
+  const Part p = upload_members<T>(L, ids, n);
   if (L.timing) harvest(L, L.ev_set ^ 1);  // the previous step has completed (stream order)
-  ensure_batch<T>(L, n, E);
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
-  estep_and_stats<T>(L, n, E, g0, L.iteration + 1);
-  train_tail<T>(L, n, E, st);
+  estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1);
+  train_tail<T>(L, n, p.E, st);
 }
 
 template <typename T>
@@ -322,41 +375,37 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
   const int64_t D = L.corpus->rows;
   L.s_counts.reserve(4 * D);
   L.s_weights.reserve(8 * D);
+  L.s_short.reserve(4 * D);
   L.s_cincl.reserve(4 * D);
   L.s_wincl.reserve(8 * D);
+  L.s_sincl.reserve(4 * D);
   const int64_t it = L.iteration + 1;
   record(L, 0);
   lda::launch_sample(s, L.corpus->indptr.as<int64_t>(), D, L.cfg.mini_batch_fraction,
-                     L.cfg.sample_with_replacement, L.cfg.seed, it, c.rank, L.s_counts.as<int32_t>(),
-                     L.s_weights.as<int64_t>());
-  size_t b1 = 0, b2 = 0;
-  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, b1, L.s_counts.as<int32_t>(), L.s_cincl.as<int32_t>(), (int)D, s));
-  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, b2, L.s_weights.as<int64_t>(), L.s_wincl.as<int64_t>(), (int)D, s));
-  L.scan_tmp.reserve(std::max(b1, b2));
-  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(L.scan_tmp.p, b1, L.s_counts.as<int32_t>(), L.s_cincl.as<int32_t>(), (int)D, s));
-  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(L.scan_tmp.p, b2, L.s_weights.as<int64_t>(), L.s_wincl.as<int64_t>(), (int)D, s));
-  int32_t n32 = 0;
+                     L.cfg.sample_with_replacement, L.cfg.seed, it, c.rank, L.wave_cap,
+                     L.s_counts.as<int32_t>(), L.s_weights.as<int64_t>(), L.s_short.as<int32_t>());
+  incl_scan<int32_t>(L, L.s_counts.as<int32_t>(), L.s_cincl.as<int32_t>(), D);
+  incl_scan<int64_t>(L, L.s_weights.as<int64_t>(), L.s_wincl.as<int64_t>(), D);
+  incl_scan<int32_t>(L, L.s_short.as<int32_t>(), L.s_sincl.as<int32_t>(), D);
+  int32_t n32 = 0, ns32 = 0;
   int64_t E = 0;
   HIP_CHECK(hipMemcpyAsync(&n32, L.s_cincl.as<int32_t>() + (D - 1), 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipMemcpyAsync(&E, L.s_wincl.as<int64_t>() + (D - 1), 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(&ns32, L.s_sincl.as<int32_t>() + (D - 1), 4, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  if (L.timing) {  // the previous step's events have completed (stream order)
-    harvest(L, L.ev_set ^ 1);
-  }
+  if (L.timing) harvest(L, L.ev_set ^ 1);  // the previous step's events have completed
   const int64_t n = n32;
-  ensure_batch<T>(L, n, E);
-  if (n > 0)
-    lda::launch_fill_batch(s, L.corpus->indptr.as<int64_t>(), D, L.s_counts.as<int32_t>(),
-                           L.s_cincl.as<int32_t>(), L.s_wincl.as<int64_t>(), L.batch.as<int32_t>(),
-                           L.bptr.as<int64_t>());
-  HIP_CHECK(hipMemcpyAsync(L.bptr.as<int64_t>() + n, &E, 8, hipMemcpyHostToDevice, s));
-  HIP_CHECK(hipStreamSynchronize(s));  // &E is a stack value
   // Spark's next(): `if (batch.isEmpty()) return this` — no iteration increment
   if (n == 0) {
     if (st) *st = stc_step_stats{};
     return;
   }
-  estep_and_stats<T>(L, n, E, nullptr, it);
+  ensure_batch<T>(L, n, E);
+  lda::launch_fill_batch(s, L.corpus->indptr.as<int64_t>(), D, L.wave_cap, L.s_counts.as<int32_t>(),
+                         L.s_cincl.as<int32_t>(), L.s_sincl.as<int32_t>(), ns32, L.batch.as<int32_t>(),
+                         L.orig.as<int32_t>(), L.nnzp.as<int64_t>());
+  slot_offsets(L, n);
+  estep_and_stats<T>(L, n, ns32, E, nullptr, it);
   train_tail<T>(L, n, E, st);
 }
 
@@ -364,21 +413,12 @@ template <typename T>
 void estep_only(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, double* gamma_out,
                 double* stat_out, int32_t* iters_out) {
   require_ready(L);
-  Ctx& c = *L.ctx;
-  hipStream_t s = c.stream;
-  std::vector<int32_t> h((size_t)n);
-  for (int64_t i = 0; i < n; ++i) {
-    STC_REQUIRE(ids[i] >= 0 && ids[i] < L.corpus->rows, "batch doc id out of range");
-    h[(size_t)i] = (int32_t)ids[i];
-  }
-  ensure_batch<T>(L, n, 0);
-  if (n > 0) HIP_CHECK(hipMemcpyAsync(L.batch.p, h.data(), 4 * n, hipMemcpyHostToDevice, s));
-  const int64_t E = batch_offsets(L, n);
-  ensure_batch<T>(L, n, E);
+  hipStream_t s = L.ctx->stream;
+  const Part p = upload_members<T>(L, ids, n);
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
   const bool t = L.timing;
   L.timing = false;
-  estep_and_stats<T>(L, n, E, g0, L.iteration + 1);
+  estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1);
   L.timing = t;
   if (gamma_out && n > 0) {
     std::vector<T> g((size_t)(n * L.k));
@@ -405,19 +445,19 @@ void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const
   STC_REQUIRE(docs.dtype == L.dtype, "document CSR dtype must match the LDA dtype");
   hipStream_t s = L.ctx->stream;
   const int64_t n = docs.rows;
+  ensure_batch<T>(L, n, 0);
   L.r.reserve(sizeof(T) * std::max<int64_t>(docs.nnz, 1));
-  L.gamma.reserve(sizeof(T) * n * L.k);
   L.bound.reserve(sizeof(double) * std::max<int64_t>(n, 1));
-  L.iters.reserve(4 * n);
   L.scal.reserve(sizeof(double) * 8);
+  const Part p = partition(L, docs.indptr.as<int64_t>(), nullptr, n);
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
   lda::EStepArgs<T> a = estep_args<T>(L);
   a.indptr = docs.indptr.as<int64_t>();
   a.indices = docs.indices.as<int32_t>();
   a.values = docs.values.as<T>();
-  a.batch = nullptr;
-  a.n = n;
-  a.bptr = docs.indptr.as<int64_t>();
+  a.batch = L.batch.as<int32_t>();
+  a.orig = L.orig.as<int32_t>();
+  a.bptr = nullptr;  // entry slots = the rows' CSR positions
   a.gamma0 = g0;
   a.seed = seed;
   a.key_mode = 1;
@@ -426,7 +466,7 @@ void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const
   a.gamma = gamma_out ? L.gamma.as<T>() : nullptr;
   a.iters = L.iters.as<int32_t>();
   a.bound = bound ? L.bound.as<double>() : nullptr;
-  lda::launch_estep<T>(s, a, false, bound);
+  launch_split<T>(L, a, n, p.n_short, false, bound);
   if (gamma_out && n > 0) {
     std::vector<T> g((size_t)(n * L.k));
     HIP_CHECK(hipMemcpyAsync(g.data(), L.gamma.p, sizeof(T) * g.size(), hipMemcpyDeviceToHost, s));
@@ -810,6 +850,8 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->P = ((L->kp / W) % 2 == 1) ? L->kp : L->kp + W;  // P/W odd: conflict-free b128 rows
     L->lds_rows = cfg->dtype == STC_F32 ? lda::estep_lds_rows<float>(L->k, L->kp, L->P)
                                         : lda::estep_lds_rows<double>(L->k, L->kp, L->P);
+    const char* nw = std::getenv("STC_DISABLE_WAVE");
+    L->wave_cap = (cfg->dtype == STC_F32 && !(nw && nw[0] == '1')) ? lda::wave_row_cap(L->k) : 0;
     // α / η resolution ([U] OnlineLDAOptimizer.initialize)
     std::vector<double> alpha((size_t)L->k);
     const int alen = cfg->doc_concentration ? cfg->doc_concentration_len : 0;

@@ -112,8 +112,8 @@ int estep_lds_rows(int k, int kp, int P) {
 // row subsets, partials in LDS), γ = eθ'⊙s + α, eθ' = exp(ψ(γ) − ψ(max γ)), meanΔγ ≤ 1e-3 stops.
 // ---------------------------------------------------------------------------------------
 template <typename T, bool STATS, bool BOUND, bool LDS>
-__device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* smem, int64_t i,
-                                          int64_t row, int64_t s0, int nnz, int64_t e0) {
+__device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* smem, int64_t slot,
+                                          int64_t mem, int64_t row, int64_t s0, int nnz, int64_t e0) {
   using VT = typename VecOf<T>::type;
   constexpr int W = VecOf<T>::W;
   const int tid = threadIdx.x;
@@ -149,23 +149,23 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
   const bool nonempty = __syncthreads_or(nz) != 0;
   if (!nonempty) {
     for (int t = tid; t < k; t += kBlock) {
-      if (a.gamma) a.gamma[i * k + t] = T(0);
-      if (STATS) a.elogth[i * k + t] = T(0);
+      if (a.gamma) a.gamma[mem * k + t] = T(0);
+      if (STATS) a.elogth[slot * k + t] = T(0);
     }
     if (STATS)
-      for (int t = tid; t < kp; t += kBlock) a.eth[i * kp + t] = T(0);
+      for (int t = tid; t < kp; t += kBlock) a.eth[slot * kp + t] = T(0);
     for (int n = tid; n < nnz; n += kBlock) {
       a.r[e0 + n] = T(0);
       if (STATS) {
         a.keys[e0 + n] = (uint32_t)a.indices[s0 + n];
         a.vals[e0 + n] = (uint32_t)(e0 + n);
-        a.edoc[e0 + n] = (int32_t)i;
+        a.edoc[e0 + n] = (int32_t)slot;
       }
     }
     if (tid == 0) {
-      if (a.iters) a.iters[i] = 0;
-      if (a.nonempty) a.nonempty[i] = 0;
-      if (BOUND) a.bound[i] = 0.0;
+      if (a.iters) a.iters[mem] = 0;
+      if (a.nonempty) a.nonempty[mem] = 0;
+      if (BOUND) a.bound[mem] = 0.0;
     }
     return;
   }
@@ -185,7 +185,7 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
   // -- γ₀ (injected or counter RNG) and eθ'
   uint64_t stream = 0;
   if (!a.gamma0) {
-    const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, i)
+    const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, mem)
                                          : (uint64_t)(a.doc_id_base + row);
     stream = doc_stream(a.seed, key);
   }
@@ -193,7 +193,7 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
   for (int t = tid; t < kp; t += kBlock) {
     T g = T(0);
     if (t < k) {
-      g = a.gamma0 ? a.gamma0[i * k + t] : (T)gamma_sample(stream, t, a.gamma_shape);
+      g = a.gamma0 ? a.gamma0[mem * k + t] : (T)gamma_sample(stream, t, a.gamma_shape);
       gsum += (double)g;
       gmax = fmax(gmax, (double)g);
     }
@@ -273,21 +273,21 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
   // -- outputs
   const double psisum = digamma_t<double>(gsum);
   for (int t = tid; t < k; t += kBlock) {
-    if (a.gamma) a.gamma[i * k + t] = s_gam[t];
-    if (STATS) a.elogth[i * k + t] = (T)(digamma_t<double>((double)s_gam[t]) - psisum);
+    if (a.gamma) a.gamma[mem * k + t] = s_gam[t];
+    if (STATS) a.elogth[slot * k + t] = (T)(digamma_t<double>((double)s_gam[t]) - psisum);
   }
   if (STATS) {
-    for (int t = tid; t < kp; t += kBlock) a.eth[i * kp + t] = s_eth[t];
+    for (int t = tid; t < kp; t += kBlock) a.eth[slot * kp + t] = s_eth[t];
     for (int n = tid; n < nnz; n += kBlock) {
       if (LDS) a.r[e0 + n] = s_r[n];
       a.keys[e0 + n] = (uint32_t)ids[n];
       a.vals[e0 + n] = (uint32_t)(e0 + n);
-      a.edoc[e0 + n] = (int32_t)i;
+      a.edoc[e0 + n] = (int32_t)slot;
     }
   }
   if (tid == 0) {
-    if (a.iters) a.iters[i] = it;
-    if (a.nonempty) a.nonempty[i] = 1;
+    if (a.iters) a.iters[mem] = it;
+    if (a.nonempty) a.nonempty[mem] = 1;
   }
   if (BOUND) {
     // E[log p(doc|θ,β)] = Σ_n cts_n (log φ'_n + m_v + max E[log θ]);  E[log p(θ|α) − log q(θ|γ)]
@@ -303,23 +303,24 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
     block_reduce3(tok, topic, dummy2, s_red);
     double as2 = asum, z = 0.0, dz = -INFINITY;
     block_reduce3(as2, z, dz, s_red);
-    if (tid == 0) a.bound[i] = tok + topic + (lgamma(as2) - lgamma(gsum));
+    if (tid == 0) a.bound[mem] = tok + topic + (lgamma(as2) - lgamma(gsum));
   }
 }
 
 template <typename T, bool STATS, bool BOUND>
 __global__ __launch_bounds__(kBlock) void k_estep(EStepArgs<T> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int64_t i = blockIdx.x;
-  if (i >= a.n) return;
-  const int64_t row = a.batch ? (int64_t)a.batch[i] : i;
+  if ((int64_t)blockIdx.x >= a.n) return;
+  const int64_t slot = a.slot0 + blockIdx.x;
+  const int64_t mem = a.orig ? (int64_t)a.orig[slot] : slot;
+  const int64_t row = a.batch ? (int64_t)a.batch[slot] : slot;
   const int64_t s0 = a.indptr[row];
   const int nnz = (int)(a.indptr[row + 1] - s0);
-  const int64_t e0 = a.bptr[i];
+  const int64_t e0 = a.bptr ? a.bptr[slot] : s0;
   if (nnz <= a.lds_rows)
-    estep_doc<T, STATS, BOUND, true>(a, smem, i, row, s0, nnz, e0);
+    estep_doc<T, STATS, BOUND, true>(a, smem, slot, mem, row, s0, nnz, e0);
   else
-    estep_doc<T, STATS, BOUND, false>(a, smem, i, row, s0, nnz, e0);
+    estep_doc<T, STATS, BOUND, false>(a, smem, slot, mem, row, s0, nnz, e0);
 }
 
 template <typename T>
@@ -802,9 +803,10 @@ void launch_batch_nnz(hipStream_t s, const int64_t* indptr, const int32_t* batch
 // RDD.sample(withReplacement, fraction): Poisson(f) (with) or Bernoulli(f) (without) per doc
 __global__ __launch_bounds__(256) void k_sample(const int64_t* __restrict__ indptr, int64_t D,
                                                 double f, int with_repl, uint64_t seed,
-                                                int64_t iteration, int rank,
+                                                int64_t iteration, int rank, int64_t cap,
                                                 int32_t* __restrict__ counts,
-                                                int64_t* __restrict__ weights) {
+                                                int64_t* __restrict__ weights,
+                                                int32_t* __restrict__ short_counts) {
   for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256) {
     const uint64_t st = doc_stream(seed ^ 0x5DEECE66Dull, train_doc_key(iteration, rank, d));
     const double u = rng_uniform(st, 0);
@@ -819,45 +821,103 @@ __global__ __launch_bounds__(256) void k_sample(const int64_t* __restrict__ indp
     } else {
       c = u < f ? 1 : 0;
     }
+    const int64_t nnz = indptr[d + 1] - indptr[d];
     counts[d] = c;
-    weights[d] = (int64_t)c * (indptr[d + 1] - indptr[d]);
+    weights[d] = (int64_t)c * nnz;
+    short_counts[d] = nnz <= cap ? c : 0;
   }
 }
 
 void launch_sample(hipStream_t s, const int64_t* indptr, int64_t D, double fraction, int with_repl,
-                   uint64_t seed, int64_t iteration, int rank, int32_t* counts, int64_t* weights) {
+                   uint64_t seed, int64_t iteration, int rank, int64_t cap, int32_t* counts,
+                   int64_t* weights, int32_t* short_counts) {
   int64_t g = ceil_div(D, 256);
   k_sample<<<(unsigned)(g > 8192 ? 8192 : g), 256, 0, s>>>(indptr, D, fraction, with_repl, seed,
-                                                           iteration, rank, counts, weights);
+                                                           iteration, rank, cap, counts, weights,
+                                                           short_counts);
   KERNEL_CHECK();
 }
 
-// count_incl / weight_incl are INCLUSIVE scans
+// Members in doc order (raw position = count_incl[d] − c + j), written to partitioned slots:
+// short docs (nnz <= cap) first, long docs after n_short.  All INCLUSIVE scans.
 __global__ __launch_bounds__(256) void k_fill_batch(const int64_t* __restrict__ indptr, int64_t D,
-                                                    const int32_t* __restrict__ counts,
+                                                    int64_t cap, const int32_t* __restrict__ counts,
                                                     const int32_t* __restrict__ count_incl,
-                                                    const int64_t* __restrict__ weight_incl,
-                                                    int32_t* __restrict__ batch,
-                                                    int64_t* __restrict__ bptr) {
+                                                    const int32_t* __restrict__ short_incl,
+                                                    int64_t n_short, int32_t* __restrict__ batch_p,
+                                                    int32_t* __restrict__ orig_p,
+                                                    int64_t* __restrict__ nnz_p) {
   for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < D; d += (int64_t)gridDim.x * 256) {
     const int c = counts[d];
     if (c == 0) continue;
     const int64_t nnz = indptr[d + 1] - indptr[d];
-    const int64_t pos0 = (int64_t)count_incl[d] - c;
-    const int64_t w0 = weight_incl[d] - (int64_t)c * nnz;
+    const int64_t raw0 = (int64_t)count_incl[d] - c;
+    const int64_t sh_before = (int64_t)short_incl[d] - (nnz <= cap ? c : 0);
+    const int64_t slot0 = nnz <= cap ? sh_before : n_short + (raw0 - sh_before);
     for (int j = 0; j < c; ++j) {
-      batch[pos0 + j] = (int32_t)d;
-      bptr[pos0 + j] = w0 + (int64_t)j * nnz;
+      batch_p[slot0 + j] = (int32_t)d;
+      orig_p[slot0 + j] = (int32_t)(raw0 + j);
+      nnz_p[slot0 + j] = nnz;
     }
   }
 }
 
-void launch_fill_batch(hipStream_t s, const int64_t* indptr, int64_t D, const int32_t* counts,
-                       const int32_t* count_off, const int64_t* weight_off, int32_t* batch,
-                       int64_t* bptr) {
+void launch_fill_batch(hipStream_t s, const int64_t* indptr, int64_t D, int64_t cap,
+                       const int32_t* counts, const int32_t* count_incl,
+                       const int32_t* short_incl, int64_t n_short, int32_t* batch_p,
+                       int32_t* orig_p, int64_t* nnz_p) {
   int64_t g = ceil_div(D, 256);
-  k_fill_batch<<<(unsigned)(g > 8192 ? 8192 : g), 256, 0, s>>>(indptr, D, counts, count_off,
-                                                               weight_off, batch, bptr);
+  k_fill_batch<<<(unsigned)(g > 8192 ? 8192 : g), 256, 0, s>>>(indptr, D, cap, counts, count_incl,
+                                                               short_incl, n_short, batch_p, orig_p,
+                                                               nnz_p);
+  KERNEL_CHECK();
+}
+
+// host-injected membership: flags + stable partition into [short | long] slots
+__global__ __launch_bounds__(256) void k_part_flags(const int64_t* __restrict__ indptr,
+                                                    const int32_t* __restrict__ batch, int64_t n,
+                                                    int64_t cap, int64_t* __restrict__ nnz_out,
+                                                    int32_t* __restrict__ short_flag) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = batch ? (int64_t)batch[i] : i;  // nullptr: identity rows
+    const int64_t nnz = indptr[r + 1] - indptr[r];
+    nnz_out[i] = nnz;
+    short_flag[i] = nnz <= cap ? 1 : 0;
+  }
+}
+
+void launch_part_flags(hipStream_t s, const int64_t* indptr, const int32_t* batch, int64_t n,
+                       int64_t cap, int64_t* nnz_out, int32_t* short_flag) {
+  if (n == 0) return;
+  int64_t g = ceil_div(n, 256);
+  k_part_flags<<<(unsigned)(g > 4096 ? 4096 : g), 256, 0, s>>>(indptr, batch, n, cap, nnz_out, short_flag);
+  KERNEL_CHECK();
+}
+
+__global__ __launch_bounds__(256) void k_part_scatter(const int32_t* __restrict__ batch,
+                                                      const int64_t* __restrict__ nnz, int64_t n,
+                                                      const int32_t* __restrict__ short_flag,
+                                                      const int32_t* __restrict__ short_incl,
+                                                      int32_t* __restrict__ batch_p,
+                                                      int32_t* __restrict__ orig_p,
+                                                      int64_t* __restrict__ nnz_p) {
+  const int64_t n_short = n > 0 ? short_incl[n - 1] : 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t sh = short_incl[i];
+    const int64_t slot = short_flag[i] ? sh - 1 : n_short + (i - sh);
+    batch_p[slot] = batch ? batch[i] : (int32_t)i;
+    orig_p[slot] = (int32_t)i;
+    nnz_p[slot] = nnz[i];
+  }
+}
+
+void launch_part_scatter(hipStream_t s, const int32_t* batch, const int64_t* nnz, int64_t n,
+                         const int32_t* short_flag, const int32_t* short_incl, int32_t* batch_p,
+                         int32_t* orig_p, int64_t* nnz_p) {
+  if (n == 0) return;
+  int64_t g = ceil_div(n, 256);
+  k_part_scatter<<<(unsigned)(g > 4096 ? 4096 : g), 256, 0, s>>>(batch, nnz, n, short_flag, short_incl,
+                                                                 batch_p, orig_p, nnz_p);
   KERNEL_CHECK();
 }
 

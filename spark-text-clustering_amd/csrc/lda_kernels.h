@@ -19,9 +19,14 @@ struct EStepArgs {
   const int64_t* indptr = nullptr;     // documents (CSR rows)
   const int32_t* indices = nullptr;
   const T* values = nullptr;
-  const int32_t* batch = nullptr;      // batch member → row (nullptr: member i is row i)
-  int64_t n = 0;                       // members
-  const int64_t* bptr = nullptr;       // member → first entry slot (n+1)
+  // A launch covers slots [slot0, slot0 + n).  slot → row via `batch` (nullptr: row = slot);
+  // slot → caller's member index via `orig` (nullptr: member = slot) — γ₀, γ, iters, nonempty,
+  // bound and the RNG key are per MEMBER; eth / elogth / entry slots are per SLOT.
+  const int32_t* batch = nullptr;
+  const int32_t* orig = nullptr;
+  int64_t slot0 = 0;
+  int64_t n = 0;                       // slots in this launch
+  const int64_t* bptr = nullptr;       // slot → first entry slot (nullptr: the row's CSR offset)
   const T* Bp = nullptr;               // V×kp  row-scaled expElogβ'
   const double* logscale = nullptr;    // V     m_v (BOUND)
   const double* alpha = nullptr;       // k
@@ -52,6 +57,18 @@ template <typename T>
 int estep_lds_rows(int k, int kp, int P);
 template <typename T>
 void launch_estep(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound);
+
+// Wave-per-document E-step (lda_wave.hip): fp32, k <= 128, nnz <= wave_row_cap(k).
+int wave_kmax(int k);                  // 0 when the wave kernel does not apply
+int wave_row_cap(int k);               // max nnz a wave keeps in VGPRs (0 if n/a)
+void launch_estep_wave(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound);
+
+// Batch partition: slots [0, n_short) = members with nnz <= cap (wave kernel), then the rest.
+void launch_part_flags(hipStream_t s, const int64_t* indptr, const int32_t* batch, int64_t n,
+                       int64_t cap, int64_t* nnz_out, int32_t* short_flag);
+void launch_part_scatter(hipStream_t s, const int32_t* batch, const int64_t* nnz, int64_t n,
+                         const int32_t* short_flag, const int32_t* short_incl, int32_t* batch_p,
+                         int32_t* orig_p, int64_t* nnz_p);
 
 template <typename T>
 void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint32_t* svals, int64_t E,
@@ -86,10 +103,13 @@ void launch_iter_stats(hipStream_t s, const int32_t* iters, const int32_t* nonem
 void launch_batch_nnz(hipStream_t s, const int64_t* indptr, const int32_t* batch, int64_t n,
                       int64_t* nnz_out);
 void launch_sample(hipStream_t s, const int64_t* indptr, int64_t D, double fraction, int with_repl,
-                   uint64_t seed, int64_t iteration, int rank, int32_t* counts, int64_t* weights);
-void launch_fill_batch(hipStream_t s, const int64_t* indptr, int64_t D, const int32_t* counts,
-                       const int32_t* count_off, const int64_t* weight_off, int32_t* batch,
-                       int64_t* bptr);
+                   uint64_t seed, int64_t iteration, int rank, int64_t cap, int32_t* counts,
+                   int64_t* weights, int32_t* short_counts);
+// writes partitioned slots: batch_p (row), orig_p (raw member position), nnz_p
+void launch_fill_batch(hipStream_t s, const int64_t* indptr, int64_t D, int64_t cap,
+                       const int32_t* counts, const int32_t* count_incl,
+                       const int32_t* short_incl, int64_t n_short, int32_t* batch_p,
+                       int32_t* orig_p, int64_t* nnz_p);
 void launch_transpose_kv(hipStream_t s, const double* lam, int64_t V, int k, double* out_kv,
                          int32_t* idx_kv);
 template <typename T>
