@@ -851,7 +851,9 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->lds_rows = cfg->dtype == STC_F32 ? lda::estep_lds_rows<float>(L->k, L->kp, L->P)
                                         : lda::estep_lds_rows<double>(L->k, L->kp, L->P);
     const char* nw = std::getenv("STC_DISABLE_WAVE");
-    L->wave_cap = (cfg->dtype == STC_F32 && !(nw && nw[0] == '1')) ? lda::wave_row_cap(L->k) : 0;
+    L->wave_cap = (cfg->dtype == STC_F32 && !(nw && nw[0] == '1') && lda::wave_row_cap(L->k) > 0)
+                      ? lda::wave_row_cap(L->k)
+                      : -1;  // −1: no slot is "short" (not even empty docs)
     // α / η resolution ([U] OnlineLDAOptimizer.initialize)
     std::vector<double> alpha((size_t)L->k);
     const int alen = cfg->doc_concentration ? cfg->doc_concentration_len : 0;

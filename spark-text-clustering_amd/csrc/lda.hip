@@ -55,6 +55,8 @@ __device__ __forceinline__ double hsum<double, VecOf<double>::type>(VecOf<double
 }
 
 __device__ __forceinline__ float exp_t(float x) { return __expf(x); }
+__device__ __forceinline__ float psi_t(float x) { return digamma_fast(x); }
+__device__ __forceinline__ double psi_t(double x) { return digamma_t<double>(x); }
 __device__ __forceinline__ double exp_t(double x) { return exp(x); }
 
 // ---------------------------------------------------------------------------------------
@@ -200,11 +202,11 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
     s_gam[t] = g;
   }
   block_reduce3(gsum, dummy, gmax, s_red);
-  T lmax = digamma_t<T>((T)gmax) - digamma_t<T>((T)gsum);  // max_t E[log θ_t]
+  T lmax = psi_t((T)gmax) - psi_t((T)gsum);  // max_t E[log θ_t]
   {
-    const T psimax = digamma_t<T>((T)gmax);
+    const T psimax = psi_t((T)gmax);
     for (int t = tid; t < kp; t += kBlock)
-      s_eth[t] = t < k ? exp_t(digamma_t<T>(s_gam[t]) - psimax) : T(0);
+      s_eth[t] = t < k ? exp_t(psi_t(s_gam[t]) - psimax) : T(0);
   }
   __syncthreads();
 
@@ -262,9 +264,9 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
     block_reduce3(dsum, gsum, gmax, s_red);
 
     // Phase D: eθ' = exp(ψ(γ) − ψ(max γ)) ; meanGammaChange = Σ|Δγ| / k
-    const T psimax = digamma_t<T>((T)gmax);
-    lmax = psimax - digamma_t<T>((T)gsum);
-    for (int t = tid; t < k; t += kBlock) s_eth[t] = exp_t(digamma_t<T>(s_gam[t]) - psimax);
+    const T psimax = psi_t((T)gmax);
+    lmax = psimax - psi_t((T)gsum);
+    for (int t = tid; t < k; t += kBlock) s_eth[t] = exp_t(psi_t(s_gam[t]) - psimax);
     ++it;
     done = dsum / (double)k <= 1e-3;
     __syncthreads();

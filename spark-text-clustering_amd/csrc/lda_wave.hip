@@ -40,14 +40,8 @@ __device__ __forceinline__ float bf(unsigned x) { return __builtin_bit_cast(floa
 
 // reduce-scatter step across lane distance 32 (or 16): lanes with the role bit clear keep topic
 // set X, the others keep Y; after the swap x + y is the pair's total of the kept topic.
-__device__ __forceinline__ float rs_swap32(float x, float y) {
-  const auto r = __builtin_amdgcn_permlane32_swap(fb(x), fb(y), false, false);
-  return bf(r[0]) + bf(r[1]);
-}
-__device__ __forceinline__ float rs_swap16(float x, float y) {
-  const auto r = __builtin_amdgcn_permlane16_swap(fb(x), fb(y), false, false);
-  return bf(r[0]) + bf(r[1]);
-}
+__device__ __forceinline__ float rs_swap32(float x, float y) { return swap32_pair(x, true, y); }
+__device__ __forceinline__ float rs_swap16(float x, float y) { return swap16_pair(x, true, y); }
 // reduce-scatter step through a DPP involution (row_mirror / row_half_mirror / quad_perm)
 template <int CTRL>
 __device__ __forceinline__ float rs_dpp(float x, float y, bool hi) {
@@ -171,14 +165,14 @@ __global__ __launch_bounds__(64) void k_estep_wave(EStepArgs<float> a) {
     gsum += gam[s];
     gmax = fmaxf(gmax, gam[s]);
   }
-  gsum = wave_sum(gsum);
-  gmax = wave_max(gmax);
-  float psimax = digamma_t<float>(gmax);
-  float lmax = psimax - digamma_t<float>(gsum);
+  gsum = wave_sum_dpp(gsum);
+  gmax = wave_max_dpp(gmax);
+  float psimax = digamma_fast(gmax);
+  float lmax = psimax - digamma_fast(gsum);
 #pragma unroll
   for (int s = 0; s < N6; ++s) {
     const int t = tt[s];
-    eth[s] = (own[s] && t < k) ? __expf(digamma_t<float>(gam[s]) - psimax) : 0.f;
+    eth[s] = (own[s] && t < k) ? __expf(digamma_fast(gam[s]) - psimax) : 0.f;
     if (own[s]) s_eth[t] = eth[s];
   }
   __builtin_amdgcn_wave_barrier();
@@ -195,20 +189,18 @@ __global__ __launch_bounds__(64) void k_estep_wave(EStepArgs<float> a) {
     for (int c = 0; c < C4; ++c) {
       const float4 e = *reinterpret_cast<const float4*>(s_eth + 4 * c);
 #pragma unroll
-      for (int j = 0; j < ROWS; ++j) {
-        if (j * 64 < nnz) {
-          dot[j] = fmaf(B[j][4 * c + 0], e.x, dot[j]);
-          dot[j] = fmaf(B[j][4 * c + 1], e.y, dot[j]);
-          dot[j] = fmaf(B[j][4 * c + 2], e.z, dot[j]);
-          dot[j] = fmaf(B[j][4 * c + 3], e.w, dot[j]);
-        }
+      for (int j = 0; j < ROWS; ++j) {  // rows past nnz are zero: no per-row branches
+        dot[j] = fmaf(B[j][4 * c + 0], e.x, dot[j]);
+        dot[j] = fmaf(B[j][4 * c + 1], e.y, dot[j]);
+        dot[j] = fmaf(B[j][4 * c + 2], e.z, dot[j]);
+        dot[j] = fmaf(B[j][4 * c + 3], e.w, dot[j]);
       }
     }
     const bool last = done || it >= a.max_iter;
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
       const float phi = dot[j] + fmaxf(__expf(lse[j] - lmax), 1.17549435e-38f);
-      rr[j] = cts[j] / phi;
+      rr[j] = __fdividef(cts[j], phi);
       if (BOUND && last && cts[j] != 0.f) {
         b_tok += (double)cts[j] * ((double)logf(fmaxf(dot[j], 1.17549435e-38f)) + a.logscale[ids[j]]);
         c_tok += (double)cts[j];
@@ -223,10 +215,8 @@ __global__ __launch_bounds__(64) void k_estep_wave(EStepArgs<float> a) {
       float x = 0.f, y = 0.f;
 #pragma unroll
       for (int j = 0; j < ROWS; ++j) {
-        if (j * 64 < nnz) {
-          x = fmaf(B[j][q], rr[j], x);
-          if (N1 + q < KMAX) y = fmaf(B[j][N1 + q], rr[j], y);
-        }
+        x = fmaf(B[j][q], rr[j], x);
+        if (N1 + q < KMAX) y = fmaf(B[j][N1 + q], rr[j], y);
       }
       p1[q] = rs_swap32(x, y);
     }
@@ -264,16 +254,16 @@ __global__ __launch_bounds__(64) void k_estep_wave(EStepArgs<float> a) {
         gmax = fmaxf(gmax, g);
       }
     }
-    dsum = wave_sum(dsum);
-    gsum = wave_sum(gsum);
-    gmax = wave_max(gmax);
+    dsum = wave_sum_dpp(dsum);
+    gsum = wave_sum_dpp(gsum);
+    gmax = wave_max_dpp(gmax);
     // Phase D: eθ' = exp(ψ(γ) − ψ(max γ)), broadcast through LDS
-    psimax = digamma_t<float>(gmax);
-    lmax = psimax - digamma_t<float>(gsum);
+    psimax = digamma_fast(gmax);
+    lmax = psimax - digamma_fast(gsum);
 #pragma unroll
     for (int s = 0; s < N6; ++s) {
       const int t = tt[s];
-      eth[s] = (own[s] && t < k) ? __expf(digamma_t<float>(gam[s]) - psimax) : 0.f;
+      eth[s] = (own[s] && t < k) ? __expf(digamma_fast(gam[s]) - psimax) : 0.f;
       if (own[s]) s_eth[t] = eth[s];
     }
     __builtin_amdgcn_wave_barrier();
@@ -290,8 +280,9 @@ __global__ __launch_bounds__(64) void k_estep_wave(EStepArgs<float> a) {
       if (a.gamma) a.gamma[mem * k + t] = gam[s];
       if (STATS) a.elogth[slot * k + t] = (float)(digamma_t<double>((double)gam[s]) - psisum);
     }
-    if (STATS && own[s] && t < kp) a.eth[slot * kp + t] = (t < k) ? eth[s] : 0.f;
   }
+  if (STATS)  // from the LDS copy φ was computed with (pads are zero)
+    for (int t = lane; t < kp; t += 64) a.eth[slot * kp + t] = s_eth[t];
 #pragma unroll
   for (int j = 0; j < ROWS; ++j) {
     const int n = j * 64 + lane;

@@ -171,6 +171,18 @@ __host__ __device__ inline R digamma_t(R x) {
               f * (R(-1.0 / 132.0) + f * (R(691.0 / 32760.0) + f * (R(-1.0 / 12.0) + f * R(3617.0) / R(8160.0))))))));
   return r + log(x) - R(0.5) / x + t;
 }
+// fp32 digamma for the E-step inner loop: ψ(x) = ψ(x+6) − Σ_{i<6} 1/(x+i) unconditionally (no
+// data-dependent loop ⇒ no lane divergence), v_rcp_f32 / v_log_f32, Breeze's asymptotic series.
+__device__ inline float digamma_fast(float x) {
+  const float r = __builtin_amdgcn_rcpf(x) + __builtin_amdgcn_rcpf(x + 1.f) + __builtin_amdgcn_rcpf(x + 2.f) +
+                  __builtin_amdgcn_rcpf(x + 3.f) + __builtin_amdgcn_rcpf(x + 4.f) + __builtin_amdgcn_rcpf(x + 5.f);
+  const float y = x + 6.f;
+  const float iy = __builtin_amdgcn_rcpf(y);
+  const float f = iy * iy;
+  const float t = f * (-1.f / 12.f + f * (1.f / 120.f + f * (-1.f / 252.f + f * (1.f / 240.f + f * (-1.f / 132.f)))));
+  return __logf(y) - 0.5f * iy + t - r;
+}
+
 __host__ __device__ inline double trigamma_d(double x) {
   double r = 0;
   while (x <= 5.0) {
@@ -186,6 +198,55 @@ __host__ __device__ inline double trigamma_d(double x) {
 // ---------------------------------------------------------------------------------------
 // Wave64 / block reductions
 // ---------------------------------------------------------------------------------------
+// fp32 wave64 all-reduce without LDS: two permlane swaps (across 32 / 16 lanes) and four DPP
+// involutions inside each 16-lane row (row_mirror, row_half_mirror, quad_perm 1032 and 2301).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// Compiler hazard (ROCm 7.2 hipcc, gfx950): with __builtin_amdgcn_permlane{16,32}_swap the compiler
+// sometimes reads the FIRST result register for both results (`v_add v0, v0, v0` after the swap;
+// seen whenever both operands carry the same value, even through an opaque copy).  The swaps are
+// therefore issued as inline asm with both registers in/out; `s_nop 1` covers the VALU-write →
+// permlane-read hazard the compiler inserts for the builtin.  `volatile` keeps the compiler from
+// re-materialising a swap inside a divergent branch (inactive partner lanes ⇒ garbage).
+__device__ __forceinline__ void pswap32(unsigned& x, unsigned& y) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+__device__ __forceinline__ void pswap16(unsigned& x, unsigned& y) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+__device__ __forceinline__ float swap32_pair(float v, bool add, float w) {
+  unsigned x = __builtin_bit_cast(unsigned, v), y = __builtin_bit_cast(unsigned, w);
+  pswap32(x, y);
+  const float a = __builtin_bit_cast(float, x), b = __builtin_bit_cast(float, y);
+  return add ? a + b : fmaxf(a, b);
+}
+__device__ __forceinline__ float swap16_pair(float v, bool add, float w) {
+  unsigned x = __builtin_bit_cast(unsigned, v), y = __builtin_bit_cast(unsigned, w);
+  pswap16(x, y);
+  const float a = __builtin_bit_cast(float, x), b = __builtin_bit_cast(float, y);
+  return add ? a + b : fmaxf(a, b);
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = swap32_pair(v, true, v);
+  v = swap16_pair(v, true, v);
+  v += dpp_f<0x140>(v);  // row_mirror
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  return v;
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = swap32_pair(v, false, v);
+  v = swap16_pair(v, false, v);
+  v = fmaxf(v, dpp_f<0x140>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  return v;
+}
+
 template <typename R>
 __device__ inline R wave_sum(R v) {
 #pragma unroll

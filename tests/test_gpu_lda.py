@@ -26,11 +26,17 @@ def _handle(ctx, corpus, k, dtype, lam=None, **kw):
     return h, d
 
 
-@pytest.mark.parametrize("dtype", ["f64", "f32"])
-def test_estep_gamma_and_stat(ctx, oracle, dtype):
-    rng = np.random.default_rng(10)
-    D, V, k = 48, 2048, 16
-    corpus = random_corpus(rng, D, V, 1, 120, empty_every=13)
+@pytest.mark.parametrize("dtype,k,kernel", [("f64", 16, "wg"), ("f32", 16, "wave"), ("f32", 16, "wg"),
+                                             ("f32", 100, "wave"), ("f32", 100, "wg"), ("f32", 128, "wave"),
+                                             ("f32", 77, "wave")])
+def test_estep_gamma_and_stat(ctx, oracle, dtype, k, kernel, monkeypatch):
+    """Both E-step kernels (wave-per-doc for fp32 k<=128, workgroup-per-doc otherwise) vs the oracle,
+    including docs longer than the wave's VGPR capacity (routed to the workgroup kernel)."""
+    if kernel == "wg":
+        monkeypatch.setenv("STC_DISABLE_WAVE", "1")
+    rng = np.random.default_rng(10 + k)
+    D, V = 48, 2048
+    corpus = random_corpus(rng, D, V, 1, 300, empty_every=13)
     lam = rng.gamma(100.0, 0.01, size=(V, k))
     g0 = rng.gamma(100.0, 0.01, size=(D, k))
     h, _ = _handle(ctx, corpus, k, dtype, lam)
