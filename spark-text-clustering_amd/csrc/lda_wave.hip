@@ -12,8 +12,9 @@
 //   s = Bᵀr : lane-local products reduce-scattered across the 64 lanes over the wave's slice only
 //     (v_permlane32/16 swaps halve the set twice, then four DPP involutions) — every lane ends
 //     owning ⌈KW/64⌉ topics, where γ, ψ(γ) and exp run; no cross-wave traffic.
-//   Σ|Δγ|, Σγ and max γ meet in LDS behind a second barrier: eθ' must share one scale across waves.
-// Per inner iteration and lane: 2·ROWS·KW FMAs, ~120 permute/add/select, two barriers (W > 1).
+//   Σ|Δγ| of each update rides along with the next φ exchange; ψ(Σγ) for eθ comes from the
+//   identity Σγ' = Σα + Σ_n r_n·dot_n, which every wave holds without an exchange.
+// Per inner iteration and lane: 2·ROWS·KW FMAs, ~100 permute/add/select, one barrier (W > 1).
 #include "lda_kernels.h"
 
 namespace stc {
@@ -24,20 +25,21 @@ namespace {
 constexpr double kLogEps = -230.25850929940458;  // ln(1e-100): Spark's φ epsilon (see lda.hip)
 constexpr float kTiny = 1.17549435e-38f;         // FLT_MIN
 
-template <int KMAX>
-struct SplitShape;  // serves k <= KMAX
-template <>
-struct SplitShape<64> {
-  static constexpr int W = 2, KW = 32, ROWS = 4;
+// (waves per document, topics per wave, rows per lane, waves per SIMD the registers allow)
+template <int W_, int KW_, int ROWS_, int OCC_>
+struct Shape {
+  static constexpr int W = W_, KW = KW_, ROWS = ROWS_, OCC = OCC_;
 };
-template <>
-struct SplitShape<104> {  // k = 100: slices [0,52) and [52,100) — 16-byte aligned row offsets
-  static constexpr int W = 2, KW = 52, ROWS = 3;
-};
-template <>
-struct SplitShape<128> {
-  static constexpr int W = 4, KW = 32, ROWS = 3;
-};
+// k <= 64 / <= 104 / <= 128.  k = 100: slices [0,52) and [52,100), 16-byte aligned row offsets.
+using Shape64 = Shape<2, 32, 4, 2>;
+using Shape104 = Shape<2, 52, 3, 2>;
+using Shape128 = Shape<4, 32, 3, 2>;
+// alternatives kept selectable for measurement (STC_WAVE_SHAPE=1..)
+using Shape104b = Shape<4, 28, 3, 3>;
+using Shape104c = Shape<4, 28, 4, 2>;
+using Shape104d = Shape<3, 36, 3, 3>;
+
+typedef float f2 __attribute__((ext_vector_type(2)));  // v_pk_fma_f32 operand pair
 
 constexpr int hup(int n) { return (n + 1) / 2; }
 template <int KW>
@@ -57,18 +59,17 @@ __device__ __forceinline__ float rs_dpp(float x, float y, bool hi) {
 }
 constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141, DPP_QP_3210 = 0x1B, DPP_QP_1032 = 0xB1;
 
-template <int KMAX, bool STATS, bool BOUND>
-__global__ __launch_bounds__(64 * SplitShape<KMAX>::W, 2) void k_estep_split(EStepArgs<float> a) {
-  constexpr int W = SplitShape<KMAX>::W, KW = SplitShape<KMAX>::KW, ROWS = SplitShape<KMAX>::ROWS;
+template <class S, bool STATS, bool BOUND>
+__global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<float> a) {
+  constexpr int W = S::W, KW = S::KW, ROWS = S::ROWS;
   constexpr int C4 = KW / 4;
   constexpr int N1 = lvl<KW>(1), N2 = lvl<KW>(2), N3 = lvl<KW>(3), N4 = lvl<KW>(4), N5 = lvl<KW>(5),
                 N6 = lvl<KW>(6);
-  static_assert(KW % 4 == 0 && N6 >= 1, "shape");
-  // one buffer each suffices: the φ barrier and the reduction barrier alternate, so a wave can
-  // only overwrite a buffer after every wave has passed the other barrier (and read it).
+  constexpr int H = KW / 2;  // topic pairs per row
+  static_assert(KW % 4 == 0 && N1 == H && H % 2 == 0 && N6 >= 1, "shape");
   __shared__ __attribute__((aligned(16))) float s_eth[W][KW];
-  __shared__ float s_phi[W][ROWS][64];
-  __shared__ float s_red[W][3];
+  __shared__ float s_phi[2][W][ROWS][64];
+  __shared__ float s_red[2][W][3];
   __shared__ double s_bd[W][2];
 
   if ((int64_t)blockIdx.x >= a.n) return;
@@ -109,7 +110,7 @@ __global__ __launch_bounds__(64 * SplitShape<KMAX>::W, 2) void k_estep_split(ESt
   }
 
   // ---- load the document: ids, counts, ε-log-scales and this wave's slice of the B rows
-  float B[ROWS][KW];
+  f2 B[ROWS][H];  // B[j][p] = topics (2p, 2p+1) of row j: packed-FMA operands
   float cts[ROWS], lse[ROWS], rr[ROWS];
   int ids[ROWS];
   int any = 0;
@@ -126,10 +127,8 @@ __global__ __launch_bounds__(64 * SplitShape<KMAX>::W, 2) void k_estep_split(ESt
     for (int c = 0; c < C4; ++c) {
       float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
       if (v && t0 + 4 * c < kp) x = src[c];
-      B[j][4 * c + 0] = x.x;
-      B[j][4 * c + 1] = x.y;
-      B[j][4 * c + 2] = x.z;
-      B[j][4 * c + 3] = x.w;
+      B[j][2 * c] = f2{x.x, x.y};
+      B[j][2 * c + 1] = f2{x.z, x.w};
     }
   }
   bool nonempty;
@@ -168,116 +167,145 @@ __global__ __launch_bounds__(64 * SplitShape<KMAX>::W, 2) void k_estep_split(ESt
     return;
   }
 
-  // (Σ, Σ, max) over the whole document: wave all-reduce, then the W waves through LDS in a fixed
-  // order, so every wave gets bit-identical totals (and therefore the same stopping decision)
-  auto block_reduce = [&](float& x, float& y, float& m) {
-    x = wave_sum_dpp(x);
-    y = wave_sum_dpp(y);
-    m = wave_max_dpp(m);
+  // Cross-wave exchange: each wave publishes its φ partials (ROWS per lane) and up to two wave-
+  // uniform scalars; one barrier; every wave combines them in the same order (a sum of two is
+  // commutative, so for W = 2 each wave adds the other's values to its own) ⇒ bit-identical
+  // results in every wave.  Double-buffered by parity: a wave can only reuse a buffer after every
+  // wave has passed the following barrier (and so finished reading it).
+  auto exchange = [&](int b, float* dot, int nd, float& x, float& y) {
     if constexpr (W > 1) {
+#pragma unroll
+      for (int j = 0; j < nd; ++j) s_phi[b][wave][j][lane] = dot[j];
       if (lane == 0) {
-        s_red[wave][0] = x;
-        s_red[wave][1] = y;
-        s_red[wave][2] = m;
+        s_red[b][wave][0] = x;
+        s_red[b][wave][1] = y;
       }
       __syncthreads();
-      x = s_red[0][0];
-      y = s_red[0][1];
-      m = s_red[0][2];
+      if constexpr (W == 2) {
+        const int o = wave ^ 1;
 #pragma unroll
-      for (int w = 1; w < W; ++w) {
-        x += s_red[w][0];
-        y += s_red[w][1];
-        m = fmaxf(m, s_red[w][2]);
+        for (int j = 0; j < nd; ++j) dot[j] += s_phi[b][o][j][lane];
+        x += s_red[b][o][0];
+        y += s_red[b][o][1];
+      } else {
+#pragma unroll
+        for (int j = 0; j < nd; ++j) {
+          float d = s_phi[b][0][j][lane];
+#pragma unroll
+          for (int w = 1; w < W; ++w) d += s_phi[b][w][j][lane];
+          dot[j] = d;
+        }
+        x = s_red[b][0][0];
+        y = s_red[b][0][1];
+#pragma unroll
+        for (int w = 1; w < W; ++w) {
+          x += s_red[b][w][0];
+          y += s_red[b][w][1];
+        }
       }
     }
   };
 
-  // ---- γ₀ for the owned topics, eθ' = exp(ψ(γ) − ψ(max γ))
+  // ---- γ₀ for the owned topics
   uint64_t stream = 0;
   if (!a.gamma0) {
     const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, mem) : (uint64_t)(a.doc_id_base + row);
     stream = doc_stream(a.seed, key);
   }
   float gam[N6], eth[N6], alp[N6];
-  float gsum = 0.f, gmax = 0.f, dsum = 0.f;
+  float gsum = 0.f, asum = 0.f;
 #pragma unroll
   for (int s = 0; s < N6; ++s) {
     const int t = t0 + tl[s];
     gam[s] = own[s] ? (a.gamma0 ? a.gamma0[mem * k + t] : (float)gamma_sample(stream, t, a.gamma_shape)) : 0.f;
     alp[s] = own[s] ? (float)a.alpha[t] : 0.f;
     gsum += gam[s];
-    gmax = fmaxf(gmax, gam[s]);
+    asum += alp[s];
   }
   for (int t = lane; t < KW; t += 64) my_eth[t] = 0.f;  // slice padding (t0 + t >= k) stays zero
-  block_reduce(gsum, dsum, gmax);
-  float psimax = digamma_fast(gmax);
-  float lmax = psimax - digamma_fast(gsum);
+  gsum = wave_sum_dpp(gsum);
+  asum = wave_sum_dpp(asum);
+  exchange(1, nullptr, 0, gsum, asum);
+  // eθ = exp(ψ(γ) − c) with c = ψ(Σγ): Spark's own (unscaled) exp(E[log θ]).  Inside the loop Σγ of
+  // the next γ comes from Σ_t γ'_t = Σα + Σ_n r_n·dot_n (exact in real arithmetic), which every wave
+  // holds identically — no exchange, off the critical path.  c is only a common scale: φ, r and
+  // the statistics are invariant to it, so rounding in Σγ̃ does not move the fixed point.
+  float cs = digamma_fast(gsum);
+  // ε'_n = max(1e-100 / e^{m_n}, FLT_MIN): Spark's φ epsilon in the row-scaled space
+  float eps[ROWS];
+#pragma unroll
+  for (int j = 0; j < ROWS; ++j) eps[j] = max_nonneg(__expf(lse[j]), kTiny);
 #pragma unroll
   for (int s = 0; s < N6; ++s) {
-    eth[s] = own[s] ? __expf(digamma_fast(gam[s]) - psimax) : 0.f;
+    eth[s] = own[s] ? __expf(digamma_fast(gam[s]) - cs) : 0.f;
     if (own[s]) my_eth[tl[s]] = eth[s];
   }
   __builtin_amdgcn_wave_barrier();  // the slice is read back only by this wave
 
   int it = 0;
-  bool done = false;
+  float dsum = 0.f, dummy = 0.f;
   double b_tok = 0.0, c_tok = 0.0;
   while (true) {
-    // Phase A: φ_n = B_n·eθ' + ε'_n ; r_n = cts_n / φ_n
+    // Phase A: φ_n = B_n·eθ + ε'_n ; r_n = cts_n / φ_n
+    // (even and odd topics accumulate in the two halves of a packed pair)
     float dot[ROWS];
+    {
+      f2 acc[ROWS];
 #pragma unroll
-    for (int j = 0; j < ROWS; ++j) dot[j] = 0.f;
+      for (int j = 0; j < ROWS; ++j) acc[j] = f2{0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < C4; ++c) {
-      const float4 e = *reinterpret_cast<const float4*>(my_eth + 4 * c);
+      for (int c = 0; c < C4; ++c) {
+        const float4 e = *reinterpret_cast<const float4*>(my_eth + 4 * c);
+        const f2 e01 = f2{e.x, e.y}, e23 = f2{e.z, e.w};
 #pragma unroll
-      for (int j = 0; j < ROWS; ++j) {  // rows past nnz are zero: no per-row branches
-        dot[j] = fmaf(B[j][4 * c + 0], e.x, dot[j]);
-        dot[j] = fmaf(B[j][4 * c + 1], e.y, dot[j]);
-        dot[j] = fmaf(B[j][4 * c + 2], e.z, dot[j]);
-        dot[j] = fmaf(B[j][4 * c + 3], e.w, dot[j]);
+        for (int j = 0; j < ROWS; ++j) {  // rows past nnz are zero: no per-row branches
+          acc[j] = __builtin_elementwise_fma(B[j][2 * c], e01, acc[j]);
+          acc[j] = __builtin_elementwise_fma(B[j][2 * c + 1], e23, acc[j]);
+        }
       }
+#pragma unroll
+      for (int j = 0; j < ROWS; ++j) dot[j] = acc[j].x + acc[j].y;
     }
-    if constexpr (W > 1) {
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) s_phi[wave][j][lane] = dot[j];
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < ROWS; ++j) {
-        float d = s_phi[0][j][lane];
-#pragma unroll
-        for (int w = 1; w < W; ++w) d += s_phi[w][j][lane];
-        dot[j] = d;
-      }
-    }
-    const bool last = done || it >= a.max_iter;
+    // Σ|Δγ| of the update that produced the current γ rides along
+    exchange(it & 1, dot, ROWS, dsum, dummy);
+    const bool last = (it > 0 && dsum <= 1e-3f * (float)k) || it >= a.max_iter;
+    float sg = 0.f;
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
-      const float phi = dot[j] + fmaxf(__expf(lse[j] - lmax), kTiny);
-      rr[j] = cts[j] * __builtin_amdgcn_rcpf(phi);
+      rr[j] = cts[j] * __builtin_amdgcn_rcpf(dot[j] + eps[j]);
+      sg = fmaf(rr[j], dot[j], sg);
       if (BOUND && last && cts[j] != 0.f) {
         b_tok += (double)cts[j] * ((double)__logf(fmaxf(dot[j], kTiny)) + a.logscale[ids[j]]);
         c_tok += (double)cts[j];
       }
     }
     if (last) break;
+    const float cs_next = digamma_fast(asum + wave_sum_dpp(sg));  // ψ(Σγ') for the next eθ
 
     // Phase B: s = Bᵀ r over the slice, reduce-scattered so the lane owns p6[0 .. N6)
-    float p1[N1];
+    // (pairs: topics (2p, 2p+1) → xs, (N1+2p, N1+2p+1) → ys; r_j broadcast to both halves)
+    float xs[N1], ys[N1];
 #pragma unroll
-    for (int q = 0; q < N1; ++q) {
-      float x = 0.f, y = 0.f;
+    for (int p = 0; p < H / 2; ++p) {
+      f2 x = f2{0.f, 0.f}, y = f2{0.f, 0.f};
 #pragma unroll
       for (int j = 0; j < ROWS; ++j) {
-        x = fmaf(B[j][q], rr[j], x);
-        if (N1 + q < KW) y = fmaf(B[j][N1 + q], rr[j], y);
+        const f2 rj = f2{rr[j], rr[j]};
+        x = __builtin_elementwise_fma(B[j][p], rj, x);
+        y = __builtin_elementwise_fma(B[j][H / 2 + p], rj, y);
       }
-      p1[q] = swap32_pair(x, true, y);
+      xs[2 * p] = x.x;
+      xs[2 * p + 1] = x.y;
+      ys[2 * p] = y.x;
+      ys[2 * p + 1] = y.y;
     }
-    float p2[N2];
+    float p1[N1];
+    swap_add_n<true, N1>(xs, ys, p1);
+    float ys2[N2];
 #pragma unroll
-    for (int q = 0; q < N2; ++q) p2[q] = swap16_pair(p1[q], true, (N2 + q < N1) ? p1[N2 + q] : 0.f);
+    for (int q = 0; q < N2; ++q) ys2[q] = (N2 + q < N1) ? p1[N2 + q] : 0.f;
+    float p2[N2];
+    swap_add_n<false, N2>(p1, ys2, p2);
     float p3[N3];
 #pragma unroll
     for (int q = 0; q < N3; ++q)
@@ -295,35 +323,36 @@ __global__ __launch_bounds__(64 * SplitShape<KMAX>::W, 2) void k_estep_split(ESt
     for (int q = 0; q < N6; ++q)
       p6[q] = rs_dpp<DPP_QP_1032>(p5[q], (N6 + q < N5) ? p5[N6 + q] : 0.f, lane & 1);
 
-    // Phase C: γ ← eθ' ⊙ s + α on the owned topics; Σ|Δγ|, Σγ, max γ over the document
+    // Phase C: γ ← eθ ⊙ s + α on the owned topics; this wave's Σ|Δγ|
     dsum = 0.f;
-    gsum = 0.f;
-    gmax = 0.f;
 #pragma unroll
     for (int s = 0; s < N6; ++s) {
       if (own[s]) {
         const float g = fmaf(eth[s], p6[s], alp[s]);
         dsum += fabsf(g - gam[s]);
         gam[s] = g;
-        gsum += g;
-        gmax = fmaxf(gmax, g);
       }
     }
-    block_reduce(dsum, gsum, gmax);
-    // Phase D: eθ' = exp(ψ(γ) − ψ(max γ)) into the wave's LDS slice
-    psimax = digamma_fast(gmax);
-    lmax = psimax - digamma_fast(gsum);
+    dsum = wave_sum_dpp(dsum);
+    // Phase D: eθ = exp(ψ(γ) − ψ(Σγ)) into the wave's LDS slice
+    cs = cs_next;
 #pragma unroll
     for (int s = 0; s < N6; ++s) {
       if (own[s]) {
-        eth[s] = __expf(digamma_fast(gam[s]) - psimax);
+        eth[s] = __expf(digamma_fast(gam[s]) - cs);
         my_eth[tl[s]] = eth[s];
       }
     }
     __builtin_amdgcn_wave_barrier();
     ++it;
-    done = dsum <= 1e-3f * (float)k;
   }
+
+  // exact Σγ of the final γ (outputs and bound); the loop's last barrier used buffer it & 1
+  gsum = 0.f;
+#pragma unroll
+  for (int s = 0; s < N6; ++s) gsum += gam[s];
+  gsum = wave_sum_dpp(gsum);
+  exchange((it + 1) & 1, nullptr, 0, gsum, dummy);
 
   // ---- outputs: topic-level from each wave's slice, token-level from wave 0
   const double psisum = digamma_t<double>((double)gsum);
@@ -381,20 +410,28 @@ __global__ __launch_bounds__(64 * SplitShape<KMAX>::W, 2) void k_estep_split(ESt
         tp += s_bd[w][0];
         as += s_bd[w][1];
       }
-      const double elog_max = digamma_t<double>((double)gmax) - psisum;
+      const double elog_max = (double)cs - psisum;  // log of the scale eθ carried (≈ 0)
       a.bound[mem] = tok + ct * elog_max + tp + (lgamma(as) - lgamma((double)gsum));
     }
   }
 }
 
-template <int KMAX>
-void launch_kmax(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound) {
+template <class S>
+void launch_shape(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound) {
   const dim3 grid((unsigned)a.n);
-  const int threads = 64 * SplitShape<KMAX>::W;
-  if (stats) k_estep_split<KMAX, true, false><<<grid, threads, 0, s>>>(a);
-  else if (bound) k_estep_split<KMAX, false, true><<<grid, threads, 0, s>>>(a);
-  else k_estep_split<KMAX, false, false><<<grid, threads, 0, s>>>(a);
+  const int threads = 64 * S::W;
+  if (stats) k_estep_split<S, true, false><<<grid, threads, 0, s>>>(a);
+  else if (bound) k_estep_split<S, false, true><<<grid, threads, 0, s>>>(a);
+  else k_estep_split<S, false, false><<<grid, threads, 0, s>>>(a);
   KERNEL_CHECK();
+}
+
+int shape_override() {
+  static const int v = [] {
+    const char* e = getenv("STC_WAVE_SHAPE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 }  // namespace
@@ -408,9 +445,15 @@ int wave_kmax(int k) {
 
 int wave_row_cap(int k) {
   switch (wave_kmax(k)) {
-    case 64: return 64 * SplitShape<64>::ROWS;
-    case 104: return 64 * SplitShape<104>::ROWS;
-    case 128: return 64 * SplitShape<128>::ROWS;
+    case 64: return 64 * Shape64::ROWS;
+    case 104:
+      switch (shape_override()) {
+        case 1: return 64 * Shape104b::ROWS;
+        case 2: return 64 * Shape104c::ROWS;
+        case 3: return 64 * Shape104d::ROWS;
+        default: return 64 * Shape104::ROWS;
+      }
+    case 128: return 64 * Shape128::ROWS;
     default: return 0;
   }
 }
@@ -418,9 +461,16 @@ int wave_row_cap(int k) {
 void launch_estep_wave(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound) {
   if (a.n == 0) return;
   switch (wave_kmax(a.k)) {
-    case 64: launch_kmax<64>(s, a, stats, bound); break;
-    case 104: launch_kmax<104>(s, a, stats, bound); break;
-    case 128: launch_kmax<128>(s, a, stats, bound); break;
+    case 64: launch_shape<Shape64>(s, a, stats, bound); break;
+    case 104:
+      switch (shape_override()) {
+        case 1: launch_shape<Shape104b>(s, a, stats, bound); break;
+        case 2: launch_shape<Shape104c>(s, a, stats, bound); break;
+        case 3: launch_shape<Shape104d>(s, a, stats, bound); break;
+        default: launch_shape<Shape104>(s, a, stats, bound); break;
+      }
+      break;
+    case 128: launch_shape<Shape128>(s, a, stats, bound); break;
     default: throw Error(STC_ERR_INVALID_ARG, "wave E-step: k > 128");
   }
 }

@@ -171,6 +171,8 @@ __host__ __device__ inline R digamma_t(R x) {
               f * (R(-1.0 / 132.0) + f * (R(691.0 / 32760.0) + f * (R(-1.0 / 12.0) + f * R(3617.0) / R(8160.0))))))));
   return r + log(x) - R(0.5) / x + t;
 }
+// ln x for positive normal x: v_log_f32 (log2) · ln 2, without the denormal-range fixup __logf carries
+__device__ __forceinline__ float ln_pos(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
 // fp32 digamma for the E-step inner loop: ψ(x) = ψ(x+6) − Σ_{i<6} 1/(x+i) unconditionally (no
 // data-dependent loop ⇒ no lane divergence), v_rcp_f32 / v_log_f32, Breeze's asymptotic series.
 __device__ inline float digamma_fast(float x) {
@@ -180,7 +182,7 @@ __device__ inline float digamma_fast(float x) {
   const float iy = __builtin_amdgcn_rcpf(y);
   const float f = iy * iy;
   const float t = f * (-1.f / 12.f + f * (1.f / 120.f + f * (-1.f / 252.f + f * (1.f / 240.f + f * (-1.f / 132.f)))));
-  return __logf(y) - 0.5f * iy + t - r;
+  return ln_pos(y) - 0.5f * iy + t - r;
 }
 
 __host__ __device__ inline double trigamma_d(double x) {
@@ -202,7 +204,12 @@ __host__ __device__ inline double trigamma_d(double x) {
 // involutions inside each 16-lane row (row_mirror, row_half_mirror, quad_perm 1032 and 2301).
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+  // all-lanes-valid permutations only (mirrors, quad_perm): bound_ctrl never fires, no `old` operand
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// max of two non-negative floats as an unsigned compare of their bits (no NaN canonicalisation)
+__device__ __forceinline__ float max_nonneg(float a, float b) {
+  return __builtin_bit_cast(float, max(__builtin_bit_cast(unsigned, a), __builtin_bit_cast(unsigned, b)));
 }
 // Compiler hazard (ROCm 7.2 hipcc, gfx950): with __builtin_amdgcn_permlane{16,32}_swap the compiler
 // sometimes reads the FIRST result register for both results (`v_add v0, v0, v0` after the swap;
@@ -227,6 +234,82 @@ __device__ __forceinline__ float swap16_pair(float v, bool add, float w) {
   pswap16(x, y);
   const float a = __builtin_bit_cast(float, x), b = __builtin_bit_cast(float, y);
   return add ? a + b : fmaxf(a, b);
+}
+// Batched swaps: up to four independent swaps behind one hazard nop.
+template <bool D32>
+__device__ __forceinline__ void pswap_4(unsigned& a0, unsigned& b0, unsigned& a1, unsigned& b1, unsigned& a2,
+                                        unsigned& b2, unsigned& a3, unsigned& b3) {
+  if constexpr (D32)
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\tv_permlane32_swap_b32 %2, %3\n\t"
+                 "v_permlane32_swap_b32 %4, %5\n\tv_permlane32_swap_b32 %6, %7"
+                 : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1), "+v"(a2), "+v"(b2), "+v"(a3), "+v"(b3));
+  else
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3\n\t"
+                 "v_permlane16_swap_b32 %4, %5\n\tv_permlane16_swap_b32 %6, %7"
+                 : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1), "+v"(a2), "+v"(b2), "+v"(a3), "+v"(b3));
+}
+template <bool D32>
+__device__ __forceinline__ void pswap_2(unsigned& a0, unsigned& b0, unsigned& a1, unsigned& b1) {
+  if constexpr (D32)
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\tv_permlane32_swap_b32 %2, %3"
+                 : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1));
+  else
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\tv_permlane16_swap_b32 %2, %3"
+                 : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1));
+}
+template <bool D32>
+__device__ __forceinline__ void pswap_1(unsigned& a0, unsigned& b0) {
+  if constexpr (D32) pswap32(a0, b0);
+  else pswap16(a0, b0);
+}
+// reduce-scatter step over lane distance 32 (D32) or 16, N pairs: lanes with the role bit clear
+// keep the xs set, the others the ys set; out[i] = this lane's kept value + the partner's
+template <bool D32, int N>
+__device__ __forceinline__ void swap_add_n(const float* xs, const float* ys, float* out) {
+  unsigned x[N], y[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    x[i] = __builtin_bit_cast(unsigned, xs[i]);
+    y[i] = __builtin_bit_cast(unsigned, ys[i]);
+  }
+  constexpr int N4 = N / 4 * 4;
+#pragma unroll
+  for (int b = 0; b < N4; b += 4) pswap_4<D32>(x[b], y[b], x[b + 1], y[b + 1], x[b + 2], y[b + 2], x[b + 3], y[b + 3]);
+  if constexpr (N - N4 >= 2) pswap_2<D32>(x[N4], y[N4], x[N4 + 1], y[N4 + 1]);
+  if constexpr ((N - N4) % 2 == 1) pswap_1<D32>(x[N - 1], y[N - 1]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = __builtin_bit_cast(float, x[i]) + __builtin_bit_cast(float, y[i]);
+}
+// three wave all-reduces at once (Σ a, Σ b, max c ≥ 0): the swaps share their hazard nops
+__device__ __forceinline__ void wave_reduce3(float& a, float& b, float& c) {
+  {
+    unsigned a0 = __builtin_bit_cast(unsigned, a), a1 = a0, b0 = __builtin_bit_cast(unsigned, b), b1 = b0,
+             c0 = __builtin_bit_cast(unsigned, c), c1 = c0, d0 = 0, d1 = 0;
+    pswap_4<true>(a0, a1, b0, b1, c0, c1, d0, d1);
+    a = __builtin_bit_cast(float, a0) + __builtin_bit_cast(float, a1);
+    b = __builtin_bit_cast(float, b0) + __builtin_bit_cast(float, b1);
+    c = max_nonneg(__builtin_bit_cast(float, c0), __builtin_bit_cast(float, c1));
+  }
+  {
+    unsigned a0 = __builtin_bit_cast(unsigned, a), a1 = a0, b0 = __builtin_bit_cast(unsigned, b), b1 = b0,
+             c0 = __builtin_bit_cast(unsigned, c), c1 = c0, d0 = 0, d1 = 0;
+    pswap_4<false>(a0, a1, b0, b1, c0, c1, d0, d1);
+    a = __builtin_bit_cast(float, a0) + __builtin_bit_cast(float, a1);
+    b = __builtin_bit_cast(float, b0) + __builtin_bit_cast(float, b1);
+    c = max_nonneg(__builtin_bit_cast(float, c0), __builtin_bit_cast(float, c1));
+  }
+  a += dpp_f<0x140>(a);
+  b += dpp_f<0x140>(b);
+  c = max_nonneg(c, dpp_f<0x140>(c));
+  a += dpp_f<0x141>(a);
+  b += dpp_f<0x141>(b);
+  c = max_nonneg(c, dpp_f<0x141>(c));
+  a += dpp_f<0xB1>(a);
+  b += dpp_f<0xB1>(b);
+  c = max_nonneg(c, dpp_f<0xB1>(c));
+  a += dpp_f<0x4E>(a);
+  b += dpp_f<0x4E>(b);
+  c = max_nonneg(c, dpp_f<0x4E>(c));
 }
 __device__ __forceinline__ float wave_sum_dpp(float v) {
   v = swap32_pair(v, true, v);

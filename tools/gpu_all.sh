@@ -14,3 +14,4 @@ step diag_wave 240 python tools/diag_wave.py
 step pytest_gpu 400 python -m pytest tests -x -q -m gpu
 step bench_wave 240 python bench.py --steps 10 --warmup 10 --no-cpu-baseline
 STC_DISABLE_WAVE=1 step bench_v1 240 python bench.py --steps 10 --warmup 10 --no-cpu-baseline
+STC_WAVE_SHAPE=1 step bench_shape1 240 python bench.py --steps 10 --warmup 10 --no-cpu-baseline
