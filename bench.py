@@ -11,10 +11,16 @@ shard (corpusSize = N·1M for the λ update), one RCCL all-reduce of k×V sstats
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N   (one rank per GPU)
 
 Rank 0 prints ONE JSON line.  value = Σ_ranks minibatch docs in the K timed steps ÷ max-over-ranks
-wall time.  roofline: SURVEY.md §8(d) algorithmic bytes per doc (nnz·(4+4) + 2·nnz·k·4 + 4k) over
-the E-step phase (k_estep + term sort + sstats SpMM kernels, HIP events on the library stream).
-cpu_baseline: the NumPy restatement (oracle/, one core) timed on a bounded sample of the same docs
-at the same model state.
+wall time.  Model state: timing starts after exactly --state-minibatches (20)
+minibatches from λ₀ (burn-in + warmup), so the inner-iteration count does not depend on --warmup;
+the first 3 minibatches from λ₀ are timed separately as the "cold" figure.
+roofline: SURVEY.md §8(d) algorithmic bytes per doc (nnz·(4+4) + 2·nnz·k·4 + 4k) over the E-step
+phase (k_estep_split + term sort + sstats SpMM kernels, HIP events on the library stream);
+traffic: the PMC FETCH_SIZE(×2, gfx950)+WRITE_SIZE of the same kernels from the committed rocprofv3
+summary of this workload (profiles/, tools/gpu_prof.sh).  roofline_compute: the E-step kernel's
+fp32 flops (4·nnz·k per inner iteration) against the 157.3 TF fp32 peak.
+cpu_baseline: oracle/lda_oracle.c (fp64, OpenMP, all host cores) timed on a bounded sample of the
+same docs at the same model state.
 """
 import argparse
 import json
@@ -29,6 +35,8 @@ sys.path.insert(0, os.path.join(ROOT, "spark-text-clustering_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+FP32_PEAK_TFS = 157.3  # MI355X dense fp32 (vector v_pk_fma_f32 = MFMA f32 rate; MI355X_MICROARCH.md)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
 def parse():
@@ -44,6 +52,8 @@ def parse():
     p.add_argument("--corpus", default="zipf", choices=["zipf", "zipf-lda"])
     p.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     p.add_argument("--seed", type=int, default=20261015)
+    p.add_argument("--state-minibatches", type=int, default=20,
+                   help="minibatches applied from λ₀ before timing (burn-in + warmup)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
 
@@ -52,6 +62,22 @@ def algorithmic_bytes(nnz, k, docs):
     """ids + counts (4+4 B per nnz), one k-wide fp32 row gathered and one
     scattered per nnz, γ out (4k B per doc)."""
     return nnz * 8.0 + 2.0 * nnz * k * 4.0 + docs * 4.0 * k
+
+
+def pmc_traffic(a):
+    """HBM bytes per minibatch of the E-step phase kernels from the committed PMC summary
+    (tools/pmc_summary.py over tools/gpu_prof.sh's separate FETCH_SIZE / WRITE_SIZE passes), if it
+    was measured on this workload; FETCH_SIZE ×2 per the gfx950 correction (MI355X_MICROARCH.md)."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return None, "no PMC summary committed"
+    w = pm.get("workload", {})
+    if (w.get("docs"), w.get("k"), w.get("vocab"), w.get("tokens"), w.get("fraction"), w.get("corpus")) != \
+            (a.docs, a.k, a.vocab, a.tokens, a.fraction, a.corpus):
+        return None, "PMC summary is for a different workload"
+    return pm["estep_phase_bytes_per_step"], f"{os.path.basename(PMC_SUMMARY)} ({pm.get('note', '')})"
 
 
 def cpu_baseline(h, corpus, k, seed, budget_s=12.0):
@@ -129,7 +155,21 @@ def main():
     h.set_corpus(dcorp, a.docs * world)
     h.init_random(a.seed)
 
-    for _ in range(a.warmup):
+    # cold: the first 3 minibatches from λ₀ (random Gamma topics), timed on their own
+    ctx.synchronize()
+    cc0 = h.counters()
+    t0 = time.perf_counter()
+    n_cold = 3
+    for _ in range(n_cold):
+        h.next(stats=False)
+    ctx.synchronize()
+    cold_s = time.perf_counter() - t0
+    cc1 = h.counters()
+    cold = {"docs_per_s": (cc1["docs"] - cc0["docs"]) / cold_s,
+            "mean_inner_iters": (cc1["inner_iters"] - cc0["inner_iters"]) / max(1, cc1["docs"] - cc0["docs"]),
+            "minibatches": n_cold}
+    burn = max(0, a.state_minibatches - n_cold - a.warmup)
+    for _ in range(burn + a.warmup):
         h.next(stats=False)
     ctx.synchronize()
     c0 = h.counters()
@@ -179,8 +219,14 @@ def main():
     estep_ms = phases["estep"] + phases["sstats"]
     per_step_docs = docs_local / max(1, a.steps)
     per_step_nnz = entries_local / max(1, a.steps)
+    per_step_iters = iters_local / max(1, a.steps)
     alg = algorithmic_bytes(per_step_nnz, a.k, per_step_docs)
     achieved = alg / (estep_ms * 1e-3) / 1e9
+    # E-step kernel flops: φ = B·eθ and Bᵀr, 2 FMAs per (entry, topic) per inner iteration
+    mean_nnz = per_step_nnz / max(1.0, per_step_docs)
+    flops = 4.0 * mean_nnz * a.k * per_step_iters
+    tflops = flops / (phases["estep"] * 1e-3) / 1e12
+    traffic, traffic_note = pmc_traffic(a)
     cpu = None
     if not a.no_cpu_baseline:
         cpu = cpu_baseline(h, corpus, a.k, a.seed)
@@ -195,7 +241,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32" if a.dtype == "f32" else "fp64",
+        "dtype": a.dtype,
         "data": f"synthetic {a.corpus} corpus (seeded, generated in {gen_s:.0f} s), resident in HBM",
         "config": {
             "workload": f"online LDA minibatch steps: {a.docs} docs x {a.tokens} tokens per GPU, "
@@ -204,14 +250,21 @@ def main():
             "subsampling_rate": a.fraction, "corpus": a.corpus, "parallelism": f"dp{world}",
             "mean_nnz_per_doc": entries_all / max(1.0, docs_all),
             "mean_inner_iters": iters_all / max(1.0, docs_all),
+            "model_state": f"after {a.state_minibatches} minibatches from lambda0 (Gamma(100,1/100))",
+            "cold": cold,
             "phase_ms": {k: round(v, 4) for k, v in phases.items() if k != "steps"},
             "estep_only_docs_per_s": per_step_docs * world / (estep_ms * 1e-3),
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "kernel": "E-step phase (k_estep + term radix sort + k_sstats/k_fixup)",
-            "algorithmic_bytes_per_step": alg, "phase_ms_per_step": estep_ms,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": "E-step phase: k_estep_split (+k_estep for long docs) + term radix sort + k_sstats/k_fixup",
+            "algorithmic_bytes_per_step": alg, "phase_ms_per_step": estep_ms, "traffic_source": traffic_note,
+        },
+        "roofline_compute": {
+            "bound": "valu_fp32", "achieved": tflops, "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": tflops / FP32_PEAK_TFS, "kernel": "k_estep_split", "flops_per_step": flops,
+            "kernel_ms_per_step": phases["estep"],
         },
         "cpu_baseline": cpu,
     }

@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 kernel stats + separate PMC passes (HBM traffic, SQ issue/wait) of the bench workload.
 # Each step has its own time limit; the script stops at the first failure.
+# Summarise afterwards (here): python tools/pmc_summary.py gpurun_out/prof --tag rNN
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof; rm -rf $OUT; mkdir -p $OUT
@@ -11,7 +12,7 @@ run() {  # run NAME SECONDS ARGS...
   local rc=$?; echo "$name rc=$rc" >> $OUT/status.log; return $rc
 }
 run stats 300 --kernel-trace --stats &&
-run fetch 300 --pmc FETCH_SIZE --kernel-include-regex "k_estep|k_sstats|k_fixup|Radix|k_lambda|k_expelog" &&
-run write 300 --pmc WRITE_SIZE --kernel-include-regex "k_estep|k_sstats|k_fixup|Radix|k_lambda|k_expelog" &&
+run fetch 300 --pmc FETCH_SIZE &&
+run write 300 --pmc WRITE_SIZE &&
 run sq 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS --kernel-include-regex "k_estep" &&
 run grbm 300 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-include-regex "k_estep"

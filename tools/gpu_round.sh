@@ -1,12 +1,14 @@
 #!/bin/bash
-# One GPU session: tests, then the default bench, then a rocprofv3 kernel-trace of a short bench.
-set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
-echo "pytest rc=$?" >> gpurun_out/status.log
-timeout -k 10 500 python bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err
-rc=$?; echo "bench rc=$rc" >> gpurun_out/status.log
-[ $rc -eq 0 ] || exit $rc
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 5 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_bench.log 2>&1
-echo "rocprof rc=$?" >> $GRAFT_REPO_ROOT/gpurun_out/status.log
+# Round measurement: GPU tests, smoke, the default bench line (with cpu_baseline), then profiles.
+mkdir -p gpurun_out; : > gpurun_out/status.log
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" >> gpurun_out/status.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+step pytest_gpu 600 python -m pytest tests -x -q -m gpu
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench 400 python bench.py
+step prof 1000 bash tools/gpu_prof.sh
