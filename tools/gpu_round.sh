@@ -8,7 +8,7 @@ step() {  # step NAME SECONDS CMD...
   echo "$name rc=$rc" >> gpurun_out/status.log
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-step pytest_gpu 600 python -m pytest tests -x -q -m gpu
+step pytest_gpu 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 400 python bench.py
 step prof 1000 bash tools/gpu_prof.sh
