@@ -1,0 +1,76 @@
+// estep_common.h — pieces shared by the register-resident E-step kernels (lda_wave.hip,
+// lda_grid.hip): Spark's φ epsilon in log space, packed-FMA operand type, reduce-scatter helpers
+// and the diagnostic s_memtime stamps.
+#pragma once
+
+#include "lda_kernels.h"
+
+namespace stc {
+namespace lda {
+
+constexpr double kLogEps = -230.25850929940458;  // ln(1e-100): Spark's φ epsilon (see lda.hip)
+constexpr float kTiny = 1.17549435e-38f;         // FLT_MIN
+
+typedef float f2 __attribute__((ext_vector_type(2)));  // v_pk_fma_f32 operand pair
+
+constexpr int hup(int n) { return (n + 1) / 2; }
+
+// reduce-scatter step through a DPP involution (row_mirror / row_half_mirror / quad_perm): lanes
+// with the role bit clear keep topic set X, the others Y; the partner sends the set it drops.
+template <int CTRL>
+__device__ __forceinline__ float rs_dpp(float x, float y, bool hi) {
+  const float keep = hi ? y : x;
+  const float send = hi ? x : y;
+  return keep + dpp_f<CTRL>(send);
+}
+// DPP controls (all lanes valid): row_mirror i↔15−i, row_half_mirror i↔7−i, row_ror:8 i↔i^8 (in a
+// 16-lane row), quad_perm [3,2,1,0] i↔i^3, [1,0,3,2] i↔i^1, [2,3,0,1] i↔i^2
+constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141, DPP_ROW_ROR8 = 0x128,
+              DPP_QP_3210 = 0x1B, DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E;
+
+// Diagnostic build only (make stamp → libstc_stamp.so, tools/stamp_estep.py): s_memtime stamps at
+// the phase boundaries of the inner loop, summed per phase over every wave of a launch.  The
+// product library compiles STAMP(i) to nothing.
+#ifdef STC_STAMP
+constexpr int kStamps = 12;
+// one copy per translation unit (no relocatable device code): each TU exports its own reader
+static __device__ unsigned long long g_stamps[kStamps];
+__device__ __forceinline__ unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define STAMP_DECL unsigned long long st_acc[::stc::lda::kStamps] = {}, st_last = ::stc::lda::stamp_now();
+#define STAMP(i)                                         \
+  do {                                                   \
+    const unsigned long long t_ = ::stc::lda::stamp_now(); \
+    st_acc[i] += t_ - st_last;                           \
+    st_last = t_;                                        \
+  } while (0)
+#define STAMP_FLUSH                                                  \
+  if ((threadIdx.x & 63) == 0)                                       \
+    for (int i_ = 0; i_ < ::stc::lda::kStamps; ++i_) atomicAdd(&::stc::lda::g_stamps[i_], st_acc[i_]);
+// diagnostic reader: copies (and optionally clears) this TU's per-phase cycle sums
+#define STC_STAMP_READER(NAME)                                                                  \
+  extern "C" int NAME(unsigned long long* out, int n, int reset) {                              \
+    if (n > ::stc::lda::kStamps) n = ::stc::lda::kStamps;                                       \
+    if (hipDeviceSynchronize() != hipSuccess) return 3;                                         \
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(::stc::lda::g_stamps), n * sizeof(unsigned long long)) != hipSuccess) \
+      return 3;                                                                                 \
+    if (reset) {                                                                                \
+      unsigned long long z[::stc::lda::kStamps] = {};                                           \
+      if (hipMemcpyToSymbol(HIP_SYMBOL(::stc::lda::g_stamps), z, sizeof(z)) != hipSuccess) return 3; \
+    }                                                                                           \
+    return 0;                                                                                   \
+  }
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_FLUSH
+#define STC_STAMP_READER(NAME)
+#endif
+
+}  // namespace lda
+}  // namespace stc

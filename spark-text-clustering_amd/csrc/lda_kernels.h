@@ -62,6 +62,10 @@ void launch_estep(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound);
 int wave_kmax(int k);                  // 0 when the wave kernel does not apply
 int wave_row_cap(int k);               // max nnz a wave keeps in VGPRs (0 if n/a)
 void launch_estep_wave(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound);
+// Row-lane × topic-group grid E-step (lda_grid.hip), the default behind the two entry points above
+// (STC_WAVE_KERNEL=split selects the topic-split kernel of lda_wave.hip instead).
+int grid_row_cap(int k);
+void launch_estep_grid(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound);
 
 // Batch partition: slots [0, n_short) = members with nnz <= cap (wave kernel), then the rest.
 void launch_part_flags(hipStream_t s, const int64_t* indptr, const int32_t* batch, int64_t n,

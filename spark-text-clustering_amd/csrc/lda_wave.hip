@@ -15,15 +15,12 @@
 //   Σ|Δγ| of each update rides along with the next φ exchange; ψ(Σγ) for eθ comes from the
 //   identity Σγ' = Σα + Σ_n r_n·dot_n, which every wave holds without an exchange.
 // Per inner iteration and lane: 2·ROWS·KW FMAs, ~100 permute/add/select, one barrier (W > 1).
-#include "lda_kernels.h"
+#include "estep_common.h"
 
 namespace stc {
 namespace lda {
 
 namespace {
-
-constexpr double kLogEps = -230.25850929940458;  // ln(1e-100): Spark's φ epsilon (see lda.hip)
-constexpr float kTiny = 1.17549435e-38f;         // FLT_MIN
 
 // (waves per document, topics per wave, rows per lane, waves per SIMD the registers allow)
 template <int W_, int KW_, int ROWS_, int OCC_>
@@ -39,25 +36,12 @@ using Shape104b = Shape<4, 28, 3, 3>;
 using Shape104c = Shape<4, 28, 4, 2>;
 using Shape104d = Shape<3, 36, 3, 3>;
 
-typedef float f2 __attribute__((ext_vector_type(2)));  // v_pk_fma_f32 operand pair
-
-constexpr int hup(int n) { return (n + 1) / 2; }
 template <int KW>
 constexpr int lvl(int L) {
   int n = KW;
   for (int i = 0; i < L; ++i) n = hup(n);
   return n;
 }
-
-// reduce-scatter step through a DPP involution (row_mirror / row_half_mirror / quad_perm): lanes
-// with the role bit clear keep topic set X, the others Y; the partner sends the set it drops.
-template <int CTRL>
-__device__ __forceinline__ float rs_dpp(float x, float y, bool hi) {
-  const float keep = hi ? y : x;
-  const float send = hi ? x : y;
-  return keep + dpp_f<CTRL>(send);
-}
-constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141, DPP_QP_3210 = 0x1B, DPP_QP_1032 = 0xB1;
 
 template <class S, bool STATS, bool BOUND>
 __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<float> a) {
@@ -73,6 +57,7 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<flo
   __shared__ double s_bd[W][2];
 
   if ((int64_t)blockIdx.x >= a.n) return;
+  STAMP_DECL
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t slot = a.slot0 + blockIdx.x;
@@ -245,6 +230,7 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<flo
   int it = 0;
   float dsum = 0.f, dummy = 0.f;
   double b_tok = 0.0, c_tok = 0.0;
+  STAMP(0);  // load + γ₀ + first eθ
   while (true) {
     // Phase A: φ_n = B_n·eθ + ε'_n ; r_n = cts_n / φ_n
     // (even and odd topics accumulate in the two halves of a packed pair)
@@ -266,8 +252,10 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<flo
 #pragma unroll
       for (int j = 0; j < ROWS; ++j) dot[j] = acc[j].x + acc[j].y;
     }
+    STAMP(1);  // phase A: eθ LDS reads + φ FMAs
     // Σ|Δγ| of the update that produced the current γ rides along
     exchange(it & 1, dot, ROWS, dsum, dummy);
+    STAMP(2);  // cross-wave φ exchange (LDS + barrier)
     const bool last = (it > 0 && dsum <= 1e-3f * (float)k) || it >= a.max_iter;
     float sg = 0.f;
 #pragma unroll
@@ -279,8 +267,10 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<flo
         c_tok += (double)cts[j];
       }
     }
+    STAMP(3);  // r = cts/φ, Σ r·dot
     if (last) break;
     const float cs_next = digamma_fast(asum + wave_sum_dpp(sg));  // ψ(Σγ') for the next eθ
+    STAMP(4);  // ψ(Σγ')
 
     // Phase B: s = Bᵀ r over the slice, reduce-scattered so the lane owns p6[0 .. N6)
     // (pairs: topics (2p, 2p+1) → xs, (N1+2p, N1+2p+1) → ys; r_j broadcast to both halves)
@@ -299,6 +289,7 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<flo
       ys[2 * p] = y.x;
       ys[2 * p + 1] = y.y;
     }
+    STAMP(5);  // phase B FMAs
     float p1[N1];
     swap_add_n<true, N1>(xs, ys, p1);
     float ys2[N2];
@@ -322,6 +313,7 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<flo
 #pragma unroll
     for (int q = 0; q < N6; ++q)
       p6[q] = rs_dpp<DPP_QP_1032>(p5[q], (N6 + q < N5) ? p5[N6 + q] : 0.f, lane & 1);
+    STAMP(6);  // reduce-scatter
 
     // Phase C: γ ← eθ ⊙ s + α on the owned topics; this wave's Σ|Δγ|
     dsum = 0.f;
@@ -334,6 +326,7 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<flo
       }
     }
     dsum = wave_sum_dpp(dsum);
+    STAMP(7);  // phase C: γ, Σ|Δγ|
     // Phase D: eθ = exp(ψ(γ) − ψ(Σγ)) into the wave's LDS slice
     cs = cs_next;
 #pragma unroll
@@ -345,6 +338,7 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<flo
     }
     __builtin_amdgcn_wave_barrier();
     ++it;
+    STAMP(8);  // phase D: ψ/exp, eθ to LDS
   }
 
   // exact Σγ of the final γ (outputs and bound); the loop's last barrier used buffer it & 1
@@ -414,6 +408,8 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<flo
       a.bound[mem] = tok + ct * elog_max + tp + (lgamma(as) - lgamma((double)gsum));
     }
   }
+  STAMP(9);  // outputs
+  STAMP_FLUSH
 }
 
 template <class S>
@@ -434,6 +430,14 @@ int shape_override() {
   return v;
 }
 
+bool use_grid() {
+  static const bool v = [] {
+    const char* e = getenv("STC_WAVE_KERNEL");
+    return !(e && std::strcmp(e, "split") == 0);
+  }();
+  return v;
+}
+
 }  // namespace
 
 int wave_kmax(int k) {
@@ -444,6 +448,7 @@ int wave_kmax(int k) {
 }
 
 int wave_row_cap(int k) {
+  if (use_grid()) return grid_row_cap(k);
   switch (wave_kmax(k)) {
     case 64: return 64 * Shape64::ROWS;
     case 104:
@@ -460,6 +465,7 @@ int wave_row_cap(int k) {
 
 void launch_estep_wave(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound) {
   if (a.n == 0) return;
+  if (use_grid()) return launch_estep_grid(s, a, stats, bound);
   switch (wave_kmax(a.k)) {
     case 64: launch_shape<Shape64>(s, a, stats, bound); break;
     case 104:
@@ -477,3 +483,5 @@ void launch_estep_wave(hipStream_t s, const EStepArgs<float>& a, bool stats, boo
 
 }  // namespace lda
 }  // namespace stc
+
+STC_STAMP_READER(stc_debug_stamps)

@@ -12,7 +12,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libstc.so")
+# STC_LIB selects an alternative build of the same library (e.g. the in-kernel stamp diagnostic
+# build tools/stamp_estep.py uses); default: the in-tree libstc.so
+LIB_PATH = os.environ.get("STC_LIB") or os.path.join(_HERE, "libstc.so")
 
 STC_OK, STC_ERR_INVALID_ARG, STC_ERR_HIP, STC_ERR_RCCL, STC_ERR_OOM, STC_ERR_STATE = range(6)
 STC_HASH_STANDARD, STC_HASH_SPARK24 = 0, 1

@@ -1,0 +1,91 @@
+"""GPU parity at the BASELINE.json configuration shapes, through the C ABI.
+
+* the E-step at each config's (V, k, doc length): k = 100 / V = 2^18 / 200 tokens (configs 2, 3),
+  k = 500 / V = 2^20 / 500 tokens (config 4) and k = 2000 / V = 2^18 / 50 tokens (config 5) — few
+  documents, so the oracle finishes in seconds, but the full V×k model on the device (the row
+  offsets id·kp pass 2^31 bytes at configs 4 and 5);
+* the full config-2 workload (1M docs × 200 tokens): one device-sampled minibatch, checked through
+  size-independent properties of the fixed point — Σ_t γ_t = Σα + Σ_n cts_n(1 − ε/φ_n) and
+  Σ_{v,t} sstats·expElogβ = Σ_n cts_n(1 − ε/φ_n) — and bitwise run-to-run determinism.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _tiled_topics(rng, V, k, P=4099):
+    """A V×k topicsMatrix tiled from a random P×k block (cheap to build, exact column sums)."""
+    base = rng.gamma(100.0, 0.01, size=(P, k)) * rng.uniform(0.2, 5.0, size=(P, 1))
+    reps = -(-V // P)
+    lam = np.tile(base, (reps, 1))[:V]
+    return lam
+
+
+def _eeb_rows(lam, ids, oracle):
+    """Spark's expElogβ restricted to rows `ids` (column sums over the whole vocabulary)."""
+    colsum = lam.sum(axis=0)
+    return np.exp(oracle.digamma(lam[ids]) - oracle.digamma(colsum)[None, :])
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(name="config2", V=1 << 18, k=100, L=200, D=24),
+    dict(name="config4", V=1 << 20, k=500, L=500, D=4),
+    dict(name="config5", V=1 << 18, k=2000, L=50, D=6),
+], ids=lambda c: c["name"])
+def test_estep_at_baseline_shapes(ctx, oracle, cfg):
+    import stc
+    from stc import synth
+
+    rng = np.random.default_rng(hash(cfg["name"]) & 0xFFFF)
+    V, k, D = cfg["V"], cfg["k"], cfg["D"]
+    corpus = synth.zipf_corpus(D, cfg["L"], V, seed=31 + k)
+    lam = _tiled_topics(rng, V, k)
+    g0 = rng.gamma(100.0, 0.01, size=(D, k))
+    h = stc.LdaHandle(ctx, k, V, dtype="f32")
+    dc = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F32)
+    h.set_corpus(dc, D)
+    h.set_topics(lam)
+    gamma, _, iters = h.estep(np.arange(D), g0)
+    alpha = np.full(k, 1.0 / k)
+    for i in range(D):
+        cid, cts = corpus.row(i)
+        eeb = _eeb_rows(lam, cid, oracle)
+        g, _, it = oracle.variational_topic_inference(np.arange(cid.size), cts, eeb, alpha, g0[i])
+        # fp32 E-step: 2e-3 relative per topic, with an absolute floor of 1e-7·Σγ for the topics
+        # that stay at α + (a sliver): their few ulps of Σγ are relative noise
+        np.testing.assert_allclose(gamma[i], g, rtol=2e-3, atol=1e-7 * g.sum(), err_msg=f"{cfg['name']} doc {i}")
+        assert abs(int(iters[i]) - it) <= max(2, it // 20), (iters[i], it)
+
+
+def test_full_size_minibatch_properties(ctx, oracle):
+    """BASELINE configs[1] at full size: 1M docs × 200 tokens, V = 2^18, k = 100, f = 0.05."""
+    import stc
+    from stc import synth
+
+    D, L, V, k = 1_000_000, 200, 1 << 18, 100
+    corpus = synth.make_corpus("zipf", D, L, V, k, 20261015)
+    dc = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F32)
+    h = stc.LdaHandle(ctx, k, V, mini_batch_fraction=0.05, optimize_doc_concentration=True, seed=1,
+                      dtype="f32")
+    h.set_corpus(dc, D)
+    h.init_random(1)
+    for _ in range(3):
+        s = h.next()
+        assert 45_000 < s["batch_docs"] < 55_000 and s["cap_hits"] == 0
+    lam = h.topics()
+    assert np.all(np.isfinite(lam)) and lam.min() > 0
+    alpha = h.alpha()
+    ids = np.random.default_rng(2).choice(D, size=20_000, replace=False)
+    gamma, stat, iters = h.estep(ids, None, want_stat=True)
+    gamma2, stat2, iters2 = h.estep(ids, None, want_stat=True)
+    assert np.array_equal(gamma, gamma2) and np.array_equal(stat, stat2) and np.array_equal(iters, iters2)
+    tok = np.array([corpus.row(i)[1].sum() for i in ids])
+    # Σ_t γ_t = Σα + Σ_n cts_n·(1 − ε/φ_n); ε/φ_n is negligible on this corpus
+    rel = np.abs(gamma.sum(axis=1) - alpha.sum() - tok) / tok
+    assert rel.max() < 2e-4, rel.max()
+    # Σ_{v,t} sstats_vt · expElogβ_vt = Σ_d Σ_n cts_n (φ normalisation)
+    eeb = oracle.topics_exp_elog_beta(lam)
+    tot = float(np.sum(stat * eeb))
+    assert abs(tot - tok.sum()) / tok.sum() < 1e-4, (tot, tok.sum())
+    assert iters.min() >= 1
