@@ -14,11 +14,11 @@ Rank 0 prints ONE JSON line.  value = Σ_ranks minibatch docs in the K timed ste
 wall time.  Model state: timing starts after exactly --state-minibatches (20)
 minibatches from λ₀ (burn-in + warmup), so the inner-iteration count does not depend on --warmup;
 the first 3 minibatches from λ₀ are timed separately as the "cold" figure.
-roofline: SURVEY.md §8(d) algorithmic bytes per doc (nnz·(4+4) + 2·nnz·k·4 + 4k) over the E-step
-phase (k_estep_split + term sort + sstats SpMM kernels, HIP events on the library stream);
-traffic: the PMC FETCH_SIZE(×2, gfx950)+WRITE_SIZE of the same kernels from the committed rocprofv3
-summary of this workload (profiles/, tools/gpu_prof.sh).  roofline_compute: the E-step kernel's
-fp32 flops (4·nnz·k per inner iteration) against the 157.3 TF fp32 peak.
+roofline: the dominant kernel, k_estep_grid (one launch per minibatch): SURVEY.md §8(d) algorithmic
+bytes per doc (nnz·(4+4) + 2·nnz·k·4 + 4k) × the launch's docs ÷ its HIP-event time on the library
+stream; traffic: that kernel's PMC FETCH_SIZE(×2, gfx950)+WRITE_SIZE per launch from the committed
+rocprofv3 summary of this workload (profiles/, tools/gpu_prof.sh).  roofline_compute: the same
+kernel's fp32 flops (4·nnz·k per inner iteration) against the 157.3 TF fp32 peak.
 cpu_baseline: oracle/lda_oracle.c (fp64, OpenMP, all host cores) timed on a bounded sample of the
 same docs at the same model state.
 """
@@ -65,7 +65,7 @@ def algorithmic_bytes(nnz, k, docs):
 
 
 def pmc_traffic(a):
-    """HBM bytes per minibatch of the E-step phase kernels from the committed PMC summary
+    """HBM bytes per launch of the training E-step kernel from the committed PMC summary
     (tools/pmc_summary.py over tools/gpu_prof.sh's separate FETCH_SIZE / WRITE_SIZE passes), if it
     was measured on this workload; FETCH_SIZE ×2 per the gfx950 correction (MI355X_MICROARCH.md)."""
     try:
@@ -77,7 +77,34 @@ def pmc_traffic(a):
     if (w.get("docs"), w.get("k"), w.get("vocab"), w.get("tokens"), w.get("fraction"), w.get("corpus")) != \
             (a.docs, a.k, a.vocab, a.tokens, a.fraction, a.corpus):
         return None, "PMC summary is for a different workload"
-    return pm["estep_phase_bytes_per_step"], f"{os.path.basename(PMC_SUMMARY)} ({pm.get('note', '')})"
+    if "estep_kernel_bytes_per_launch" not in pm:
+        return None, "PMC summary predates the per-launch E-step figure"
+    return pm["estep_kernel_bytes_per_launch"], f"{os.path.basename(PMC_SUMMARY)} ({pm.get('note', '')})"
+
+
+def hbm_copy_gbs(device):
+    """STREAM-style device copy (1 GiB → 1 GiB, torch) for the measured-HBM line next to the 8 TB/s spec."""
+    try:
+        import torch
+
+        if not torch.cuda.is_available():
+            return None
+        n = 1 << 28
+        x = torch.empty(n, dtype=torch.float32, device=f"cuda:{device}")
+        y = torch.empty_like(x)
+        for _ in range(3):
+            y.copy_(x)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(10):
+            y.copy_(x)
+        torch.cuda.synchronize()
+        gbs = 2.0 * 4.0 * n * 10 / (time.perf_counter() - t0) / 1e9
+        del x, y
+        torch.cuda.empty_cache()
+        return gbs
+    except Exception:
+        return None
 
 
 def cpu_baseline(h, corpus, k, seed, budget_s=12.0):
@@ -216,7 +243,9 @@ def main():
         return
 
     value = docs_all / elapsed
-    estep_ms = phases["estep"] + phases["sstats"]
+    # roofline of the dominant kernel: the training E-step (k_estep_grid), ONE launch per minibatch;
+    # SURVEY.md §8(d)'s bytes per doc × the docs of a launch ÷ its HIP-event time on the library stream
+    estep_ms = phases["estep"]
     per_step_docs = docs_local / max(1, a.steps)
     per_step_nnz = entries_local / max(1, a.steps)
     per_step_iters = iters_local / max(1, a.steps)
@@ -225,8 +254,9 @@ def main():
     # E-step kernel flops: φ = B·eθ and Bᵀr, 2 FMAs per (entry, topic) per inner iteration
     mean_nnz = per_step_nnz / max(1.0, per_step_docs)
     flops = 4.0 * mean_nnz * a.k * per_step_iters
-    tflops = flops / (phases["estep"] * 1e-3) / 1e12
+    tflops = flops / (estep_ms * 1e-3) / 1e12
     traffic, traffic_note = pmc_traffic(a)
+    copy_gbs = hbm_copy_gbs(local)
     cpu = None
     if not a.no_cpu_baseline:
         cpu = cpu_baseline(h, corpus, a.k, a.seed)
@@ -258,13 +288,16 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "E-step phase: k_estep_split (+k_estep for long docs) + term radix sort + k_sstats/k_fixup",
-            "algorithmic_bytes_per_step": alg, "phase_ms_per_step": estep_ms, "traffic_source": traffic_note,
+            "kernel": "k_estep_grid (lda_grid.hip): the training E-step, one launch per minibatch",
+            "algorithmic_bytes_per_launch": alg, "kernel_ms_per_launch": estep_ms,
+            "traffic_source": traffic_note, "hbm_copy_measured_GBs": copy_gbs,
+            "note": "the E-step is VALU-bound (~150 fixed-point iterations per doc over a register-resident "
+                    "block), so the HBM fraction is small by construction; see roofline_compute",
         },
         "roofline_compute": {
             "bound": "valu_fp32", "achieved": tflops, "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": tflops / FP32_PEAK_TFS, "kernel": "k_estep_split", "flops_per_step": flops,
-            "kernel_ms_per_step": phases["estep"],
+            "frac": tflops / FP32_PEAK_TFS, "kernel": "k_estep_grid", "flops_per_launch": flops,
+            "kernel_ms_per_launch": estep_ms,
         },
         "cpu_baseline": cpu,
     }

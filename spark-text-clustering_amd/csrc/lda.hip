@@ -576,8 +576,9 @@ void launch_colsum_reduce(hipStream_t s, const double* colpart, int64_t nblocks,
   KERNEL_CHECK();
 }
 
-// expElogβ'[v][t] = exp(ψ(λ_vt) − ψ(colsum_t) − m_v), m_v = max_t (ψ(λ_vt) − ψ(colsum_t)); one wave / term
-template <typename T>
+// expElogβ'[v][t] = exp(ψ(λ_vt) − ψ(colsum_t) − m_v), m_v = max_t (ψ(λ_vt) − ψ(colsum_t)); one wave
+// per term, each lane's Q topics held in registers so ψ(λ) is evaluated once per element
+template <typename T, int Q>
 __global__ __launch_bounds__(256) void k_expelogbeta(const double* __restrict__ lam,
                                                      const double* __restrict__ colsum, int64_t V,
                                                      int k, int kp, const double* __restrict__ gate,
@@ -590,20 +591,40 @@ __global__ __launch_bounds__(256) void k_expelogbeta(const double* __restrict__ 
   const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (v >= V) return;
   const double* lr = lam + v * k;
+  double e[Q];
   double m = -INFINITY;
-  for (int t = lane; t < k; t += 64) m = fmax(m, digamma_t<double>(lr[t]) - s_psic[t]);
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int t = lane + 64 * q;
+    e[q] = t < k ? digamma_t<double>(lr[t]) - s_psic[t] : -INFINITY;
+    m = fmax(m, e[q]);
+  }
   m = wave_max(m);
   T* br = Bp + v * kp;
-  for (int t = lane; t < kp; t += 64)
-    br[t] = t < k ? (T)exp(digamma_t<double>(lr[t]) - s_psic[t] - m) : T(0);
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int t = lane + 64 * q;
+    if (t < kp) br[t] = t < k ? (T)exp(e[q] - m) : T(0);
+  }
   if (lane == 0) logscale[v] = m;
 }
 
 template <typename T>
 void launch_expelogbeta(hipStream_t s, const double* lam, const double* colsum, int64_t V, int k,
                         int kp, const double* gate, T* Bp, double* logscale) {
-  k_expelogbeta<T><<<(unsigned)ceil_div(V, 4), 256, sizeof(double) * k, s>>>(lam, colsum, V, k, kp,
-                                                                              gate, Bp, logscale);
+  const unsigned grid = (unsigned)ceil_div(V, 4);
+  const size_t sh = sizeof(double) * k;
+  const int q = (kp + 63) / 64;
+#define STC_EEB(QQ) k_expelogbeta<T, QQ><<<grid, 256, sh, s>>>(lam, colsum, V, k, kp, gate, Bp, logscale)
+  if (q <= 1) STC_EEB(1);
+  else if (q <= 2) STC_EEB(2);
+  else if (q <= 4) STC_EEB(4);
+  else if (q <= 8) STC_EEB(8);
+  else if (q <= 16) STC_EEB(16);
+  else if (q <= 32) STC_EEB(32);
+  else if (q <= 64) STC_EEB(64);
+  else throw Error(STC_ERR_INVALID_ARG, "k > 4096 topics is not supported");
+#undef STC_EEB
   KERNEL_CHECK();
 }
 

@@ -14,7 +14,8 @@
 //     permlane16 swaps, then row_half_mirror / quad_perm involutions, all of which keep bit 3):
 //     KL values per lane instead of the 52 of the topic-split kernel (lda_wave.hip).
 //   γ, ψ(γ), exp on the owned topic (one per lane); eθ' of the group slice back through LDS.
-//   ψ(Σγ') from Σγ' = Σα + Σ_n r_n·dot_n (each row is held by two lanes: ½ of the wave sum).
+//   ψ(Σγ') from Σγ' = Σα + Σ_n cts_n − Σ_n cts_n·ε'_n/φ_n: a per-document constant unless a ballot
+//   finds a row whose ε' is visible at fp32 resolution.
 #include "estep_common.h"
 
 namespace stc {
@@ -188,8 +189,13 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
     xchg<S>(sm, 1, wave, lane, nullptr, 0, gsum, asum);
     d.asum = asum;
     // eθ = exp(ψ(γ) − ψ(Σγ)): Spark's unscaled exp(E[log θ]); inside the loop ψ(Σγ') comes from
-    // the Σα + Σ r·dot identity (a common scale on eθ: φ, r and the statistics are invariant to it)
+    // the Σα + Σcts − Σ cts·ε'/φ identity, so without live ε' it is one constant per document
     float cs = digamma_fast(gsum);
+    float ct = 0.f;
+#pragma unroll
+    for (int j = 0; j < R; ++j) ct += cts[j];
+    const float ctot = 0.5f * wave_sum_dpp(ct);  // Σ_n cts_n (each row is held by both groups)
+    const float cs_flat = digamma_fast(asum + ctot);
     float gam = d.gam, eth = d.own ? __expf(digamma_fast(gam) - cs) : 0.f;
     const float alp = d.alp;
     if (d.own) my_eth[d.tl] = eth;
@@ -226,11 +232,12 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
       xchg<S>(sm, it & 1, wave, lane, dot, R, dsum, dummy);  // Σ|Δγ| of the last update rides along
       STAMP(2);
       const bool last = (it > 0 && dsum <= k_tol) || it >= a.max_iter;
-      float sg = 0.f;
+      int eps_live = 0;
 #pragma unroll
       for (int j = 0; j < R; ++j) {
-        rr[j] = cts[j] * __builtin_amdgcn_rcpf(dot[j] + eps[j]);
-        sg = fmaf(rr[j], dot[j], sg);
+        const float ph = dot[j] + eps[j];
+        rr[j] = cts[j] * __builtin_amdgcn_rcpf(ph);
+        eps_live |= (cts[j] != 0.f) & (eps[j] * 16777216.f >= ph);  // ε' ≥ 2^-24·φ: visible in Σγ'
         if (BOUND && last && d.g == 0 && cts[j] != 0.f) {
           d.b_tok += (double)cts[j] * ((double)__logf(fmaxf(dot[j], kTiny)) + a.logscale[ids[j]]);
           d.c_tok += (double)cts[j];
@@ -238,7 +245,18 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
       }
       STAMP(3);
       if (last) break;
-      const float cs_next = digamma_fast(asum + 0.5f * wave_sum_dpp(sg));  // each row counted twice
+      // ψ(Σγ') for the next eθ from Σγ' = Σα + Σ_n cts_n − Σ_n cts_n·ε'_n/φ_n (exact in real
+      // arithmetic).  The ε' part is below the fp32 resolution of Σγ' unless some row has
+      // ε'_n ≥ 2^-24·φ_n (a ballot); only then is it reduced.  The decision and the sums are the same
+      // in every wave (like φ and r), so every wave scales its eθ slice identically.
+      float cs_next = cs_flat;
+      if (__any(eps_live)) {
+        float e = 0.f;
+#pragma unroll
+        for (int j = 0; j < R; ++j)  // cts·ε'/φ as cts·(1 − dot/φ): 0 for padding, cts when ε' = ∞
+          e = fmaf(cts[j], 1.f - dot[j] * __builtin_amdgcn_rcpf(dot[j] + eps[j]), e);
+        cs_next = digamma_fast(asum + ctot - 0.5f * wave_sum_dpp(e));  // each row is held twice
+      }
       STAMP(4);
 
       // Phase B: s = Bᵀr over the group's KL topics, then reduce-scatter over the 32 row lanes

@@ -66,6 +66,7 @@ class LdaHandle:
         self.handle = h
         self.k, self.vocab_size, self.dtype = cfg.k, cfg.vocab_size, cfg.dtype
         self.seed = cfg.seed
+        self.gamma_shape = cfg.gamma_shape
         self._corpus = None
 
     # ---- state
@@ -255,6 +256,65 @@ class LDAModel:
                 d.free()
 
     topicDistribution = transform
+
+    # ---- persistence: [U] LocalLDAModel.save / LocalLDAModel.load (SaveLoadV1_0 layout, stc.io)
+    def save(self, path, overwrite=False):
+        """Write this model as a Spark mllib LocalLDAModel directory (stock Spark can load it)."""
+        from . import io
+
+        io.save_local(path, self.topicsMatrix(), self.estimatedDocConcentration(), self.getTopicConcentration(),
+                      self._h.gamma_shape, overwrite=overwrite)
+
+    @staticmethod
+    def load(path, dtype="f32", seed=0, ctx: Context | None = None) -> "LDAModel":
+        """Read a Spark mllib LocalLDAModel directory onto the GPU."""
+        from . import io
+
+        m = io.load_local(path)
+        return LDAModel.from_topics(m["topics"], m["alpha"], m["eta"], gamma_shape=m["gamma_shape"], seed=seed,
+                                    dtype=dtype, ctx=ctx)
+
+
+class DistributedLDAModel:
+    """[U] DistributedLDAModel as the reference loads it (LDALoader.scala:37): the saved EM graph, read
+    from its parquet layout (stc.io).  What the reference then asks of it — describeTopics
+    (LDALoader.scala:66) and toLocal.topicDistribution (:108) — runs on the GPU through ``toLocal``
+    (topicsMatrix = the term vertices' counts n_wk)."""
+
+    def __init__(self, data):
+        self._d = data
+        self.k, self.vocabSize = data["k"], data["vocab_size"]
+        self.docConcentration = data["alpha"]
+        self.topicConcentration = data["eta"]
+        self.gammaShape = data["gamma_shape"]
+        self.iterationTimes = data["iteration_times"]
+        self._local = {}
+
+    @staticmethod
+    def load(path) -> "DistributedLDAModel":
+        from . import io
+
+        return DistributedLDAModel(io.load_distributed(path))
+
+    def isDistributed(self):
+        return True
+
+    def topicsMatrix(self):
+        return self._d["topics"].copy()
+
+    def globalTopicTotals(self):
+        return self._d["global_topic_totals"].copy()
+
+    def toLocal(self, dtype="f64", seed=0, ctx: Context | None = None) -> LDAModel:
+        key = (dtype, seed, id(ctx))
+        if key not in self._local:
+            self._local[key] = LDAModel.from_topics(self._d["topics"], self.docConcentration, self.topicConcentration,
+                                                    gamma_shape=self.gammaShape, seed=seed, dtype=dtype, ctx=ctx)
+        return self._local[key]
+
+    def describeTopics(self, maxTermsPerTopic=10, ctx: Context | None = None):
+        """Top terms per topic by n_wk / Σ_w n_wk (the EM model's column totals), on the GPU."""
+        return self.toLocal(ctx=ctx).describeTopics(maxTermsPerTopic)
 
 
 class LDA:

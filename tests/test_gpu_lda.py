@@ -221,3 +221,51 @@ def test_fit_pipeline_end_to_end(ctx, oracle):
     theta = model.transform(corpus)
     np.testing.assert_allclose(theta.sum(axis=1), 1.0, rtol=1e-5)
     assert len(model.describeTopics(5)) == k
+
+
+def test_model_save_load_round_trip_on_gpu(ctx, tmp_path):
+    """LocalLDAModel.save → LocalLDAModel.load (Spark's directory layout) keeps the model exactly:
+    same topicsMatrix, describeTopics and topicDistribution from the GPU."""
+    import stc
+
+    rng = np.random.default_rng(17)
+    V, k, D = 700, 6, 20
+    lam = rng.gamma(100.0, 0.01, size=(V, k)) * rng.uniform(0.5, 5.0, size=(V, 1))
+    m = stc.LDAModel.from_topics(lam, rng.uniform(0.1, 0.5, size=k), 0.2, dtype="f64", ctx=ctx)
+    path = str(tmp_path / "lda")
+    m.save(path)
+    m2 = stc.LDAModel.load(path, dtype="f64", ctx=ctx)
+    assert np.array_equal(m2.topicsMatrix(), lam)
+    assert np.array_equal(m2.estimatedDocConcentration(), m.estimatedDocConcentration())
+    for (t1, i1, w1), (t2, i2, w2) in zip(m.describeTopics(8), m2.describeTopics(8)):
+        assert t1 == t2 and np.array_equal(i1, i2) and np.array_equal(w1, w2)
+    corpus = random_corpus(rng, D, V, 1, 40)
+    g0 = rng.gamma(100.0, 0.01, size=(D, k))
+    assert np.array_equal(m.transform(corpus, gamma0=g0), m2.transform(corpus, gamma0=g0))
+
+
+def test_distributed_model_load_to_local_on_gpu(ctx, oracle, tmp_path):
+    """The reference's flow (LDALoader.scala:37, :66, :108) on a synthetic EM model saved in the
+    DistributedLDAModel layout: load → describeTopics → toLocal.topicDistribution, vs the oracle."""
+    import stc
+
+    rng = np.random.default_rng(18)
+    V, k, D = 500, 5, 12
+    nwk = rng.gamma(0.3, 20.0, size=(V, k))
+    docs = random_corpus(rng, D, V, 5, 60)
+    src = np.repeat(np.arange(D), np.diff(docs.indptr))
+    stc.io.save_distributed(str(tmp_path / "em"), np.arange(D), rng.uniform(1, 9, size=(D, k)), nwk,
+                            (src, docs.indices, docs.values), 11.0, 1.1)
+    dm = stc.DistributedLDAModel.load(str(tmp_path / "em"))
+    assert np.array_equal(dm.topicsMatrix(), nwk)
+    idx_o, w_o = oracle.describe_topics(nwk, 10)
+    for t, idx, w in dm.describeTopics(10, ctx=ctx):
+        assert np.array_equal(idx, idx_o[t])
+        np.testing.assert_allclose(w, w_o[t], rtol=1e-12)
+    g0 = rng.gamma(100.0, 0.01, size=(D, k))
+    theta = dm.toLocal(ctx=ctx).transform(docs, gamma0=g0)
+    eeb = oracle.topics_exp_elog_beta(nwk)
+    for i in range(D):
+        cid, cts = docs.row(i)
+        exp_t = oracle.topic_distribution(cid, cts, nwk, np.full(k, 11.0), g0[i], eeb)
+        np.testing.assert_allclose(theta[i], exp_t, rtol=1e-7, atol=1e-12)

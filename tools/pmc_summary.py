@@ -27,6 +27,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # kernels of the E-step phase (the bench roofline's "kernel"): E-step, term sort, sstats SpMM,
 # the stat memset, and the partition scans (rocprim; tiny)
 PHASE = re.compile(r"k_estep|k_sstats|k_fixup|rocprim|fillBuffer|k_part_|k_fill_batch|k_batch_nnz")
+# the dominant kernel (bench.py's roofline): the training E-step launches (STATS variant), one per minibatch
+ESTEP = re.compile(r"k_estep\w*<.*true, false>")
 
 
 def short(name):
@@ -87,17 +89,25 @@ def main():
         if PHASE.search(kn):
             phase_total += 2.0 * f_raw + w_b
     per_step = phase_total / max(1, steps)
+    est = {kn: v for kn, v in kernels.items() if ESTEP.search(kn)}
+    est_launches = max((v["dispatches"] for v in est.values()), default=0)
+    est_bytes = sum((v["fetch_bytes_x2_per_dispatch"] + v["write_bytes_per_dispatch"]) * v["dispatches"]
+                    for v in est.values()) / max(1, est_launches)
     wl = {"docs": a.docs, "tokens": a.tokens, "vocab": a.vocab, "k": a.k, "fraction": a.fraction,
           "corpus": a.corpus}
     detail = {"workload": wl, "minibatches_in_run": steps, "kernels": kernels, "sq_per_dispatch": sq,
-              "estep_phase_bytes_per_step": per_step}
+              "estep_phase_bytes_per_step": per_step, "estep_kernel": sorted(est),
+              "estep_kernel_bytes_per_launch": est_bytes}
     with open(os.path.join(out_dir, f"{a.tag}_pmc.json"), "w") as f:
         json.dump(detail, f, indent=1)
     with open(os.path.join(out_dir, "pmc_traffic.json"), "w") as f:
-        json.dump({"workload": wl, "estep_phase_bytes_per_step": per_step, "minibatches_in_run": steps,
-                   "note": f"{a.tag}: FETCH_SIZE x2 + WRITE_SIZE, E-step phase kernels, averaged over "
-                           f"{steps} minibatches (incl. burn-in)"}, f, indent=1)
-    print(json.dumps({"minibatches": steps, "estep_phase_bytes_per_step": per_step}))
+        json.dump({"workload": wl, "estep_kernel": sorted(est), "estep_kernel_bytes_per_launch": est_bytes,
+                   "estep_phase_bytes_per_step": per_step, "minibatches_in_run": steps,
+                   "note": f"{a.tag}: FETCH_SIZE x2 + WRITE_SIZE per launch of the training E-step kernel "
+                           f"(and of the whole E-step phase per minibatch), averaged over {steps} minibatches "
+                           f"(incl. burn-in)"}, f, indent=1)
+    print(json.dumps({"minibatches": steps, "estep_kernel_bytes_per_launch": est_bytes,
+                      "estep_phase_bytes_per_step": per_step}))
     for kn, v in kernels.items():
         if v["in_estep_phase"]:
             print(f"  {kn[:90]:90s} n={v['dispatches']:4d} fetch×2={v['fetch_bytes_x2_per_dispatch'] / 1e6:9.1f} MB "
