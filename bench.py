@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--state-minibatches", type=int, default=20,
                    help="minibatches applied from λ₀ before timing (burn-in + warmup)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-hbm-copy", action="store_true", help="skip the torch device-copy HBM probe")
     return p.parse_args()
 
 
@@ -83,28 +84,38 @@ def pmc_traffic(a):
 
 
 def hbm_copy_gbs(device):
-    """STREAM-style device copy (1 GiB → 1 GiB, torch) for the measured-HBM line next to the 8 TB/s spec."""
-    try:
-        import torch
+    """STREAM-style device-to-device copy (1 GiB, hipMemcpy through libamdhip64 via ctypes, timed with
+    HIP events) for the measured-HBM figure next to the 8 TB/s spec.  Reported, never fatal."""
+    import ctypes as C
 
-        if not torch.cuda.is_available():
-            return None
-        n = 1 << 28
-        x = torch.empty(n, dtype=torch.float32, device=f"cuda:{device}")
-        y = torch.empty_like(x)
+    try:
+        hip = C.CDLL("libamdhip64.so")
+        ok = (lambda r: r == 0)
+        n = 1 << 30
+        a, b = C.c_void_p(), C.c_void_p()
+        e0, e1 = C.c_void_p(), C.c_void_p()
+        if not (ok(hip.hipSetDevice(int(device))) and ok(hip.hipMalloc(C.byref(a), C.c_size_t(n)))
+                and ok(hip.hipMalloc(C.byref(b), C.c_size_t(n)))):
+            return "hipMalloc failed"
+        hip.hipMemset(a, 1, C.c_size_t(n))
+        hip.hipEventCreate(C.byref(e0))
+        hip.hipEventCreate(C.byref(e1))
         for _ in range(3):
-            y.copy_(x)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(10):
-            y.copy_(x)
-        torch.cuda.synchronize()
-        gbs = 2.0 * 4.0 * n * 10 / (time.perf_counter() - t0) / 1e9
-        del x, y
-        torch.cuda.empty_cache()
-        return gbs
-    except Exception:
-        return None
+            hip.hipMemcpy(b, a, C.c_size_t(n), 3)  # hipMemcpyDeviceToDevice
+        hip.hipDeviceSynchronize()
+        reps = 10
+        hip.hipEventRecord(e0, None)
+        for _ in range(reps):
+            hip.hipMemcpyAsync(b, a, C.c_size_t(n), 3, None)
+        hip.hipEventRecord(e1, None)
+        hip.hipEventSynchronize(e1)
+        ms = C.c_float()
+        hip.hipEventElapsedTime(C.byref(ms), e0, e1)
+        hip.hipFree(a)
+        hip.hipFree(b)
+        return 2.0 * n * reps / (ms.value * 1e-3) / 1e9 if ms.value > 0 else "no timing"
+    except Exception as e:
+        return f"copy probe failed: {type(e).__name__}: {e}"[:200]
 
 
 def cpu_baseline(h, corpus, k, seed, budget_s=12.0):
@@ -176,6 +187,8 @@ def main():
     t0 = time.perf_counter()
     corpus = synth.make_corpus(a.corpus, a.docs, a.tokens, a.vocab, a.k, a.seed + 7919 * rank)
     gen_s = time.perf_counter() - t0
+    log = (lambda msg: print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True))  # progress on stderr
+    log(f"corpus generated in {gen_s:.1f} s")
     dcorp = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F32 if a.dtype == "f32" else stc.STC_F64)
     h = stc.LdaHandle(ctx, a.k, a.vocab, mini_batch_fraction=a.fraction, optimize_doc_concentration=True,
                       seed=a.seed, dtype=a.dtype)
@@ -196,6 +209,7 @@ def main():
             "mean_inner_iters": (cc1["inner_iters"] - cc0["inner_iters"]) / max(1, cc1["docs"] - cc0["docs"]),
             "minibatches": n_cold}
     burn = max(0, a.state_minibatches - n_cold - a.warmup)
+    log("cold minibatches done; burn-in + warmup")
     for _ in range(burn + a.warmup):
         h.next(stats=False)
     ctx.synchronize()
@@ -215,6 +229,7 @@ def main():
             dist.barrier()
 
     barrier()
+    log(f"timing {a.steps} steps")
     t_start = time.perf_counter()
     for _ in range(a.steps):
         h.next(stats=False)
@@ -256,7 +271,7 @@ def main():
     flops = 4.0 * mean_nnz * a.k * per_step_iters
     tflops = flops / (estep_ms * 1e-3) / 1e12
     traffic, traffic_note = pmc_traffic(a)
-    copy_gbs = hbm_copy_gbs(local)
+    copy_gbs = None if a.no_hbm_copy else hbm_copy_gbs(local)
     cpu = None
     if not a.no_cpu_baseline:
         cpu = cpu_baseline(h, corpus, a.k, a.seed)

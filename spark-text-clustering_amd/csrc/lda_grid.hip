@@ -23,15 +23,6 @@ namespace lda {
 
 namespace {
 
-// Experiment (make prio): raise the wave priority over the latency-bound sections of an inner
-// iteration (exchange, r, reduce-scatter, ψ/exp) and drop it over the FMA blocks, so a SIMD's
-// co-resident wave fills the FMA time instead of delaying the critical chain.
-#ifdef STC_GRID_PRIO
-#define GRID_PRIO(p) __builtin_amdgcn_s_setprio(p)
-#else
-#define GRID_PRIO(p)
-#endif
-
 // (waves per document, topics per lane group, max rows per lane, waves per SIMD)
 template <int W_, int KL_, int RMAX_, int OCC_>
 struct GShape {
@@ -204,7 +195,6 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
     const float k_tol = 1e-3f * (float)d.k;
     STAMP(0);
     while (true) {
-      GRID_PRIO(0);
       // Phase A: φ_n = B_n·eθ + ε'_n ; r_n = cts_n / φ_n
       float dot[R];
       {
@@ -228,7 +218,6 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
         }
       }
       STAMP(1);
-      GRID_PRIO(1);
       xchg<S>(sm, it & 1, wave, lane, dot, R, dsum, dummy);  // Σ|Δγ| of the last update rides along
       STAMP(2);
       const bool last = (it > 0 && dsum <= k_tol) || it >= a.max_iter;
@@ -260,7 +249,6 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
       STAMP(4);
 
       // Phase B: s = Bᵀr over the group's KL topics, then reduce-scatter over the 32 row lanes
-      GRID_PRIO(0);
       float flat[KL];
 #pragma unroll
       for (int p = 0; p < H; ++p) {
@@ -271,7 +259,6 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
         flat[2 * p + 1] = x.y;
       }
       STAMP(5);
-      GRID_PRIO(1);
       float ys1[N1];
 #pragma unroll
       for (int q = 0; q < N1; ++q) ys1[q] = (N1 + q < KL) ? flat[N1 + q] : 0.f;
@@ -314,7 +301,6 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
       ++it;
       STAMP(8);
     }
-    GRID_PRIO(0);
     d.gam = gam;
     d.eth = eth;
     d.cs = cs;

@@ -8,6 +8,8 @@
   size-independent properties of the fixed point — Σ_t γ_t = Σα + Σ_n cts_n(1 − ε/φ_n) and
   Σ_{v,t} sstats·expElogβ = Σ_n cts_n(1 − ε/φ_n) — and bitwise run-to-run determinism.
 """
+import zlib
+
 import numpy as np
 import pytest
 
@@ -37,7 +39,7 @@ def test_estep_at_baseline_shapes(ctx, oracle, cfg):
     import stc
     from stc import synth
 
-    rng = np.random.default_rng(hash(cfg["name"]) & 0xFFFF)
+    rng = np.random.default_rng(zlib.crc32(cfg["name"].encode()))  # stable across processes
     V, k, D = cfg["V"], cfg["k"], cfg["D"]
     corpus = synth.zipf_corpus(D, cfg["L"], V, seed=31 + k)
     lam = _tiled_topics(rng, V, k)
@@ -52,9 +54,14 @@ def test_estep_at_baseline_shapes(ctx, oracle, cfg):
         cid, cts = corpus.row(i)
         eeb = _eeb_rows(lam, cid, oracle)
         g, _, it = oracle.variational_topic_inference(np.arange(cid.size), cts, eeb, alpha, g0[i])
-        # fp32 E-step: 2e-3 relative per topic, with an absolute floor of 1e-7·Σγ for the topics
-        # that stay at α + (a sliver): their few ulps of Σγ are relative noise
-        np.testing.assert_allclose(gamma[i], g, rtol=2e-3, atol=1e-7 * g.sum(), err_msg=f"{cfg['name']} doc {i}")
+        # fp32 vs fp64: the fixed point is only defined up to Spark's own stopping rule (mean |Δγ| ≤
+        # 1e-3, i.e. Σ|Δγ| ≤ 1e-3·k per iteration), and the two runs may stop an iteration apart: so
+        # Σ|γ − γ_oracle| within two iterations' worth, and 2e-3 relative on every topic that holds
+        # at least one token's mass
+        l1 = np.abs(gamma[i] - g).sum()
+        assert l1 <= 2e-3 * k, (cfg["name"], i, l1)
+        big = g >= 1.0
+        np.testing.assert_allclose(gamma[i][big], g[big], rtol=2e-3, err_msg=f"{cfg['name']} doc {i}")
         assert abs(int(iters[i]) - it) <= max(2, it // 20), (iters[i], it)
 
 

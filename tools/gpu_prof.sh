@@ -5,7 +5,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof; rm -rf $OUT; mkdir -p $OUT
-B="bench.py --steps 5 --warmup 3 --no-cpu-baseline"
+B="bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-hbm-copy"
 run() {  # run NAME SECONDS ARGS...
   local name=$1 secs=$2; shift 2
   timeout -k 10 "$secs" rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 $B > $OUT/$name.log 2>&1
