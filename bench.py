@@ -89,14 +89,18 @@ def hbm_copy_gbs(device):
     import ctypes as C
 
     try:
-        hip = C.CDLL("libamdhip64.so")
+        hip = C.CDLL("libamdhip64.so.7")  # the runtime libstc.so links (torch/lib carries its own copy)
         ok = (lambda r: r == 0)
         n = 1 << 30
         a, b = C.c_void_p(), C.c_void_p()
         e0, e1 = C.c_void_p(), C.c_void_p()
-        if not (ok(hip.hipSetDevice(int(device))) and ok(hip.hipMalloc(C.byref(a), C.c_size_t(n)))
-                and ok(hip.hipMalloc(C.byref(b), C.c_size_t(n)))):
-            return "hipMalloc failed"
+        hip.hipGetErrorString.restype = C.c_char_p
+        for what, rc in (("hipSetDevice", lambda: hip.hipSetDevice(C.c_int(int(device)))),
+                         ("hipMalloc", lambda: hip.hipMalloc(C.byref(a), C.c_size_t(n))),
+                         ("hipMalloc", lambda: hip.hipMalloc(C.byref(b), C.c_size_t(n)))):
+            r = rc()
+            if not ok(r):
+                return f"{what} failed: {r} {hip.hipGetErrorString(r).decode()}"
         hip.hipMemset(a, 1, C.c_size_t(n))
         hip.hipEventCreate(C.byref(e0))
         hip.hipEventCreate(C.byref(e1))

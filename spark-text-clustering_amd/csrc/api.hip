@@ -48,7 +48,7 @@ struct stc_lda {
   DevBuf lam, Bp, logscale, colsum, colpart, alpha, small, scal;
   DevBuf batch_raw, batch, orig, flags, sincl, bptr, bnnz, nnzp, g0, gamma, eth, elogth, iters,
       nonempty, r, keys, vals, skeys, svals, edoc, stat, headbuf, tailbuf, sort_tmp, scan_tmp,
-      stats4, cum2, bound, dtmp;
+      stats4, cum2, bound, dtmp, lpart;
   DevBuf s_counts, s_weights, s_short, s_cincl, s_wincl, s_sincl;
   int64_t wave_cap = 0;  // docs with nnz <= wave_cap run the wave-per-document E-step
 
@@ -142,6 +142,7 @@ void ensure_batch(stc_lda& L, int64_t n, int64_t E) {
   const int64_t nchunks = ceil_div(E, lda::kChunk) + 1;
   L.headbuf.reserve(ts * nchunks * L.kp);
   L.tailbuf.reserve(ts * nchunks * L.kp);
+  L.lpart.reserve(sizeof(double) * lda::kLogphatBlocks * (L.k + 1));
   size_t tb = 0;
   HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, L.keys.as<uint32_t>(), L.skeys.as<uint32_t>(),
                                                L.vals.as<uint32_t>(), L.svals.as<uint32_t>(),
@@ -278,7 +279,8 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
                           L.headbuf.as<T>(), L.tailbuf.as<T>());
   }
   if (n > 0) {
-    lda::launch_logphat<T>(s, L.elogth.as<T>(), L.nonempty.as<int32_t>(), n, L.k, L.small.as<double>());
+    lda::launch_logphat<T>(s, L.elogth.as<T>(), L.nonempty.as<int32_t>(), n, L.k, L.small.as<double>(),
+                             L.lpart.as<double>());
     lda::launch_iter_stats(s, L.iters.as<int32_t>(), L.nonempty.as<int32_t>(), n, L.cfg.max_inner_iter,
                            L.stats4.as<int64_t>(), L.cum2.as<int64_t>());
   } else {

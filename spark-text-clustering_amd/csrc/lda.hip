@@ -371,6 +371,11 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
                                                 const T* __restrict__ eth, int kp, T* __restrict__ stat,
                                                 T* __restrict__ headbuf, T* __restrict__ tailbuf,
                                                 int64_t nchunks) {
+  // kU entries in flight per wave: their (term, r, doc) are read out of the lanes that loaded them
+  // (v_readlane: wave-uniform, so the eθ' row address is scalar) and their eθ' rows are all requested
+  // before the first is accumulated — the gathers are served by L2 / MALL, and one row at a time
+  // left the wave waiting a full round trip per entry.
+  constexpr int kU = 8;
   const int lane = threadIdx.x & 63;
   const int64_t chunk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (chunk >= nchunks) return;
@@ -397,7 +402,7 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
   };
   for (int64_t pb = p0; pb < p1; pb += 64) {
     const int64_t p = pb + lane;
-    uint32_t kv = 0xFFFFFFFFu;
+    uint32_t kv = cur;
     T rv = T(0);
     int32_t dv = 0;
     if (p < p1) {
@@ -407,19 +412,32 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
       dv = edoc[j];
     }
     const int cnt = (int)((p1 - pb) < 64 ? (p1 - pb) : 64);
-    for (int jj = 0; jj < cnt; ++jj) {
-      const uint32_t v = (uint32_t)__shfl((int)kv, jj, 64);
-      const T rj = __shfl(rv, jj, 64);
-      const int32_t d = __shfl(dv, jj, 64);
-      if (v != cur) {
-        flush(cur);
-        cur = v;
-      }
-      const T* er = eth + (int64_t)d * kp;
+    for (int j0 = 0; j0 < cnt; j0 += kU) {
+      uint32_t vk[kU];
+      T rk[kU];
+      T e[kU][Q];
 #pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const int col = lane + 64 * q;
-        if (col < kp) acc[q] += rj * er[col];
+      for (int u = 0; u < kU; ++u) {  // lanes past cnt hold (cur, 0, doc 0): harmless to add
+        const int jj = j0 + u < 64 ? j0 + u : 63;
+        vk[u] = (uint32_t)__builtin_amdgcn_readlane((int)kv, jj);
+        rk[u] = readlane_t(rv, jj);
+        const T* er = eth + (int64_t)__builtin_amdgcn_readlane(dv, jj) * kp;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const int col = lane + 64 * q;
+          e[u][q] = col < kp ? er[col] : T(0);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (j0 + u < cnt) {
+          if (vk[u] != cur) {
+            flush(cur);
+            cur = vk[u];
+          }
+#pragma unroll
+          for (int q = 0; q < Q; ++q) acc[q] += rk[u] * e[u][q];
+        }
       }
     }
   }
@@ -431,6 +449,10 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
                                                int kp, T* __restrict__ stat,
                                                const T* __restrict__ headbuf,
                                                const T* __restrict__ tailbuf, int64_t nchunks) {
+  // the run's owner (the chunk where it starts) adds the head partials of the chunks the run covers,
+  // in chunk order; kG chunks are fetched at a time (keys and partials), so a run over hundreds of
+  // chunks (the most frequent terms) costs hundreds / kG dependent round trips, not hundreds
+  constexpr int kG = 8;
   const int lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= nchunks) return;
@@ -446,15 +468,32 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
     const int col = lane + 64 * q;
     acc[q] = col < kp ? tailbuf[c * kp + col] : T(0);
   }
-  for (int64_t c2 = c + 1; c2 < nchunks; ++c2) {
+  bool more = true;
+  for (int64_t cb = c + 1; more && cb < nchunks; cb += kG) {
+    bool go[kG];
+    T h[kG][Q];
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int col = lane + 64 * q;
-      if (col < kp) acc[q] += headbuf[c2 * kp + col];
+    for (int g = 0; g < kG; ++g) {  // chunk cb+g continues the run past its end?
+      const int64_t c2 = cb + g < nchunks ? cb + g : nchunks - 1;
+      const int64_t q0 = c2 * kChunk;
+      const int64_t q1 = (q0 + kChunk < E) ? q0 + kChunk : E;
+      go[g] = skeys[q1 - 1] == last && q1 < E && skeys[q1] == last;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int col = lane + 64 * q;
+        h[g][q] = col < kp ? headbuf[c2 * kp + col] : T(0);
+      }
     }
-    const int64_t q0 = c2 * kChunk;
-    const int64_t q1 = (q0 + kChunk < E) ? q0 + kChunk : E;
-    if (!(skeys[q1 - 1] == last && q1 < E && skeys[q1] == last)) break;
+#pragma unroll
+    for (int g = 0; g < kG; ++g) {
+      if (more && cb + g < nchunks) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) acc[q] += h[g][q];
+        more = go[g];
+      } else {
+        more = false;
+      }
+    }
   }
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
@@ -576,8 +615,23 @@ void launch_colsum_reduce(hipStream_t s, const double* colpart, int64_t nblocks,
   KERNEL_CHECK();
 }
 
-// expElogβ'[v][t] = exp(ψ(λ_vt) − ψ(colsum_t) − m_v), m_v = max_t (ψ(λ_vt) − ψ(colsum_t)); one wave
-// per term, each lane's Q topics held in registers so ψ(λ) is evaluated once per element
+// expElogβ'[v][t] = exp(ψ(λ_vt) − ψ(colsum_t) − m_v), m_v ≈ max_t (ψ(λ_vt) − ψ(colsum_t)); one wave
+// per term (grid-stride over terms, so ψ(colsum) is staged once per block for many rows), each
+// lane's Q topics held in registers so ψ(λ) is evaluated once per element (branch-free fp64
+// digamma).  m_v only has to be common to the row and to logscale, not the exact maximum: the
+// fp32 build takes it from an fp32 DPP max, and evaluates the exponential as 2^n · 2^f with the
+// integer/fraction split done in fp64, so the fp32 argument never loses the bits of a large |Elogβ|.
+__device__ __forceinline__ float exp_scaled(double x, float) {
+  const double y = x * 1.4426950408889634;  // log2 e
+  const double n = floor(y);
+  return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f((float)(y - n)), (int)n);
+}
+__device__ __forceinline__ double exp_scaled(double x, double) { return exp(x); }
+__device__ __forceinline__ double row_max(double m, float) {
+  return (double)wave_max_dpp((float)m);
+}
+__device__ __forceinline__ double row_max(double m, double) { return wave_max(m); }
+
 template <typename T, int Q>
 __global__ __launch_bounds__(256) void k_expelogbeta(const double* __restrict__ lam,
                                                      const double* __restrict__ colsum, int64_t V,
@@ -585,34 +639,34 @@ __global__ __launch_bounds__(256) void k_expelogbeta(const double* __restrict__ 
                                                      T* __restrict__ Bp, double* __restrict__ logscale) {
   if (gate && gate[0] == 0.0) return;
   extern __shared__ double s_psic[];
-  for (int t = threadIdx.x; t < k; t += 256) s_psic[t] = digamma_t<double>(colsum[t]);
+  for (int t = threadIdx.x; t < k; t += 256) s_psic[t] = digamma_fast_d(colsum[t]);
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (v >= V) return;
-  const double* lr = lam + v * k;
-  double e[Q];
-  double m = -INFINITY;
+  for (int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); v < V; v += (int64_t)gridDim.x * 4) {
+    const double* lr = lam + v * k;
+    double e[Q];
+    double m = -INFINITY;
 #pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int t = lane + 64 * q;
-    e[q] = t < k ? digamma_t<double>(lr[t]) - s_psic[t] : -INFINITY;
-    m = fmax(m, e[q]);
-  }
-  m = wave_max(m);
-  T* br = Bp + v * kp;
+    for (int q = 0; q < Q; ++q) {
+      const int t = lane + 64 * q;
+      e[q] = t < k ? digamma_fast_d(lr[t]) - s_psic[t] : -INFINITY;
+      m = fmax(m, e[q]);
+    }
+    m = row_max(m, T());
+    T* br = Bp + v * kp;
 #pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int t = lane + 64 * q;
-    if (t < kp) br[t] = t < k ? (T)exp(e[q] - m) : T(0);
+    for (int q = 0; q < Q; ++q) {
+      const int t = lane + 64 * q;
+      if (t < kp) br[t] = t < k ? exp_scaled(e[q] - m, T()) : T(0);
+    }
+    if (lane == 0) logscale[v] = m;
   }
-  if (lane == 0) logscale[v] = m;
 }
 
 template <typename T>
 void launch_expelogbeta(hipStream_t s, const double* lam, const double* colsum, int64_t V, int k,
                         int kp, const double* gate, T* Bp, double* logscale) {
-  const unsigned grid = (unsigned)ceil_div(V, 4);
+  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(V, 4), 2048);  // ≈ 8 terms per wave at V = 2^18
   const size_t sh = sizeof(double) * k;
   const int q = (kp + 63) / 64;
 #define STC_EEB(QQ) k_expelogbeta<T, QQ><<<grid, 256, sh, s>>>(lam, colsum, V, k, kp, gate, Bp, logscale)
@@ -628,29 +682,43 @@ void launch_expelogbeta(hipStream_t s, const double* lam, const double* colsum, 
   KERNEL_CHECK();
 }
 
-// logphat = Σ_docs E[log θ_d] (fixed order) ; small[k] = #non-empty docs
+// logphat = Σ_docs E[log θ_d] (fixed order) ; small[k] = #non-empty docs.  Two passes: kLogphatBlocks
+// blocks each sum a contiguous range of docs with lanes along the (coalesced) topic rows, then one
+// block adds the block partials in block order — the same tree every run.
 template <typename T>
-__global__ __launch_bounds__(256) void k_logphat(const T* __restrict__ elogth,
-                                                 const int32_t* __restrict__ nonempty, int64_t n,
-                                                 int k, double* __restrict__ small) {
+__global__ __launch_bounds__(256) void k_logphat_part(const T* __restrict__ elogth,
+                                                      const int32_t* __restrict__ nonempty, int64_t n,
+                                                      int k, double* __restrict__ part) {
   __shared__ double s[256];
-  const int t = blockIdx.x;  // t == k: count non-empty docs
-  double acc = 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += 256)
-    acc += t < k ? (double)elogth[i * k + t] : (double)nonempty[i];
-  s[threadIdx.x] = acc;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * per, i1 = i0 + per < n ? i0 + per : n;
+  const int col = threadIdx.x & 127, half = threadIdx.x >> 7;
+  for (int c0 = 0; c0 <= k; c0 += 128) {
+    const int t = c0 + col;
+    double acc = 0.0;
+    if (t <= k)
+      for (int64_t i = i0 + half; i < i1; i += 2) acc += t < k ? (double)elogth[i * k + t] : (double)nonempty[i];
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    if (half == 0 && t <= k) part[(int64_t)blockIdx.x * (k + 1) + t] = s[col] + s[128 + col];
     __syncthreads();
   }
-  if (threadIdx.x == 0) small[t] = s[0];
+}
+__global__ __launch_bounds__(256) void k_logphat_final(const double* __restrict__ part, int nb, int k,
+                                                       double* __restrict__ small) {
+  for (int t = threadIdx.x; t <= k; t += 256) {
+    double acc = 0.0;
+    for (int b = 0; b < nb; ++b) acc += part[(int64_t)b * (k + 1) + t];
+    small[t] = acc;
+  }
 }
 
 template <typename T>
 void launch_logphat(hipStream_t s, const T* elogth, const int32_t* nonempty, int64_t n, int k,
-                    double* small) {
-  k_logphat<T><<<k + 1, 256, 0, s>>>(elogth, nonempty, n, k, small);
+                    double* small, double* part) {
+  k_logphat_part<T><<<kLogphatBlocks, 256, 0, s>>>(elogth, nonempty, n, k, part);
+  KERNEL_CHECK();
+  k_logphat_final<<<1, 256, 0, s>>>(part, kLogphatBlocks, k, small);
   KERNEL_CHECK();
 }
 
@@ -766,43 +834,65 @@ void launch_sum_vals(hipStream_t s, const T* x, int64_t n, double* out) {
   KERNEL_CHECK();
 }
 
-__global__ __launch_bounds__(256) void k_iter_stats(const int32_t* __restrict__ iters,
-                                                    const int32_t* __restrict__ nonempty, int64_t n,
-                                                    int max_iter, int64_t* __restrict__ out4,
-                                                    int64_t* __restrict__ cum2) {
-  __shared__ int64_t s[4][256];
-  int64_t sum = 0, mx = 0, cap = 0, ne = 0;
-  for (int64_t i = threadIdx.x; i < n; i += 256) {
-    const int32_t it = iters[i];
-    sum += it;
-    mx = it > mx ? it : mx;
-    cap += (it >= max_iter) ? 1 : 0;
-    ne += nonempty[i];
-  }
-  s[0][threadIdx.x] = sum;
-  s[1][threadIdx.x] = mx;
-  s[2][threadIdx.x] = cap;
-  s[3][threadIdx.x] = ne;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) {
-      s[0][threadIdx.x] += s[0][threadIdx.x + w];
-      s[1][threadIdx.x] = s[1][threadIdx.x] > s[1][threadIdx.x + w] ? s[1][threadIdx.x] : s[1][threadIdx.x + w];
-      s[2][threadIdx.x] += s[2][threadIdx.x + w];
-      s[3][threadIdx.x] += s[3][threadIdx.x + w];
+__global__ __launch_bounds__(1024) void k_iter_stats(const int32_t* __restrict__ iters,
+                                                     const int32_t* __restrict__ nonempty, int64_t n,
+                                                     int max_iter, int64_t* __restrict__ out4,
+                                                     int64_t* __restrict__ cum2) {
+  // one block (the cumulative counters need no atomics); 1024 threads with four loads each in flight
+  __shared__ int64_t s[4][16];
+  int64_t sum = 0, cap = 0, ne = 0;
+  int mx = 0;
+  for (int64_t b = 0; b < n; b += 4 * 1024) {
+    int it[4], nz[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = b + u * 1024 + threadIdx.x;
+      it[u] = i < n ? iters[i] : 0;
+      nz[u] = i < n ? nonempty[i] : 0;
     }
-    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sum += it[u];
+      mx = it[u] > mx ? it[u] : mx;
+      cap += (it[u] >= max_iter) ? 1 : 0;
+      ne += nz[u];
+    }
   }
-  if (threadIdx.x < 4) out4[threadIdx.x] = s[threadIdx.x][0];
-  if (threadIdx.x == 0 && cum2) {  // cumulative Σ iterations, cap hits (single block: no race)
-    cum2[0] += s[0][0];
-    cum2[1] += s[2][0];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sum += __shfl_xor(sum, o, 64);
+    cap += __shfl_xor(cap, o, 64);
+    ne += __shfl_xor(ne, o, 64);
+    const int m2 = __shfl_xor(mx, o, 64);
+    mx = m2 > mx ? m2 : mx;
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s[0][w] = sum;
+    s[1][w] = mx;
+    s[2][w] = cap;
+    s[3][w] = ne;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t r[4] = {0, 0, 0, 0};
+    for (int j = 0; j < 16; ++j) {
+      r[0] += s[0][j];
+      r[1] = s[1][j] > r[1] ? s[1][j] : r[1];
+      r[2] += s[2][j];
+      r[3] += s[3][j];
+    }
+    for (int j = 0; j < 4; ++j) out4[j] = r[j];
+    if (cum2) {  // cumulative Σ iterations, cap hits
+      cum2[0] += r[0];
+      cum2[1] += r[2];
+    }
   }
 }
 
 void launch_iter_stats(hipStream_t s, const int32_t* iters, const int32_t* nonempty, int64_t n,
                        int max_iter, int64_t* out4, int64_t* cum2) {
-  k_iter_stats<<<1, 256, 0, s>>>(iters, nonempty, n, max_iter, out4, cum2);
+  k_iter_stats<<<1, 1024, 0, s>>>(iters, nonempty, n, max_iter, out4, cum2);
   KERNEL_CHECK();
 }
 
@@ -990,7 +1080,7 @@ void launch_unscale_stat(hipStream_t s, const T* stat, const double* logscale, i
                                         double, double, double, const double*, double*, int64_t); \
   template void launch_expelogbeta<T>(hipStream_t, const double*, const double*, int64_t, int, int, \
                                       const double*, T*, double*);                               \
-  template void launch_logphat<T>(hipStream_t, const T*, const int32_t*, int64_t, int, double*);  \
+  template void launch_logphat<T>(hipStream_t, const T*, const int32_t*, int64_t, int, double*, double*);  \
   template void launch_topics_bound<T>(hipStream_t, const double*, const double*, int64_t, int,   \
                                        double, double*, int64_t);                                 \
   template void launch_sum_vals<T>(hipStream_t, const T*, int64_t, double*);                      \

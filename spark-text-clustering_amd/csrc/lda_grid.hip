@@ -55,8 +55,12 @@ __device__ __forceinline__ void xchg(GLds<S>& sm, int b, int wave, int lane, flo
                                      float& y) {
   constexpr int W = S::W;
   if constexpr (W > 1) {
+    // addresses from one lane-dependent base (hoisted by the compiler) plus wave-uniform offsets
+    float* const base = &sm.phi[0][0][0][0] + lane;
+    constexpr int BS = S::W * S::RMAX * 64, WS = S::RMAX * 64;
+    float* const mine = base + (b * BS + wave * WS);
 #pragma unroll
-    for (int j = 0; j < nd; ++j) sm.phi[b][wave][j][lane] = dot[j];
+    for (int j = 0; j < nd; ++j) mine[64 * j] = dot[j];
     if (lane == 0) {
       sm.red[b][wave][0] = x;
       sm.red[b][wave][1] = y;
@@ -64,8 +68,9 @@ __device__ __forceinline__ void xchg(GLds<S>& sm, int b, int wave, int lane, flo
     __syncthreads();
     if constexpr (W == 2) {
       const int o = wave ^ 1;
+      const float* const other = base + (b * BS + o * WS);
 #pragma unroll
-      for (int j = 0; j < nd; ++j) dot[j] += sm.phi[b][o][j][lane];
+      for (int j = 0; j < nd; ++j) dot[j] += other[64 * j];
       x += sm.red[b][o][0];
       y += sm.red[b][o][1];
     } else {
@@ -97,6 +102,9 @@ struct GDoc {
   int64_t slot, row, mem, s0, e0;
   float gam, alp, eth, cs, gsum, asum;
   double b_tok, c_tok;
+#ifdef STC_STAMP
+  unsigned long long st0;  // kernel entry (stamp build): the preamble's cycles go to stamp slot 11
+#endif
 };
 
 template <class S, int R, bool STATS, bool BOUND>
@@ -105,6 +113,9 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
   constexpr int N1 = hup(KL), N2 = hup(N1), N3 = hup(N2), N4 = hup(N3), N5 = hup(N4);
   static_assert(KL % 2 == 0 && N5 == 1 && R >= 1 && R <= S::RMAX, "shape");
   STAMP_DECL
+#ifdef STC_STAMP
+  st_acc[11] += st_last - d.st0;
+#endif
   const int lane = d.lane, wave = d.wave, rl = d.rl, nnz = d.nnz, kp = d.kp;
   const int64_t s0 = d.s0, e0 = d.e0;
   float* const my_eth = sm.eth[d.wave][d.g];
@@ -168,9 +179,12 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
     }
     __builtin_amdgcn_wave_barrier();
   }
+  STAMP(10);
+  // ε'_n = max(1e-100 / e^{m_n}, FLT_MIN), held as 2^24·ε'_n (φ = dot + 2^-24·that is exact): the
+  // ballot below asks 2^24·ε' ≥ φ directly.  Padding rows hold −2^24 (φ = −1, r = −0, never live).
 #pragma unroll
-  for (int j = 0; j < R; ++j)  // ε'_n = max(1e-100 / e^{m_n}, FLT_MIN)
-    eps[j] = (32 * j + rl < nnz) ? max_nonneg(__expf((float)(kLogEps - ls[j])), kTiny) : 1.f;
+  for (int j = 0; j < R; ++j)
+    eps[j] = (32 * j + rl < nnz) ? 16777216.f * max_nonneg(__expf((float)(kLogEps - ls[j])), kTiny) : -16777216.f;
   bool nonempty;
   if constexpr (W > 1) nonempty = __syncthreads_or(any) != 0;
   else nonempty = __any(any);
@@ -220,13 +234,17 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
       STAMP(1);
       xchg<S>(sm, it & 1, wave, lane, dot, R, dsum, dummy);  // Σ|Δγ| of the last update rides along
       STAMP(2);
-      const bool last = (it > 0 && dsum <= k_tol) || it >= a.max_iter;
-      int eps_live = 0;
+      // wave-uniform by construction (dsum is the same in every lane); readfirstlane tells the compiler,
+      // so the loop is a scalar loop: no exec-mask bookkeeping, the counter and offsets in SGPRs
+      const bool last =
+          __builtin_amdgcn_readfirstlane((int)((it > 0 && dsum <= k_tol) || it >= a.max_iter)) != 0;
+      uint64_t eps_live = 0;
 #pragma unroll
       for (int j = 0; j < R; ++j) {
-        const float ph = dot[j] + eps[j];
+        const float ph = fmaf(eps[j], 0x1p-24f, dot[j]);
         rr[j] = cts[j] * __builtin_amdgcn_rcpf(ph);
-        eps_live |= (cts[j] != 0.f) & (eps[j] * 16777216.f >= ph);  // ε' ≥ 2^-24·φ: visible in Σγ'
+        // ε' ≥ 2^-24·φ: visible in Σγ' (a row with cts = 0 only costs time)
+        eps_live |= __builtin_amdgcn_ballot_w64(eps[j] >= ph);
         if (BOUND && last && d.g == 0 && cts[j] != 0.f) {
           d.b_tok += (double)cts[j] * ((double)__logf(fmaxf(dot[j], kTiny)) + a.logscale[ids[j]]);
           d.c_tok += (double)cts[j];
@@ -239,11 +257,11 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
       // ε'_n ≥ 2^-24·φ_n (a ballot); only then is it reduced.  The decision and the sums are the same
       // in every wave (like φ and r), so every wave scales its eθ slice identically.
       float cs_next = cs_flat;
-      if (__any(eps_live)) {
+      if (eps_live) {
         float e = 0.f;
 #pragma unroll
         for (int j = 0; j < R; ++j)  // cts·ε'/φ as cts·(1 − dot/φ): 0 for padding, cts when ε' = ∞
-          e = fmaf(cts[j], 1.f - dot[j] * __builtin_amdgcn_rcpf(dot[j] + eps[j]), e);
+          e = fmaf(cts[j], 1.f - dot[j] * __builtin_amdgcn_rcpf(fmaf(eps[j], 0x1p-24f, dot[j])), e);
         cs_next = digamma_fast(asum + ctot - 0.5f * wave_sum_dpp(e));  // each row is held twice
       }
       STAMP(4);
@@ -333,6 +351,9 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_grid(EStepArgs<floa
   __shared__ GLds<S> sm;
   if ((int64_t)blockIdx.x >= a.n) return;
   GDoc d;
+#ifdef STC_STAMP
+  d.st0 = stamp_now();
+#endif
   d.lane = threadIdx.x & 63;
   d.wave = threadIdx.x >> 6;
   d.g = (d.lane >> 3) & 1;

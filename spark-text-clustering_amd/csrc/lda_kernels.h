@@ -92,7 +92,8 @@ void launch_expelogbeta(hipStream_t s, const double* lam, const double* colsum, 
                         int kp, const double* gate, T* Bp, double* logscale);
 template <typename T>
 void launch_logphat(hipStream_t s, const T* elogth, const int32_t* nonempty, int64_t n, int k,
-                    double* small /* k+1 */);
+                    double* small /* k+1 */, double* part /* kLogphatBlocks × (k+1) scratch */);
+constexpr int kLogphatBlocks = 128;
 void launch_update_alpha(hipStream_t s, double* alpha, const double* small, int k, double rho);
 void launch_init_lambda(hipStream_t s, double* lam, int64_t V, int k, uint64_t seed, double shape);
 template <typename T>

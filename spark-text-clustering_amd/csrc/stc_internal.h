@@ -188,6 +188,31 @@ __device__ inline float digamma_fast(float x) {
   return ln_pos(y) - 0.5f * iy + t - r;
 }
 
+// fp64 1/q from v_rcp_f64 and two Newton steps (≤ 1 ulp apart from the correctly rounded quotient)
+__device__ __forceinline__ double rcp_nr(double q) {
+  double r = __builtin_amdgcn_rcp(q);
+  r = fma(r, fma(-q, r, 1.0), r);
+  return fma(r, fma(-q, r, 1.0), r);
+}
+// fp64 digamma for the M-step's V×k elements, branch-free: Breeze's recurrence Σ_{i<6} 1/(x+i) for
+// x ≤ 5 as one rational Q'(x)/Q(x), Q = x(x+1)…(x+5), and the same 8-term asymptotic series at
+// y = x + 6 (or y = x when x > 5, where Breeze does not shift).  Agrees with digamma_t<double> to a
+// few ulp; the loop form costs a divergent chain of up to six fp64 divisions per element.
+__device__ inline double digamma_fast_d(double x) {
+  const bool sh = x <= 5.0;
+  const double q = ((((((x + 15.0) * x + 85.0) * x + 225.0) * x + 274.0) * x + 120.0) * x);
+  const double p = (((((6.0 * x + 75.0) * x + 340.0) * x + 675.0) * x + 548.0) * x + 120.0);
+  const double iq = rcp_nr(sh ? q : 1.0);
+  double c = p * iq;
+  c = fma(fma(-q, c, p), iq, c);  // one residual correction of p/q
+  const double y = sh ? x + 6.0 : x;
+  const double iy = rcp_nr(y);
+  const double f = iy * iy;
+  const double t = f * (-1.0 / 12.0 + f * (1.0 / 120.0 + f * (-1.0 / 252.0 + f * (1.0 / 240.0 +
+                   f * (-1.0 / 132.0 + f * (691.0 / 32760.0 + f * (-1.0 / 12.0 + f * 3617.0 / 8160.0)))))));
+  return (sh ? -c : 0.0) + log(y) - 0.5 * iy + t;
+}
+
 __host__ __device__ inline double trigamma_d(double x) {
   double r = 0;
   while (x <= 5.0) {
@@ -209,6 +234,16 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
   // all-lanes-valid permutations only (mirrors, quad_perm): bound_ctrl never fires, no `old` operand
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// v_readlane of a float / double (wave-uniform lane index)
+__device__ __forceinline__ float readlane_t(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ double readlane_t(double v, int l) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 // max of two non-negative floats as an unsigned compare of their bits (no NaN canonicalisation)
 __device__ __forceinline__ float max_nonneg(float a, float b) {

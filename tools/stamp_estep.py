@@ -18,9 +18,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "spark-text-clustering_amd"))
 
-PHASES = ["load+init", "A: eth reads + phi FMAs", "phi exchange (LDS+barrier)", "r, sum r*dot",
+PHASES = ["eps, partner barrier, init", "A: eth reads + phi FMAs", "phi exchange (LDS+barrier)", "r, sum r*dot",
           "psi(sum gamma')", "B: s FMAs", "reduce-scatter", "C: gamma, sum|dgamma|", "D: psi/exp, eth->LDS",
-          "outputs", "-", "-"]
+          "outputs", "loads: ids + staged B rows", "preamble: indptr, gamma0 sampling"]
 
 
 def main():
