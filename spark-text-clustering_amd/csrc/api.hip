@@ -47,7 +47,7 @@ struct stc_lda {
 
   DevBuf lam, Bp, logscale, colsum, colpart, alpha, small, scal;
   DevBuf batch_raw, batch, orig, flags, sincl, bptr, bnnz, nnzp, g0, gamma, eth, elogth, iters,
-      nonempty, r, keys, vals, skeys, svals, edoc, stat, headbuf, tailbuf, sort_tmp, scan_tmp,
+      nonempty, r, keys, vals, skeys, svals, stat, headbuf, tailbuf, sort_tmp, scan_tmp,
       stats4, cum2, bound, dtmp, lpart;
   DevBuf s_counts, s_weights, s_short, s_cincl, s_wincl, s_sincl;
   int64_t wave_cap = 0;  // docs with nnz <= wave_cap run the wave-per-document E-step
@@ -60,10 +60,14 @@ struct stc_lda {
   int64_t timed_steps = 0;
   int64_t cum_docs = 0, cum_entries = 0;
 
+  int64_t* hcnt = nullptr;  // pinned host words for the per-step count readback (one small copy)
+  DevBuf dcnt;
+
   ~stc_lda() {
     for (auto& s : ev)
       for (auto& e : s)
         if (e) (void)hipEventDestroy(e);
+    if (hcnt) (void)hipHostFree(hcnt);
   }
 };
 
@@ -135,17 +139,16 @@ void ensure_batch(stc_lda& L, int64_t n, int64_t E) {
   L.nonempty.reserve(4 * n);
   L.r.reserve(ts * E);
   L.keys.reserve(4 * E);
-  L.vals.reserve(4 * E);
+  L.vals.reserve(8 * E);
   L.skeys.reserve(4 * E);
-  L.svals.reserve(4 * E);
-  L.edoc.reserve(4 * E);
+  L.svals.reserve(8 * E);
   const int64_t nchunks = ceil_div(E, lda::kChunk) + 1;
   L.headbuf.reserve(ts * nchunks * L.kp);
   L.tailbuf.reserve(ts * nchunks * L.kp);
   L.lpart.reserve(sizeof(double) * lda::kLogphatBlocks * (L.k + 1));
   size_t tb = 0;
   HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, L.keys.as<uint32_t>(), L.skeys.as<uint32_t>(),
-                                               L.vals.as<uint32_t>(), L.svals.as<uint32_t>(),
+                                               L.vals.as<uint64_t>(), L.svals.as<uint64_t>(),
                                                (int)std::max<int64_t>(E, 1), 0, bits_for(L.V),
                                                L.ctx->stream));
   L.sort_tmp.reserve(tb);
@@ -261,8 +264,7 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   a.elogth = L.elogth.as<T>();
   a.r = L.r.as<T>();
   a.keys = L.keys.as<uint32_t>();
-  a.vals = L.vals.as<uint32_t>();
-  a.edoc = L.edoc.as<int32_t>();
+  a.vals = L.vals.as<uint64_t>();
   a.iters = L.iters.as<int32_t>();
   a.nonempty = L.nonempty.as<int32_t>();
   record(L, 1);
@@ -272,10 +274,10 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   if (E > 0) {
     size_t tb = L.sort_tmp.bytes;
     HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(L.sort_tmp.p, tb, L.keys.as<uint32_t>(),
-                                                 L.skeys.as<uint32_t>(), L.vals.as<uint32_t>(),
-                                                 L.svals.as<uint32_t>(), (int)E, 0, bits_for(L.V), s));
-    lda::launch_sstats<T>(s, L.skeys.as<uint32_t>(), L.svals.as<uint32_t>(), E, L.r.as<T>(),
-                          L.edoc.as<int32_t>(), L.eth.as<T>(), L.kp, L.stat.as<T>(),
+                                                 L.skeys.as<uint32_t>(), L.vals.as<uint64_t>(),
+                                                 L.svals.as<uint64_t>(), (int)E, 0, bits_for(L.V), s));
+    lda::launch_sstats<T>(s, L.skeys.as<uint32_t>(), L.svals.as<uint64_t>(), E, L.r.as<T>(),
+                          L.eth.as<T>(), L.kp, L.stat.as<T>(),
                           L.headbuf.as<T>(), L.tailbuf.as<T>());
   }
   if (n > 0) {
@@ -389,12 +391,15 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
   incl_scan<int32_t>(L, L.s_counts.as<int32_t>(), L.s_cincl.as<int32_t>(), D);
   incl_scan<int64_t>(L, L.s_weights.as<int64_t>(), L.s_wincl.as<int64_t>(), D);
   incl_scan<int32_t>(L, L.s_short.as<int32_t>(), L.s_sincl.as<int32_t>(), D);
-  int32_t n32 = 0, ns32 = 0;
-  int64_t E = 0;
-  HIP_CHECK(hipMemcpyAsync(&n32, L.s_cincl.as<int32_t>() + (D - 1), 4, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipMemcpyAsync(&E, L.s_wincl.as<int64_t>() + (D - 1), 8, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipMemcpyAsync(&ns32, L.s_sincl.as<int32_t>() + (D - 1), 4, hipMemcpyDeviceToHost, s));
+  // (n, E, n_short) from the scans' last elements: one kernel packs them, one copy into pinned
+  // memory (three pageable copies cost ≈ 90 µs of idle GPU per step), one sync
+  if (!L.hcnt) HIP_CHECK(hipHostMalloc((void**)&L.hcnt, 4 * sizeof(int64_t), hipHostMallocDefault));
+  L.dcnt.reserve(4 * sizeof(int64_t));
+  lda::launch_last3(s, L.s_cincl.as<int32_t>() + (D - 1), L.s_wincl.as<int64_t>() + (D - 1),
+                    L.s_sincl.as<int32_t>() + (D - 1), L.dcnt.as<int64_t>());
+  HIP_CHECK(hipMemcpyAsync(L.hcnt, L.dcnt.p, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
+  const int64_t n32 = L.hcnt[0], E = L.hcnt[1], ns32 = L.hcnt[2];
   if (L.timing) harvest(L, L.ev_set ^ 1);  // the previous step's events have completed
   const int64_t n = n32;
   // Spark's next(): `if (batch.isEmpty()) return this` — no iteration increment

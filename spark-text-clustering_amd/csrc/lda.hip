@@ -160,8 +160,7 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
       a.r[e0 + n] = T(0);
       if (STATS) {
         a.keys[e0 + n] = (uint32_t)a.indices[s0 + n];
-        a.vals[e0 + n] = (uint32_t)(e0 + n);
-        a.edoc[e0 + n] = (int32_t)slot;
+        a.vals[e0 + n] = entry_val<T>(slot, e0 + n, T(0));
       }
     }
     if (tid == 0) {
@@ -281,10 +280,10 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
   if (STATS) {
     for (int t = tid; t < kp; t += kBlock) a.eth[slot * kp + t] = s_eth[t];
     for (int n = tid; n < nnz; n += kBlock) {
-      if (LDS) a.r[e0 + n] = s_r[n];
+      const T rv = LDS ? s_r[n] : a.r[e0 + n];  // the L2 path wrote r before the block barrier
+      if (LDS) a.r[e0 + n] = rv;
       a.keys[e0 + n] = (uint32_t)ids[n];
-      a.vals[e0 + n] = (uint32_t)(e0 + n);
-      a.edoc[e0 + n] = (int32_t)slot;
+      a.vals[e0 + n] = entry_val<T>(slot, e0 + n, rv);
     }
   }
   if (tid == 0) {
@@ -366,8 +365,8 @@ void launch_estep(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound) 
 // ---------------------------------------------------------------------------------------
 template <typename T, int Q>
 __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ skeys,
-                                                const uint32_t* __restrict__ svals, int64_t E,
-                                                const T* __restrict__ r, const int32_t* __restrict__ edoc,
+                                                const uint64_t* __restrict__ svals, int64_t E,
+                                                const T* __restrict__ r,
                                                 const T* __restrict__ eth, int kp, T* __restrict__ stat,
                                                 T* __restrict__ headbuf, T* __restrict__ tailbuf,
                                                 int64_t nchunks) {
@@ -405,11 +404,12 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
     uint32_t kv = cur;
     T rv = T(0);
     int32_t dv = 0;
-    if (p < p1) {
+    if (p < p1) {  // (slot, r) travel with the sorted keys (entry_val); fp64 gathers r[e]
       kv = skeys[p];
-      const uint32_t j = svals[p];
-      rv = r[j];
-      dv = edoc[j];
+      const uint64_t pv = svals[p];
+      dv = (int32_t)(pv >> 32);
+      if constexpr (sizeof(T) == 4) rv = __builtin_bit_cast(T, (uint32_t)pv);
+      else rv = r[(uint32_t)pv];
     }
     const int cnt = (int)((p1 - pb) < 64 ? (p1 - pb) : 64);
     for (int j0 = 0; j0 < cnt; j0 += kU) {
@@ -452,7 +452,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
   // the run's owner (the chunk where it starts) adds the head partials of the chunks the run covers,
   // in chunk order; kG chunks are fetched at a time (keys and partials), so a run over hundreds of
   // chunks (the most frequent terms) costs hundreds / kG dependent round trips, not hundreds
-  constexpr int kG = 8;
+  constexpr int kG = 32;
   const int lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= nchunks) return;
@@ -503,30 +503,28 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
 }
 
 template <typename T, int Q>
-static void sstats_q(hipStream_t s, const uint32_t* skeys, const uint32_t* svals, int64_t E,
-                     const T* r, const int32_t* edoc, const T* eth, int kp, T* stat, T* headbuf,
-                     T* tailbuf) {
+static void sstats_q(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, int64_t E,
+                     const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf) {
   const int64_t nchunks = ceil_div(E, kChunk);
   const dim3 grid((unsigned)ceil_div(nchunks, 4));
-  k_sstats<T, Q><<<grid, 256, 0, s>>>(skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf, nchunks);
+  k_sstats<T, Q><<<grid, 256, 0, s>>>(skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, nchunks);
   KERNEL_CHECK();
   k_fixup<T, Q><<<grid, 256, 0, s>>>(skeys, E, kp, stat, headbuf, tailbuf, nchunks);
   KERNEL_CHECK();
 }
 
 template <typename T>
-void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint32_t* svals, int64_t E,
-                   const T* r, const int32_t* edoc, const T* eth, int kp, T* stat, T* headbuf,
-                   T* tailbuf) {
+void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, int64_t E,
+                   const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf) {
   if (E == 0) return;
   const int q = (kp + 63) / 64;
-  if (q <= 1) sstats_q<T, 1>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 2) sstats_q<T, 2>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 4) sstats_q<T, 4>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 8) sstats_q<T, 8>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 16) sstats_q<T, 16>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 32) sstats_q<T, 32>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 64) sstats_q<T, 64>(s, skeys, svals, E, r, edoc, eth, kp, stat, headbuf, tailbuf);
+  if (q <= 1) sstats_q<T, 1>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
+  else if (q <= 2) sstats_q<T, 2>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
+  else if (q <= 4) sstats_q<T, 4>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
+  else if (q <= 8) sstats_q<T, 8>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
+  else if (q <= 16) sstats_q<T, 16>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
+  else if (q <= 32) sstats_q<T, 32>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
+  else if (q <= 64) sstats_q<T, 64>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
   else throw Error(STC_ERR_INVALID_ARG, "k > 4096 topics is not supported");
 }
 
@@ -642,14 +640,28 @@ __global__ __launch_bounds__(256) void k_expelogbeta(const double* __restrict__ 
   for (int t = threadIdx.x; t < k; t += 256) s_psic[t] = digamma_fast_d(colsum[t]);
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  for (int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); v < V; v += (int64_t)gridDim.x * 4) {
-    const double* lr = lam + v * k;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  double nx[Q];  // the next row's λ, requested before this row's ψ work (hides the load latency)
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int t = lane + 64 * q;
+    nx[q] = (v < V && t < k) ? lam[v * k + t] : 1.0;
+  }
+  for (; v < V; v += stride) {
+    double lv[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int t = lane + 64 * q;
+      lv[q] = nx[q];
+      nx[q] = (v + stride < V && t < k) ? lam[(v + stride) * k + t] : 1.0;
+    }
     double e[Q];
     double m = -INFINITY;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int t = lane + 64 * q;
-      e[q] = t < k ? digamma_fast_d(lr[t]) - s_psic[t] : -INFINITY;
+      e[q] = t < k ? digamma_fast_d(lv[q]) - s_psic[t] : -INFINITY;
       m = fmax(m, e[q]);
     }
     m = row_max(m, T());
@@ -689,28 +701,36 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_logphat_part(const T* __restrict__ elogth,
                                                       const int32_t* __restrict__ nonempty, int64_t n,
                                                       int k, double* __restrict__ part) {
-  __shared__ double s[256];
+  // block b sums docs [b·per, (b+1)·per) for column t = threadIdx.x (+256·c): four independent loads
+  // in flight per thread, the rows of a step contiguous across the block's threads
   const int64_t per = (n + gridDim.x - 1) / gridDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * per, i1 = i0 + per < n ? i0 + per : n;
-  const int col = threadIdx.x & 127, half = threadIdx.x >> 7;
-  for (int c0 = 0; c0 <= k; c0 += 128) {
-    const int t = c0 + col;
-    double acc = 0.0;
-    if (t <= k)
-      for (int64_t i = i0 + half; i < i1; i += 2) acc += t < k ? (double)elogth[i * k + t] : (double)nonempty[i];
-    s[threadIdx.x] = acc;
-    __syncthreads();
-    if (half == 0 && t <= k) part[(int64_t)blockIdx.x * (k + 1) + t] = s[col] + s[128 + col];
-    __syncthreads();
+  for (int t = threadIdx.x; t <= k; t += 256) {
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int64_t i = i0; i < i1; i += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t iu = i + u;
+        if (iu < i1) acc[u] += t < k ? (double)elogth[iu * k + t] : (double)nonempty[iu];
+      }
+    }
+    part[(int64_t)blockIdx.x * (k + 1) + t] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   }
 }
+// column t's kLogphatBlocks partials: 256 threads × (kLogphatBlocks / 256) loads, then a fixed tree
 __global__ __launch_bounds__(256) void k_logphat_final(const double* __restrict__ part, int nb, int k,
                                                        double* __restrict__ small) {
-  for (int t = threadIdx.x; t <= k; t += 256) {
-    double acc = 0.0;
-    for (int b = 0; b < nb; ++b) acc += part[(int64_t)b * (k + 1) + t];
-    small[t] = acc;
+  __shared__ double s[256];
+  const int t = blockIdx.x;
+  double acc = 0.0;
+  for (int b = threadIdx.x; b < nb; b += 256) acc += part[(int64_t)b * (k + 1) + t];
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+    __syncthreads();
   }
+  if (threadIdx.x == 0) small[t] = s[0];
 }
 
 template <typename T>
@@ -718,7 +738,7 @@ void launch_logphat(hipStream_t s, const T* elogth, const int32_t* nonempty, int
                     double* small, double* part) {
   k_logphat_part<T><<<kLogphatBlocks, 256, 0, s>>>(elogth, nonempty, n, k, part);
   KERNEL_CHECK();
-  k_logphat_final<<<1, 256, 0, s>>>(part, kLogphatBlocks, k, small);
+  k_logphat_final<<<k + 1, 256, 0, s>>>(part, kLogphatBlocks, k, small);
   KERNEL_CHECK();
 }
 
@@ -834,24 +854,36 @@ void launch_sum_vals(hipStream_t s, const T* x, int64_t n, double* out) {
   KERNEL_CHECK();
 }
 
+__global__ void k_last3(const int32_t* a, const int64_t* b, const int32_t* c, int64_t* out) {
+  if (threadIdx.x == 0) {
+    out[0] = *a;
+    out[1] = *b;
+    out[2] = *c;
+  }
+}
+void launch_last3(hipStream_t s, const int32_t* a, const int64_t* b, const int32_t* c, int64_t* out) {
+  k_last3<<<1, 64, 0, s>>>(a, b, c, out);
+  KERNEL_CHECK();
+}
+
 __global__ __launch_bounds__(1024) void k_iter_stats(const int32_t* __restrict__ iters,
                                                      const int32_t* __restrict__ nonempty, int64_t n,
                                                      int max_iter, int64_t* __restrict__ out4,
                                                      int64_t* __restrict__ cum2) {
-  // one block (the cumulative counters need no atomics); 1024 threads with four loads each in flight
+  // one block (the cumulative counters need no atomics); 1024 threads with 16 loads each in flight
   __shared__ int64_t s[4][16];
   int64_t sum = 0, cap = 0, ne = 0;
   int mx = 0;
-  for (int64_t b = 0; b < n; b += 4 * 1024) {
-    int it[4], nz[4];
+  for (int64_t b = 0; b < n; b += 16 * 1024) {
+    int it[16], nz[16];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const int64_t i = b + u * 1024 + threadIdx.x;
       it[u] = i < n ? iters[i] : 0;
       nz[u] = i < n ? nonempty[i] : 0;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 16; ++u) {
       sum += it[u];
       mx = it[u] > mx ? it[u] : mx;
       cap += (it[u] >= max_iter) ? 1 : 0;
@@ -1074,8 +1106,8 @@ void launch_unscale_stat(hipStream_t s, const T* stat, const double* logscale, i
   template size_t estep_lds_bytes<T>(int, int, int);                                              \
   template int estep_lds_rows<T>(int, int, int);                                                  \
   template void launch_estep<T>(hipStream_t, const EStepArgs<T>&, bool, bool);                    \
-  template void launch_sstats<T>(hipStream_t, const uint32_t*, const uint32_t*, int64_t, const T*, \
-                                 const int32_t*, const T*, int, T*, T*, T*);                      \
+  template void launch_sstats<T>(hipStream_t, const uint32_t*, const uint64_t*, int64_t, const T*, \
+                                 const T*, int, T*, T*, T*);                                      \
   template void launch_lambda_update<T>(hipStream_t, double*, const T*, const T*, int64_t, int, int, \
                                         double, double, double, const double*, double*, int64_t); \
   template void launch_expelogbeta<T>(hipStream_t, const double*, const double*, int64_t, int, int, \

@@ -207,6 +207,7 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
     __builtin_amdgcn_wave_barrier();  // the slices are read back only by this wave
     int it = 0;
     const float k_tol = 1e-3f * (float)d.k;
+    float dg = 0.f;  // |Δγ| of the owned topic in the last update
     STAMP(0);
     while (true) {
       // Phase A: φ_n = B_n·eθ + ε'_n ; r_n = cts_n / φ_n
@@ -231,6 +232,9 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
           dot[j] = x + dpp_f<DPP_ROW_ROR8>(x);  // + the other topic group (i ↔ i^8): commutative
         }
       }
+      // Σ|Δγ| of the last update, reduced here rather than at the end of that update: the DPP chain
+      // shares a basic block with Phase A's LDS reads and FMAs, which hide its latency
+      dsum = wave_sum_dpp(dg);
       STAMP(1);
       xchg<S>(sm, it & 1, wave, lane, dot, R, dsum, dummy);  // Σ|Δγ| of the last update rides along
       STAMP(2);
@@ -300,21 +304,18 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
       const float s_own = rs_dpp<DPP_QP_1032>(p4[0], y5, lane & 1);
       STAMP(6);
 
-      // Phase C: γ ← eθ ⊙ s + α on the owned topic; Σ|Δγ| of the wave
-      float dg = 0.f;
-      if (d.own) {
+      // Phase C: γ ← eθ ⊙ s + α on the owned topic (lanes without one keep γ = 0 and dg = 0)
+      {
         const float gn = fmaf(eth, s_own, alp);
-        dg = fabsf(gn - gam);
-        gam = gn;
+        dg = d.own ? fabsf(gn - gam) : 0.f;
+        gam = d.own ? gn : gam;
       }
-      dsum = wave_sum_dpp(dg);
       STAMP(7);
-      // Phase D: eθ = exp(ψ(γ) − ψ(Σγ)) into the group's LDS slice
+      // Phase D: eθ = exp(ψ(γ) − ψ(Σγ)) into the group's LDS slice; computed in every lane (no
+      // exec-mask region), stored by the owners
       cs = cs_next;
-      if (d.own) {
-        eth = __expf(digamma_fast(gam) - cs);
-        my_eth[d.tl] = eth;
-      }
+      eth = d.own ? __expf(digamma_fast(d.own ? gam : 1.f) - cs) : 0.f;
+      if (d.own) my_eth[d.tl] = eth;
       __builtin_amdgcn_wave_barrier();
       ++it;
       STAMP(8);
@@ -333,8 +334,7 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
         a.r[e0 + n] = rr[j];
         if (STATS) {
           a.keys[e0 + n] = (uint32_t)ids[j];
-          a.vals[e0 + n] = (uint32_t)(e0 + n);
-          a.edoc[e0 + n] = (int32_t)d.slot;
+          a.vals[e0 + n] = entry_val<float>(d.slot, e0 + n, rr[j]);
         }
       }
     }

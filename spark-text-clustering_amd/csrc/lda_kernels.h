@@ -11,6 +11,17 @@ constexpr int kLdsBudget = 80 * 1024; // dynamic LDS per E-step workgroup → 2 
 constexpr int kChunk = 256;           // sorted entries per wave in the sstats segmented SpMM
 constexpr int kRowsPerBlock = 64;     // terms per workgroup in the λ update
 
+// An entry's sort value for the term-sorted sstats SpMM: its member slot in the high word and, in
+// the low word, r itself for fp32 (so the SpMM reads (slot, r) with the sorted keys instead of
+// gathering them per entry) or the entry index for fp64 (r is gathered from r[e]).
+template <typename T>
+__device__ __forceinline__ uint64_t entry_val(int64_t slot, int64_t e, T r) {
+  if constexpr (sizeof(T) == 4)
+    return ((uint64_t)(uint32_t)slot << 32) | __builtin_bit_cast(uint32_t, r);
+  else
+    return ((uint64_t)(uint32_t)slot << 32) | (uint32_t)e;
+}
+
 // Everything the E-step kernel reads/writes.  T = the E-step arithmetic type (float/double).
 template <typename T>
 struct EStepArgs {
@@ -44,8 +55,7 @@ struct EStepArgs {
   T* elogth = nullptr;                 // n×k  E[log θ] (STATS: logphat)
   T* r = nullptr;                      // entry slots: cts/φ' (always)
   uint32_t* keys = nullptr;            // entry slots: term id (STATS)
-  uint32_t* vals = nullptr;            // entry slots: slot index (STATS)
-  int32_t* edoc = nullptr;             // entry slots: member index (STATS)
+  uint64_t* vals = nullptr;            // entry slots: entry_val(slot, entry, r) (STATS)
   int32_t* iters = nullptr;            // n (optional)
   int32_t* nonempty = nullptr;         // n (optional)
   double* bound = nullptr;             // n (BOUND)
@@ -75,9 +85,8 @@ void launch_part_scatter(hipStream_t s, const int32_t* batch, const int64_t* nnz
                          int32_t* orig_p, int64_t* nnz_p);
 
 template <typename T>
-void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint32_t* svals, int64_t E,
-                   const T* r, const int32_t* edoc, const T* eth, int kp, T* stat, T* headbuf,
-                   T* tailbuf);
+void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, int64_t E,
+                   const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf);
 
 template <typename T>
 void launch_lambda_update(hipStream_t s, double* lam, const T* stat, const T* Bp, int64_t V, int k,
@@ -93,7 +102,7 @@ void launch_expelogbeta(hipStream_t s, const double* lam, const double* colsum, 
 template <typename T>
 void launch_logphat(hipStream_t s, const T* elogth, const int32_t* nonempty, int64_t n, int k,
                     double* small /* k+1 */, double* part /* kLogphatBlocks × (k+1) scratch */);
-constexpr int kLogphatBlocks = 128;
+constexpr int kLogphatBlocks = 2048;
 void launch_update_alpha(hipStream_t s, double* alpha, const double* small, int k, double rho);
 void launch_init_lambda(hipStream_t s, double* lam, int64_t V, int k, uint64_t seed, double shape);
 template <typename T>
@@ -111,6 +120,8 @@ void launch_sample(hipStream_t s, const int64_t* indptr, int64_t D, double fract
                    uint64_t seed, int64_t iteration, int rank, int64_t cap, int32_t* counts,
                    int64_t* weights, int32_t* short_counts);
 // writes partitioned slots: batch_p (row), orig_p (raw member position), nnz_p
+// out[0..2] = {*a, *b, *c} (the inclusive scans' totals for one readback)
+void launch_last3(hipStream_t s, const int32_t* a, const int64_t* b, const int32_t* c, int64_t* out);
 void launch_fill_batch(hipStream_t s, const int64_t* indptr, int64_t D, int64_t cap,
                        const int32_t* counts, const int32_t* count_incl,
                        const int32_t* short_incl, int64_t n_short, int32_t* batch_p,

@@ -138,8 +138,7 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<flo
           a.r[e0 + n] = 0.f;
           if (STATS) {
             a.keys[e0 + n] = (uint32_t)ids[j];
-            a.vals[e0 + n] = (uint32_t)(e0 + n);
-            a.edoc[e0 + n] = (int32_t)slot;
+            a.vals[e0 + n] = entry_val<float>(slot, e0 + n, 0.f);
           }
         }
       }
@@ -368,8 +367,7 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_split(EStepArgs<flo
         a.r[e0 + n] = rr[j];
         if (STATS) {
           a.keys[e0 + n] = (uint32_t)ids[j];
-          a.vals[e0 + n] = (uint32_t)(e0 + n);
-          a.edoc[e0 + n] = (int32_t)slot;
+          a.vals[e0 + n] = entry_val<float>(slot, e0 + n, rr[j]);
         }
       }
     }

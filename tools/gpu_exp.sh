@@ -1,5 +1,5 @@
 #!/bin/bash
-# E-step / step-tail experiments: GPU parity tests, bench, stamps
+# E-step / step-tail experiments: GPU parity tests, bench, kernel stats
 mkdir -p gpurun_out; : > gpurun_out/status.log
 step() {  # step NAME SECONDS CMD...
   local name=$1 secs=$2; shift 2
@@ -11,4 +11,6 @@ step() {  # step NAME SECONDS CMD...
 }
 step pytest_gpu 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread
 step bench_grid 240 python bench.py --steps 10 --warmup 5 --no-cpu-baseline
-STC_LIB=spark-text-clustering_amd/stc/libstc_stamp.so step stamp_grid 240 python tools/stamp_estep.py
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+rm -rf gpurun_out/prof; mkdir -p gpurun_out/prof
+step prof_stats 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/stats -o stats --output-format csv -- python3 bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-hbm-copy
