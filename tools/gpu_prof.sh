@@ -1,13 +1,16 @@
 #!/bin/bash
 # rocprofv3 kernel stats + separate PMC passes (HBM traffic, SQ issue/wait) of the bench workload.
 # Each step has its own time limit; the script stops at the first failure.
+# PROF_PASSES="stats fetch write" limits the passes (default: all five).
 # Summarise afterwards (here): python tools/pmc_summary.py gpurun_out/prof --tag rNN
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof; rm -rf $OUT; mkdir -p $OUT
 B="bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-hbm-copy"
+PASSES=${PROF_PASSES:-"stats fetch write sq grbm"}
 run() {  # run NAME SECONDS ARGS...
   local name=$1 secs=$2; shift 2
+  case " $PASSES " in *" $name "*) ;; *) return 0 ;; esac
   timeout -k 10 "$secs" rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 $B > $OUT/$name.log 2>&1
   local rc=$?; echo "$name rc=$rc" >> $OUT/status.log; return $rc
 }

@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round measurement: GPU tests, smoke, the default bench line (with cpu_baseline), then profiles.
+# PROF_PASSES selects the rocprofv3 passes of tools/gpu_prof.sh (default: all).
 mkdir -p gpurun_out; : > gpurun_out/status.log
 step() {  # step NAME SECONDS CMD...
   local name=$1 secs=$2; shift 2
