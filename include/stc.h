@@ -8,6 +8,9 @@
  * Which reference interface each entry point replaces ([U] = upstream spark-mllib 2.4.3,
  * TextClustering/build.sbt:10; paths relative to /root/reference/TextClustering/src/main/scala):
  *
+ *   stc_tokenize[_hashing_tf_dev] [U] ml.feature.Tokenizer (toLowerCase.split("\\s")), the step in
+ *                               front of HashingTF (the reference's own
+ *                               CoreNLP front-end at LDAClustering.scala:116-139 is out of scope)
  *   stc_hashing_tf[_dev]        [U] mllib.feature.HashingTF.transform / murmur3Hash — the slot of
  *                               the vocab-indexed counting at LDAClustering.scala:154-167
  *   stc_idf_fit                 IDF(minDocFreq).fit(tf).idf — LDAClustering.scala:177
@@ -116,6 +119,22 @@ int stc_hashing_tf(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int
 /* raw per-token bucket indices (test hook for K1): idx_out[n_tok] */
 int stc_hash_tokens(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int64_t* tok_off,
                     int64_t n_tok, int32_t num_features, int hash_variant, int32_t* idx_out);
+
+/* ---- Tokenizer (K0) ----------------------------------------------------------------------
+ * Document d is the UTF-8 string text[text_off[d] .. text_off[d+1]).  Output: Spark's
+ * Tokenizer result — lower-case, split on each Java \\s character ([ \t\n\x0B\f\r]), interior empty
+ * tokens kept, trailing empty tokens dropped, a separator-free string is one token ("" → [""]) —
+ * laid out as stc_hashing_tf's input: the separator-free lower-cased blob utf8_out (capacity
+ * n_bytes), tok_off_out (capacity n_bytes + n_docs + 1) and doc_off_out[n_docs+1].
+ * Lower-casing covers ASCII and Latin-1; a character that needs other case tables fails with
+ * STC_ERR_INVALID_ARG (caseless punctuation/CJK/emoji blocks pass through).                 */
+int stc_tokenize(stc_ctx* ctx, const uint8_t* text, int64_t n_bytes, const int64_t* text_off,
+                 int64_t n_docs, uint8_t* utf8_out, int64_t* n_out_bytes, int64_t* tok_off_out,
+                 int64_t* n_tok_out, int64_t* doc_off_out);
+/* Tokenizer → HashingTF fused on device (no host round trip between the two stages) */
+int stc_tokenize_hashing_tf_dev(stc_ctx* ctx, const uint8_t* text, int64_t n_bytes,
+                                const int64_t* text_off, int64_t n_docs, int32_t num_features,
+                                int binary, int hash_variant, int value_dtype, stc_dcsr** out);
 
 /* ---- IDF (K3 df count, K4 idf, K5 transform) ---------------------------------------------
  * df_j = #rows with value_j > 0, m = #rows (summed over all ranks when connected);

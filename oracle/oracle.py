@@ -107,6 +107,36 @@ def non_negative_mod(x: int, mod: int) -> int:
     return raw + (mod if raw < 0 else 0)
 
 
+# [U] ml.feature.Tokenizer.createTransformFunc: text.toLowerCase.split("\\s") — the step in front of
+# HashingTF.  Java's \s (no UNICODE_CHARACTER_CLASS) is [ \t\n\x0B\f\r];
+# String.split(regex) = split(regex, 0): interior empty strings kept, trailing ones removed, and a
+# string with no match comes back whole ("" → [""]).
+_JAVA_SPACE = " \t\n\x0b\f\r"
+
+
+def java_split_whitespace(s: str):
+    """Java ``s.split("\\s")`` (limit 0), restated with explicit loops."""
+    pieces, cur, matched = [], [], False
+    for ch in s:
+        if ch in _JAVA_SPACE:
+            pieces.append("".join(cur))
+            cur, matched = [], True
+        else:
+            cur.append(ch)
+    if not matched:
+        return [s]
+    pieces.append("".join(cur))
+    while pieces and pieces[-1] == "":
+        pieces.pop()
+    return pieces
+
+
+def tokenize(text: str):
+    """[U] Tokenizer: lower-case then split.  Python's str.lower agrees with Java's
+    toLowerCase(Locale.ROOT) on the ASCII/Latin-1 range the GPU kernel supports."""
+    return java_split_whitespace(text.lower())
+
+
 def hashing_tf(docs, num_features=1 << 18, binary=False, variant=HASH_STANDARD):
     """[U] HashingTF.transform for each doc (a sequence of str tokens) → CSR (sorted indices).
 

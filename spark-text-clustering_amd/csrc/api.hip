@@ -764,6 +764,74 @@ int stc_hashing_tf(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int
   return rc;
 }
 
+// ---- Tokenizer (K0) ---------------------------------------------------------------------
+namespace {
+struct Tokens {
+  DevBuf utf8, tok_off, doc_off;
+  int64_t n_tok = 0, n_bytes = 0;
+};
+void run_tokenizer(Ctx& c, Tokens& t, const uint8_t* text, int64_t n_bytes, const int64_t* text_off,
+                   int64_t n_docs) {
+  STC_REQUIRE(n_bytes >= 0 && n_docs >= 0, "sizes must be >= 0");
+  STC_REQUIRE(n_docs < (int64_t(1) << 31) - 1, "at most 2^31-2 documents per call");
+  STC_REQUIRE(text_off && (n_bytes == 0 || text), "text/text_off");
+  STC_REQUIRE(text_off[0] == 0 && text_off[n_docs] == n_bytes, "text_off must span [0, n_bytes]");
+  for (int64_t d = 0; d < n_docs; ++d) STC_REQUIRE(text_off[d + 1] >= text_off[d], "text_off must be non-decreasing");
+  DevBuf d_text, d_off;
+  d_text.reserve(std::max<int64_t>(n_bytes, 1));
+  d_off.reserve(8 * (n_docs + 1));
+  if (n_bytes) HIP_CHECK(hipMemcpyAsync(d_text.p, text, n_bytes, hipMemcpyHostToDevice, c.stream));
+  HIP_CHECK(hipMemcpyAsync(d_off.p, text_off, 8 * (n_docs + 1), hipMemcpyHostToDevice, c.stream));
+  int64_t bad = -1;
+  tokenizer::tokenize(c, d_text.as<uint8_t>(), d_off.as<int64_t>(), n_docs, t.utf8, t.tok_off, t.doc_off,
+                      t.n_tok, t.n_bytes, bad);
+  if (bad >= 0) {
+    char msg[160];
+    snprintf(msg, sizeof msg, "Tokenizer: the GPU lower-casing covers ASCII, Latin-1 and caseless blocks only; "
+             "unsupported character at byte %lld (lead byte 0x%02X)", (long long)bad, (unsigned)text[bad]);
+    throw Error(STC_ERR_INVALID_ARG, msg);
+  }
+}
+}  // namespace
+
+int stc_tokenize(stc_ctx* ctx, const uint8_t* text, int64_t n_bytes, const int64_t* text_off,
+                 int64_t n_docs, uint8_t* utf8_out, int64_t* n_out_bytes, int64_t* tok_off_out,
+                 int64_t* n_tok_out, int64_t* doc_off_out) {
+  return guard([&] {
+    STC_REQUIRE(ctx && n_out_bytes && n_tok_out && tok_off_out && doc_off_out && (utf8_out || n_bytes == 0),
+                "ctx/outputs");
+    ctx->use();
+    Tokens t;
+    run_tokenizer(*ctx, t, text, n_bytes, text_off, n_docs);
+    hipStream_t s = ctx->stream;
+    if (t.n_bytes) HIP_CHECK(hipMemcpyAsync(utf8_out, t.utf8.p, t.n_bytes, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(tok_off_out, t.tok_off.p, 8 * (t.n_tok + 1), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipMemcpyAsync(doc_off_out, t.doc_off.p, 8 * (n_docs + 1), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    *n_out_bytes = t.n_bytes;
+    *n_tok_out = t.n_tok;
+  });
+}
+
+int stc_tokenize_hashing_tf_dev(stc_ctx* ctx, const uint8_t* text, int64_t n_bytes,
+                                const int64_t* text_off, int64_t n_docs, int32_t num_features,
+                                int binary, int hash_variant, int value_dtype, stc_dcsr** out) {
+  return guard([&] {
+    STC_REQUIRE(ctx && out, "ctx/out");
+    STC_REQUIRE(num_features > 0, "numFeatures must be > 0");
+    STC_REQUIRE(hash_variant == STC_HASH_STANDARD || hash_variant == STC_HASH_SPARK24, "hash_variant");
+    STC_REQUIRE(value_dtype == STC_F32 || value_dtype == STC_F64, "value_dtype");
+    ctx->use();
+    Tokens t;
+    run_tokenizer(*ctx, t, text, n_bytes, text_off, n_docs);
+    auto m = std::make_unique<stc_dcsr>();
+    m->ctx = ctx;
+    hashing::build_csr(*ctx, t.utf8.as<uint8_t>(), t.tok_off.as<int64_t>(), t.n_tok, t.doc_off.as<int64_t>(),
+                       n_docs, num_features, binary, hash_variant, value_dtype, *m);
+    *out = m.release();
+  });
+}
+
 // ---- IDF --------------------------------------------------------------------------------
 int stc_idf_fit(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, double* idf_out,
                 int64_t* df_out, int64_t* m_out) {

@@ -391,6 +391,14 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
                const int64_t* d_doc_off, int64_t n_docs, int32_t num_features, int binary,
                int variant, int value_dtype, DCsr& out);
 }  // namespace hashing
+namespace tokenizer {
+// Spark ML Tokenizer on device: d_text/d_text_off (n_docs+1) in; lower-cased, separator-free blob,
+// token offsets (n_tok+1) and per-document token offsets (n_docs+1) out.  bad_pos >= 0 reports the
+// first byte whose character the kernel cannot lower-case (outputs then unset).
+void tokenize(Ctx& c, const uint8_t* d_text, const int64_t* d_text_off, int64_t n_docs,
+              DevBuf& out_utf8, DevBuf& out_tok_off, DevBuf& out_doc_off, int64_t& n_tok,
+              int64_t& n_out_bytes, int64_t& bad_pos);
+}  // namespace tokenizer
 namespace idf {
 void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df /* cols */);
 void finalize(Ctx& c, const int64_t* d_df, int64_t cols, int64_t m, int64_t min_df, double* d_idf);

@@ -1,0 +1,180 @@
+// tokenizer.hip — K0: Spark ML Tokenizer (`text.toLowerCase.split("\\s")`) on gfx950, the step
+// in front of HashingTF.
+//
+// Replaces [U] org.apache.spark.ml.feature.Tokenizer.createTransformFunc (Spark 2.4.3,
+// build.sbt:10): lower-case the document, split on every single Java `\s` character
+// ([ \t\n\x0B\f\r]), keep interior empty tokens, drop trailing empty tokens (String.split with
+// limit 0), and return the whole string as one token when it holds no separator ("" → [""]).
+// The reference's own CoreNLP/OpenNLP front-end (LDAClustering.scala:116-139) stays out of scope.
+//
+// Lower-casing: ASCII and Latin-1 (U+00C0–U+00DE except U+00D7, the German/French/… capitals)
+// are mapped exactly as Java's String.toLowerCase (root/English locale) maps them; both keep the
+// UTF-8 length.  Code points whose case mapping needs tables this kernel does not carry (Latin
+// Extended, Greek, Cyrillic, fullwidth, …) are REJECTED loudly (STC_ERR_INVALID_ARG with the byte
+// position); caseless blocks that real text carries are accepted: U+0080–U+00FF, U+2000–U+20BF
+// (punctuation, quotes, dashes, currency), U+3000–U+9FFF (CJK), U+1F000–U+1FFFF (emoji).
+//
+// Layout: in = one UTF-8 blob + int64 text offsets per document.  Out = the lower-cased blob with
+// the separator bytes removed, so token t is the contiguous out[tok_off[t] .. tok_off[t+1]) and
+// document d owns tokens [doc_off[d], doc_off[d+1]) — exactly stc_hashing_tf's input.
+// One wave per document walks it 64 bytes at a time (coalesced byte loads); a ballot of the
+// separator flags gives each lane its separator rank, from which both the compacted byte position
+// and the token starts follow without atomics.  Two passes (count, emit) around one device scan.
+// HBM-bound: 2 reads + 1 write of the blob.
+#include <hipcub/hipcub.hpp>
+
+#include "stc_internal.h"
+
+namespace stc {
+namespace tokenizer {
+
+constexpr int kWaves = 4;  // waves (documents) per 256-thread workgroup
+
+__device__ __forceinline__ bool is_java_space(uint32_t b) {
+  return b == 0x20u || (b >= 0x09u && b <= 0x0Du);  // \t \n \x0B \f \r and ' '
+}
+
+// true when the UTF-8 lead byte `b` (followed by `nx`) starts a code point outside the supported set
+__device__ __forceinline__ bool unsupported(uint32_t b, uint32_t nx) {
+  if (b < 0xC4u) return false;                           // ASCII, continuation, U+0080–U+00FF
+  if (b == 0xE2u) return nx < 0x80u || nx > 0x82u;       // U+2000–U+20BF only
+  if (b >= 0xE3u && b <= 0xE9u) return false;            // U+3000–U+9FFF
+  if (b == 0xF0u) return nx != 0x9Fu;                    // U+1F000–U+1FFFF only
+  return true;
+}
+
+__device__ __forceinline__ uint32_t to_lower(uint32_t b, uint32_t prev) {
+  if (b >= 0x41u && b <= 0x5Au) return b + 0x20u;                                // A–Z
+  if (prev == 0xC3u && b >= 0x80u && b <= 0x9Eu && b != 0x97u) return b + 0x20u;  // À–Þ except ×
+  return b;
+}
+
+__device__ __forceinline__ int64_t lanes_below(uint64_t m, int lane) {
+  return __popcll(m & ((lane ? (~0ull >> (64 - lane)) : 0ull)));
+}
+
+// pass 1: per document, token count and kept (non-separator) byte count; first bad byte position
+__global__ __launch_bounds__(64 * kWaves) void k_count(const uint8_t* __restrict__ text,
+                                                       const int64_t* __restrict__ text_off,
+                                                       int64_t n_docs, int64_t* __restrict__ ntok,
+                                                       int64_t* __restrict__ nkeep,
+                                                       unsigned long long* __restrict__ bad) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t d = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); d < n_docs;
+       d += (int64_t)gridDim.x * kWaves) {
+    const int64_t s = text_off[d], e = text_off[d + 1];
+    int64_t seps = 0, last_keep = -1;
+    for (int64_t c = s; c < e; c += 64) {
+      const int64_t i = c + lane;
+      const bool in = i < e;
+      const uint32_t b = in ? text[i] : 0x20u;
+      const bool sep = is_java_space(b);
+      if (in && b >= 0xC4u) {
+        const uint32_t nx = (i + 1 < e) ? text[i + 1] : 0u;
+        if (unsupported(b, nx)) atomicMin(bad, (unsigned long long)i);
+      }
+      const uint64_t sm = __ballot(sep), km = __ballot(in && !sep);
+      seps += __popcll(sm & __ballot(in));
+      if (km) last_keep = c + 63 - __clzll(km);
+    }
+    if (lane == 0) {
+      const int64_t len = e - s;
+      int64_t t;
+      if (seps == 0) t = 1;                      // no match: the whole string ("" included)
+      else if (last_keep < 0) t = 0;             // only separators: every piece is a trailing empty
+      else t = seps + 1 - (e - 1 - last_keep);   // drop the trailing empty pieces
+      ntok[d] = t;
+      nkeep[d] = len - seps;
+    }
+  }
+}
+
+// pass 2: lower-case + compact the kept bytes, write each token's start
+__global__ __launch_bounds__(64 * kWaves) void k_emit(const uint8_t* __restrict__ text,
+                                                      const int64_t* __restrict__ text_off,
+                                                      int64_t n_docs,
+                                                      const int64_t* __restrict__ doc_off,
+                                                      const int64_t* __restrict__ byte_off,
+                                                      uint8_t* __restrict__ out,
+                                                      int64_t* __restrict__ tok_off) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t d = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); d < n_docs;
+       d += (int64_t)gridDim.x * kWaves) {
+    const int64_t s = text_off[d], e = text_off[d + 1];
+    const int64_t base = byte_off[d], tb = doc_off[d], nt = doc_off[d + 1] - tb;
+    if (nt > 0 && lane == 0) tok_off[tb] = base;
+    int64_t seps = 0;
+    for (int64_t c = s; c < e; c += 64) {
+      const int64_t i = c + lane;
+      const bool in = i < e;
+      const uint32_t b = in ? text[i] : 0x20u;
+      const uint32_t prev = (in && i > s) ? text[i - 1] : 0u;
+      const bool sep = is_java_space(b);
+      const uint64_t sm = __ballot(in && sep);
+      const int64_t j = seps + lanes_below(sm, lane);  // separators before byte i in this doc
+      if (in) {
+        if (!sep) out[base + (i - s) - j] = (uint8_t)to_lower(b, prev);
+        else if (j + 1 < nt) tok_off[tb + j + 1] = base + (i - s) - j;
+      }
+      seps += __popcll(sm);
+    }
+  }
+}
+
+static int grid_docs(int64_t n_docs) {
+  int64_t g = ceil_div(n_docs, kWaves);
+  if (g < 1) g = 1;
+  if (g > 256 * 32) g = 256 * 32;
+  return (int)g;
+}
+
+void tokenize(Ctx& c, const uint8_t* d_text, const int64_t* d_text_off, int64_t n_docs,
+              DevBuf& out_utf8, DevBuf& out_tok_off, DevBuf& out_doc_off, int64_t& n_tok,
+              int64_t& n_out_bytes, int64_t& bad_pos) {
+  hipStream_t s = c.stream;
+  DevBuf cnt, keep, byte_off, badb, tmp;
+  cnt.reserve(8 * (n_docs + 1));
+  keep.reserve(8 * (n_docs + 1));
+  byte_off.reserve(8 * (n_docs + 1));
+  badb.reserve(8);
+  out_doc_off.reserve(8 * (n_docs + 1));
+  HIP_CHECK(hipMemsetAsync(cnt.p, 0, 8 * (n_docs + 1), s));
+  HIP_CHECK(hipMemsetAsync(keep.p, 0, 8 * (n_docs + 1), s));
+  HIP_CHECK(hipMemsetAsync(badb.p, 0xFF, 8, s));
+  if (n_docs > 0) {
+    k_count<<<grid_docs(n_docs), 64 * kWaves, 0, s>>>(d_text, d_text_off, n_docs, cnt.as<int64_t>(),
+                                                      keep.as<int64_t>(), badb.as<unsigned long long>());
+    KERNEL_CHECK();
+  }
+  size_t tb = 0;
+  HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt.as<int64_t>(), out_doc_off.as<int64_t>(),
+                                             (int)(n_docs + 1), s));
+  tmp.reserve(tb);
+  HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, cnt.as<int64_t>(), out_doc_off.as<int64_t>(),
+                                             (int)(n_docs + 1), s));
+  HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, keep.as<int64_t>(), byte_off.as<int64_t>(),
+                                             (int)(n_docs + 1), s));
+  int64_t h[3];
+  HIP_CHECK(hipMemcpyAsync(&h[0], out_doc_off.as<int64_t>() + n_docs, 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(&h[1], byte_off.as<int64_t>() + n_docs, 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(&h[2], badb.p, 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  n_tok = h[0];
+  n_out_bytes = h[1];
+  bad_pos = h[2];  // -1 (all ones) when every character is supported
+  if (bad_pos >= 0) return;
+  out_utf8.reserve(std::max<int64_t>(n_out_bytes, 1));
+  out_tok_off.reserve(8 * (n_tok + 1));
+  if (n_docs > 0) {
+    k_emit<<<grid_docs(n_docs), 64 * kWaves, 0, s>>>(d_text, d_text_off, n_docs,
+                                                     out_doc_off.as<int64_t>(), byte_off.as<int64_t>(),
+                                                     out_utf8.as<uint8_t>(), out_tok_off.as<int64_t>());
+    KERNEL_CHECK();
+  }
+  HIP_CHECK(hipMemcpyAsync(out_tok_off.as<int64_t>() + n_tok, byte_off.as<int64_t>() + n_docs, 8,
+                           hipMemcpyDeviceToDevice, s));
+  HIP_CHECK(hipStreamSynchronize(s));  // scratch buffers die at scope exit
+}
+
+}  // namespace tokenizer
+}  // namespace stc

@@ -9,10 +9,10 @@ from . import io
 from .clustering import (LDA, ML_LDA_DEFAULT_SEED, DistributedLDAModel, LdaHandle, LDAModel, MllibLDA,
                          OnlineLDAOptimizer, reference_mini_batch_fraction)
 from .core import Context, CsrMatrix, DeviceCsr
-from .feature import IDF, HashingTF, IDFModel, encode_tokens
+from .feature import IDF, HashingTF, IDFModel, Tokenizer, encode_texts, encode_tokens
 
 __all__ = [
-    "Context", "CsrMatrix", "DeviceCsr", "HashingTF", "IDF", "IDFModel", "encode_tokens", "LDA",
+    "Context", "CsrMatrix", "DeviceCsr", "HashingTF", "IDF", "IDFModel", "Tokenizer", "encode_texts", "encode_tokens", "LDA",
     "LDAModel", "DistributedLDAModel", "LdaHandle", "io", "MllibLDA", "OnlineLDAOptimizer", "ML_LDA_DEFAULT_SEED",
     "reference_mini_batch_fraction", "StcError", "StcIllegalArgument", "load", "STC_F32", "STC_F64",
     "STC_HASH_STANDARD", "STC_HASH_SPARK24", "STC_LAYOUT_VK", "STC_LAYOUT_KV",

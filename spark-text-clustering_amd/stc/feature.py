@@ -34,6 +34,54 @@ def encode_tokens(docs):
     return np.ascontiguousarray(blob), tok_off, doc_off
 
 
+def encode_texts(texts):
+    """list[str|bytes] → (utf8 uint8 blob, text_off int64[n_docs+1]) — one string per document."""
+    parts = [t.encode("utf-8") if isinstance(t, str) else bytes(t) for t in texts]
+    blob = np.frombuffer(b"".join(parts), np.uint8) if parts else np.zeros(0, np.uint8)
+    off = np.zeros(len(parts) + 1, np.int64)
+    np.cumsum([len(p) for p in parts], out=off[1:])
+    return np.ascontiguousarray(blob), off
+
+
+class Tokenizer:
+    """Lower-cases each document and splits it on Java whitespace, on the GPU (kernel K0).
+
+    Mirrors ``org.apache.spark.ml.feature.Tokenizer`` ([U] spark 2.4.3, build.sbt:10):
+    ``text.toLowerCase.split("\\s")`` — interior empty tokens kept, trailing ones dropped, a
+    document without whitespace is one token.  Lower-casing covers ASCII and Latin-1; text with
+    characters that need other case tables raises ``ValueError`` (STC_ERR_INVALID_ARG).
+    """
+
+    def __init__(self, inputCol=None, outputCol=None, ctx: Context | None = None):
+        self.inputCol, self.outputCol = inputCol, outputCol
+        self._ctx = ctx
+
+    @property
+    def ctx(self):
+        return self._ctx or Context.get()
+
+    def encode(self, texts):
+        """Tokens of every doc in HashingTF's input layout: (utf8 blob, tok_off, doc_off)."""
+        text, off = encode_texts(texts)
+        n_docs = off.size - 1
+        blob = np.zeros(max(text.size, 1), np.uint8)
+        tok_off = np.zeros(text.size + n_docs + 1, np.int64)
+        doc_off = np.zeros(n_docs + 1, np.int64)
+        nb, nt = C.c_int64(), C.c_int64()
+        L.check(self.ctx.lib.stc_tokenize(self.ctx.handle, L.ptr(text, C.c_uint8), text.size,
+                                          L.ptr(off, C.c_int64), n_docs, L.ptr(blob, C.c_uint8),
+                                          C.byref(nb), L.ptr(tok_off, C.c_int64), C.byref(nt),
+                                          L.ptr(doc_off, C.c_int64)))
+        return blob[:nb.value].copy(), tok_off[:nt.value + 1].copy(), doc_off
+
+    def transform(self, texts):
+        """list[str] → list[list[str]] (the tokens of each document)."""
+        blob, tok_off, doc_off = self.encode(texts)
+        raw = blob.tobytes()
+        toks = [raw[tok_off[t]:tok_off[t + 1]].decode("utf-8") for t in range(tok_off.size - 1)]
+        return [toks[doc_off[d]:doc_off[d + 1]] for d in range(doc_off.size - 1)]
+
+
 class HashingTF:
     """Maps a sequence of terms to their term frequencies using the hashing trick.
 
@@ -92,6 +140,17 @@ class HashingTF:
             self.ctx.handle, L.ptr(blob, C.c_uint8), blob.size, L.ptr(tok_off, C.c_int64),
             tok_off.size - 1, L.ptr(doc_off, C.c_int64), doc_off.size - 1, self.numFeatures,
             int(self.binary), _VARIANTS[self.hashAlgorithm], int(value_dtype), C.byref(h)))
+        return DeviceCsr(self.ctx, h)
+
+    def transform_text_device(self, texts, value_dtype=L.STC_F64) -> DeviceCsr:
+        """Tokenizer → HashingTF fused on the GPU: raw document strings in, term frequencies left
+        resident in HBM (no host round trip between the stages)."""
+        text, off = encode_texts(texts)
+        h = C.c_void_p()
+        L.check(self.ctx.lib.stc_tokenize_hashing_tf_dev(
+            self.ctx.handle, L.ptr(text, C.c_uint8), text.size, L.ptr(off, C.c_int64), off.size - 1,
+            self.numFeatures, int(self.binary), _VARIANTS[self.hashAlgorithm], int(value_dtype),
+            C.byref(h)))
         return DeviceCsr(self.ctx, h)
 
     def transform(self, docs, encoded=None) -> CsrMatrix:
