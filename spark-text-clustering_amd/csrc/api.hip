@@ -778,7 +778,7 @@ void run_tokenizer(Ctx& c, Tokens& t, const uint8_t* text, int64_t n_bytes, cons
   STC_REQUIRE(text_off[0] == 0 && text_off[n_docs] == n_bytes, "text_off must span [0, n_bytes]");
   for (int64_t d = 0; d < n_docs; ++d) STC_REQUIRE(text_off[d + 1] >= text_off[d], "text_off must be non-decreasing");
   DevBuf d_text, d_off;
-  d_text.reserve(std::max<int64_t>(n_bytes, 1));
+  d_text.reserve(n_bytes + 64);  // k_count reads whole aligned dwords past the last byte
   d_off.reserve(8 * (n_docs + 1));
   if (n_bytes) HIP_CHECK(hipMemcpyAsync(d_text.p, text, n_bytes, hipMemcpyHostToDevice, c.stream));
   HIP_CHECK(hipMemcpyAsync(d_off.p, text_off, 8 * (n_docs + 1), hipMemcpyHostToDevice, c.stream));

@@ -17,7 +17,7 @@
 // Layout: in = one UTF-8 blob + int64 text offsets per document.  Out = the lower-cased blob with
 // the separator bytes removed, so token t is the contiguous out[tok_off[t] .. tok_off[t+1]) and
 // document d owns tokens [doc_off[d], doc_off[d+1]) — exactly stc_hashing_tf's input.
-// One wave per document walks it 64 bytes at a time (coalesced byte loads); a ballot of the
+// One wave per document (k_count: 256 bytes per step as aligned dword lane loads; k_emit: 64); a ballot of the
 // separator flags gives each lane its separator rank, from which both the compacted byte position
 // and the token starts follow without atomics.  Two passes (count, emit) around one device scan.
 // HBM-bound: 2 reads + 1 write of the blob.
@@ -53,7 +53,9 @@ __device__ __forceinline__ int64_t lanes_below(uint64_t m, int lane) {
   return __popcll(m & ((lane ? (~0ull >> (64 - lane)) : 0ull)));
 }
 
-// pass 1: per document, token count and kept (non-separator) byte count; first bad byte position
+// pass 1: per document, token count and kept (non-separator) byte count; first bad byte position.
+// Each lane reads one aligned dword (the caller pads the blob by >= 4 bytes), so a wave step covers
+// 256 bytes; the four per-byte ballots give the separator count and the last kept byte.
 __global__ __launch_bounds__(64 * kWaves) void k_count(const uint8_t* __restrict__ text,
                                                        const int64_t* __restrict__ text_off,
                                                        int64_t n_docs, int64_t* __restrict__ ntok,
@@ -64,18 +66,26 @@ __global__ __launch_bounds__(64 * kWaves) void k_count(const uint8_t* __restrict
        d += (int64_t)gridDim.x * kWaves) {
     const int64_t s = text_off[d], e = text_off[d + 1];
     int64_t seps = 0, last_keep = -1;
-    for (int64_t c = s; c < e; c += 64) {
-      const int64_t i = c + lane;
-      const bool in = i < e;
-      const uint32_t b = in ? text[i] : 0x20u;
-      const bool sep = is_java_space(b);
-      if (in && b >= 0xC4u) {
-        const uint32_t nx = (i + 1 < e) ? text[i + 1] : 0u;
-        if (unsupported(b, nx)) atomicMin(bad, (unsigned long long)i);
+    for (int64_t c = s & ~int64_t(3); c < e; c += 256) {
+      const int64_t w = c + 4 * lane;
+      const uint32_t word = (w < e) ? *reinterpret_cast<const uint32_t*>(text + w) : 0x20202020u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t i = w + j;
+        const bool in = i >= s && i < e;
+        const uint32_t b = (word >> (8 * j)) & 0xFFu;
+        const bool sep = is_java_space(b);
+        if (in && b >= 0xC4u) {
+          const uint32_t nx = (i + 1 < e) ? text[i + 1] : 0u;
+          if (unsupported(b, nx)) atomicMin(bad, (unsigned long long)i);
+        }
+        const uint64_t sm = __ballot(in && sep), km = __ballot(in && !sep);
+        seps += __popcll(sm);
+        if (km) {
+          const int64_t lk = c + 4 * (63 - __clzll(km)) + j;
+          last_keep = lk > last_keep ? lk : last_keep;
+        }
       }
-      const uint64_t sm = __ballot(sep), km = __ballot(in && !sep);
-      seps += __popcll(sm & __ballot(in));
-      if (km) last_keep = c + 63 - __clzll(km);
     }
     if (lane == 0) {
       const int64_t len = e - s;
