@@ -57,6 +57,9 @@ enum stc_status {
   STC_ERR_STATE = 5        /* call not valid in the handle's current state */
 };
 
+/* The reference pins spark-mllib 2.4.3 (TextClustering/build.sbt:10), whose HashingTF hashes with the
+ * legacy tail: callers reproducing the reference's pipeline pass STC_HASH_SPARK24 (the Python mirror's
+ * default, stc.HashingTF(hashAlgorithm="murmur3-spark24")).  The two agree iff len % 4 == 0. */
 enum stc_hash_variant {
   STC_HASH_STANDARD = 0, /* MurmurHash3_x86_32 (Spark 3.x hashUnsafeBytes2) */
   STC_HASH_SPARK24 = 1   /* Spark 2.4.x hashUnsafeBytes: per-byte sign-extended tail */

@@ -438,9 +438,11 @@ def log_likelihood_bound(docs, gamma0s, topics_matrix, alpha, eta):
         b += np.sum(gammaln(gamma) - gammaln(alpha))
         b += gammaln(alpha.sum()) - gammaln(gamma.sum())
         corpus += b
+    # E[log p(β|η) − log q(β|λ)]: Σ(η−λ)·Elogβ + Σ(lgamma λ − lgamma η) + Σ_k (lgamma(Vη) − lgamma Σ_v λ_vk)
+    # (upstream: `sum(lgamma(sumEta) - lgamma(sum(lambda(::, breeze.linalg.*))))`, λ = topicsMatrix V×k)
     sum_eta = eta * V
     topics = (np.sum((eta - lam) * elog_beta) + np.sum(gammaln(lam) - gammaln(eta))
-              + np.sum(gammaln(lam.sum(axis=0)) - gammaln(sum_eta)))
+              + np.sum(gammaln(sum_eta) - gammaln(lam.sum(axis=0))))
     return corpus + topics, corpus, topics
 
 

@@ -385,32 +385,41 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
   L.s_sincl.reserve(4 * D);
   const int64_t it = L.iteration + 1;
   record(L, 0);
-  lda::launch_sample(s, L.corpus->indptr.as<int64_t>(), D, L.cfg.mini_batch_fraction,
-                     L.cfg.sample_with_replacement, L.cfg.seed, it, c.rank, L.wave_cap,
-                     L.s_counts.as<int32_t>(), L.s_weights.as<int64_t>(), L.s_short.as<int32_t>());
-  incl_scan<int32_t>(L, L.s_counts.as<int32_t>(), L.s_cincl.as<int32_t>(), D);
-  incl_scan<int64_t>(L, L.s_weights.as<int64_t>(), L.s_wincl.as<int64_t>(), D);
-  incl_scan<int32_t>(L, L.s_short.as<int32_t>(), L.s_sincl.as<int32_t>(), D);
-  // (n, E, n_short) from the scans' last elements: one kernel packs them, one copy into pinned
-  // memory (three pageable copies cost ≈ 90 µs of idle GPU per step), one sync
   if (!L.hcnt) HIP_CHECK(hipHostMalloc((void**)&L.hcnt, 4 * sizeof(int64_t), hipHostMallocDefault));
   L.dcnt.reserve(4 * sizeof(int64_t));
-  lda::launch_last3(s, L.s_cincl.as<int32_t>() + (D - 1), L.s_wincl.as<int64_t>() + (D - 1),
-                    L.s_sincl.as<int32_t>() + (D - 1), L.dcnt.as<int64_t>());
-  HIP_CHECK(hipMemcpyAsync(L.hcnt, L.dcnt.p, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  if (D > 0) {
+    lda::launch_sample(s, L.corpus->indptr.as<int64_t>(), D, L.cfg.mini_batch_fraction,
+                       L.cfg.sample_with_replacement, L.cfg.seed, it, c.rank, L.wave_cap,
+                       L.s_counts.as<int32_t>(), L.s_weights.as<int64_t>(), L.s_short.as<int32_t>());
+    incl_scan<int32_t>(L, L.s_counts.as<int32_t>(), L.s_cincl.as<int32_t>(), D);
+    incl_scan<int64_t>(L, L.s_weights.as<int64_t>(), L.s_wincl.as<int64_t>(), D);
+    incl_scan<int32_t>(L, L.s_short.as<int32_t>(), L.s_sincl.as<int32_t>(), D);
+    // (n, E, n_short) from the scans' last elements: one kernel packs them, one copy into pinned
+    // memory (three pageable copies cost ≈ 90 µs of idle GPU per step), one sync
+    lda::launch_last3(s, L.s_cincl.as<int32_t>() + (D - 1), L.s_wincl.as<int64_t>() + (D - 1),
+                      L.s_sincl.as<int32_t>() + (D - 1), L.dcnt.as<int64_t>());
+  } else {  // a rank without documents still takes part in every collective below
+    HIP_CHECK(hipMemsetAsync(L.dcnt.p, 0, 3 * sizeof(int64_t), s));
+  }
+  // Spark skips a step only when the GLOBAL batch is empty (`batch.isEmpty()` over the whole RDD):
+  // word 3 = Σ_ranks n, so every rank takes the same decision and the collectives stay paired
+  HIP_CHECK(hipMemcpyAsync(L.dcnt.as<int64_t>() + 3, L.dcnt.p, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+  if (c.comm)
+    RCCL_CHECK(ncclAllReduce(L.dcnt.as<int64_t>() + 3, L.dcnt.as<int64_t>() + 3, 1, ncclInt64, ncclSum, c.comm, s));
+  HIP_CHECK(hipMemcpyAsync(L.hcnt, L.dcnt.p, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  const int64_t n32 = L.hcnt[0], E = L.hcnt[1], ns32 = L.hcnt[2];
+  const int64_t n = L.hcnt[0], E = L.hcnt[1], ns32 = L.hcnt[2], n_global = L.hcnt[3];
   if (L.timing) harvest(L, L.ev_set ^ 1);  // the previous step's events have completed
-  const int64_t n = n32;
   // Spark's next(): `if (batch.isEmpty()) return this` — no iteration increment
-  if (n == 0) {
+  if (n_global == 0) {
     if (st) *st = stc_step_stats{};
     return;
   }
   ensure_batch<T>(L, n, E);
-  lda::launch_fill_batch(s, L.corpus->indptr.as<int64_t>(), D, L.wave_cap, L.s_counts.as<int32_t>(),
-                         L.s_cincl.as<int32_t>(), L.s_sincl.as<int32_t>(), ns32, L.batch.as<int32_t>(),
-                         L.orig.as<int32_t>(), L.nnzp.as<int64_t>());
+  if (n > 0)
+    lda::launch_fill_batch(s, L.corpus->indptr.as<int64_t>(), D, L.wave_cap, L.s_counts.as<int32_t>(),
+                           L.s_cincl.as<int32_t>(), L.s_sincl.as<int32_t>(), ns32, L.batch.as<int32_t>(),
+                           L.orig.as<int32_t>(), L.nnzp.as<int64_t>());
   slot_offsets(L, n);
   estep_and_stats<T>(L, n, ns32, E, nullptr, it);
   train_tail<T>(L, n, E, st);
@@ -506,8 +515,10 @@ double topics_part(stc_lda& L) {
   HIP_CHECK(hipMemcpyAsync(&part, L.scal.as<double>() + 3, sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipMemcpyAsync(cs.data(), L.colsum.p, sizeof(double) * L.k, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
+  // [U] logLikelihoodBound topicsPart, last term: Σ_k (lgamma(sumEta) − lgamma(Σ_v λ_vk)),
+  // sumEta = η·V (Dirichlet normaliser of q(β_k|λ_k) minus that of p(β_k|η))
   const double lg_sum_eta = std::lgamma(L.eta * (double)L.V);
-  for (int t = 0; t < L.k; ++t) part += std::lgamma(cs[(size_t)t]) - lg_sum_eta;
+  for (int t = 0; t < L.k; ++t) part += lg_sum_eta - std::lgamma(cs[(size_t)t]);
   return part;
 }
 

@@ -801,7 +801,8 @@ void launch_init_lambda(hipStream_t s, double* lam, int64_t V, int k, uint64_t s
   KERNEL_CHECK();
 }
 
-// topicsPart of logLikelihoodBound without the per-topic lgamma(Σλ) − lgamma(ηV) term
+// topicsPart of logLikelihoodBound: Σ(η−λ)·Elogβ + Σ(lgamma λ − lgamma η) over the V×k elements; the
+// per-topic Σ_k (lgamma(ηV) − lgamma Σ_v λ_vk) term is added on the host (api.hip topics_part)
 template <typename T>
 __global__ __launch_bounds__(256) void k_topics_bound(const double* __restrict__ lam,
                                                       const double* __restrict__ colsum, int64_t V,

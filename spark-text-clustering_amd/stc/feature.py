@@ -86,11 +86,14 @@ class HashingTF:
     """Maps a sequence of terms to their term frequencies using the hashing trick.
 
     numFeatures (default 2^18) buckets; bucket = nonNegativeMod(murmur3_x86_32(utf8(term), 42),
-    numFeatures).  ``hashAlgorithm="murmur3"`` is the standard MurmurHash3_x86_32 tail (Spark 3.x);
-    ``"murmur3-spark24"`` reproduces Spark 2.4's per-byte tail (the version build.sbt pins).
+    numFeatures).  The default ``hashAlgorithm="murmur3-spark24"`` is what the pinned Spark 2.4.3
+    (TextClustering/build.sbt:10) computes: ``Murmur3_x86_32.hashUnsafeBytes`` mixes each of the
+    len % 4 tail bytes, sign-extended, as its own block, so a drop-in for the reference's pipeline
+    lands every term in the same bucket.  ``"murmur3"`` selects the standard MurmurHash3_x86_32 tail
+    (Spark 3.x ``hashUnsafeBytes2``); the two agree whenever the UTF-8 length is a multiple of 4.
     """
 
-    def __init__(self, numFeatures=1 << 18, binary=False, hashAlgorithm="murmur3",
+    def __init__(self, numFeatures=1 << 18, binary=False, hashAlgorithm="murmur3-spark24",
                  inputCol=None, outputCol=None, ctx: Context | None = None):
         self.setNumFeatures(numFeatures)
         self.setBinary(binary)

@@ -46,13 +46,14 @@ def test_library_is_gfx950_code():
 def test_fails_loudly_without_gpu():
     import stc
 
-    if os.environ.get("HIP_VISIBLE_DEVICES") is None:
-        try:
-            n = stc.Context.device_count()
-        except stc.StcError:
-            n = 0
-        if n > 0:
-            pytest.skip("a GPU is visible")
+    # probe whatever devices this process can see (a GPU box may set HIP_VISIBLE_DEVICES to a real
+    # device list): the test is about the no-GPU case only
+    try:
+        n = stc.Context.device_count()
+    except stc.StcError:
+        n = 0
+    if n > 0:
+        pytest.skip("a GPU is visible")
     with pytest.raises(stc.StcError):
         stc.Context(0)
 

@@ -29,7 +29,7 @@ def test_murmur3_known_answers_on_device(ctx):
 
     from oracle import oracle as O
 
-    htf = stc.HashingTF(numFeatures=(1 << 31) - 1, ctx=ctx)
+    htf = stc.HashingTF(numFeatures=(1 << 31) - 1, hashAlgorithm="murmur3", ctx=ctx)
     words = ["", "a", "ab", "abc", "abcd", "hello", "The quick brown fox jumps over the lazy dog"]
     got = htf.indices_of(words)
     for w, g in zip(words, got):
@@ -109,12 +109,12 @@ def test_pipeline_hashing_idf_device_resident(ctx, oracle):
 
     rng = np.random.default_rng(4)
     docs = random_tokens(rng, 200, max_len=60)
-    htf = stc.HashingTF(numFeatures=1 << 12, ctx=ctx)
+    htf = stc.HashingTF(numFeatures=1 << 12, ctx=ctx)  # default: Spark 2.4.3's legacy tail
     d = htf.transform_device(docs)
     model = stc.IDF(minDocFreq=2, ctx=ctx).fit_device(d)
     model.transform_device(d)
     got = d.download()
-    ip, ix, vv = oracle.hashing_tf(docs, 1 << 12)
+    ip, ix, vv = oracle.hashing_tf(docs, 1 << 12, variant=oracle.HASH_SPARK24)
     idf_o, _, _ = oracle.idf_fit(ip, ix, vv, 1 << 12, 2)
     assert np.array_equal(got.indices, ix)
     np.testing.assert_allclose(got.values, oracle.idf_transform(ix, vv, idf_o), rtol=1e-15, atol=0)

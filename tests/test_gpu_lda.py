@@ -141,10 +141,16 @@ def test_log_likelihood_and_perplexity(ctx, oracle, dtype):
     ll = model.logLikelihood(corpus, gamma0=g0)
     lp = model.logPerplexity(corpus, gamma0=g0)
     docs = [corpus.row(i) for i in range(D)]
-    b_o, _, _ = oracle.log_likelihood_bound(docs, list(g0), lam, alpha, 0.07)
+    b_o, cp_o, tp_o = oracle.log_likelihood_bound(docs, list(g0), lam, alpha, 0.07)
     lp_o = oracle.log_perplexity(docs, list(g0), lam, alpha, 0.07)
     assert abs(ll - b_o) / abs(b_o) < TOL[dtype]["bound"], (ll, b_o)
     assert abs(lp - lp_o) / abs(lp_o) < TOL[dtype]["bound"], (lp, lp_o)
+    # the two parts separately (the topics part is pinned independently in test_bound_restatement.py)
+    d = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F32 if dtype == "f32" else stc.STC_F64)
+    parts = model._h.bound(d, model.gammaSeed, 0, g0)
+    assert abs(parts["corpus_part"] - cp_o) / abs(cp_o) < TOL[dtype]["bound"], (parts, cp_o)
+    assert abs(parts["topics_part"] - tp_o) / abs(tp_o) < 1e-10, (parts, tp_o)  # fp64 on every path
+    assert parts["token_count"] == sum(float(np.sum(c)) for _, c in docs)
 
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
