@@ -221,7 +221,12 @@ void launch_split(stc_lda& L, lda::EStepArgs<T> a, int64_t n, int64_t n_short, b
       lda::launch_estep_wave(s, w, stats, bound);
     }
   } else {
-    STC_REQUIRE(n_short == 0, "wave kernel is fp32-only");
+    if (n_short > 0) {
+      lda::EStepArgs<double> w = a;
+      w.slot0 = 0;
+      w.n = n_short;
+      lda::launch_estep_grid64(s, w, stats, bound);
+    }
   }
   if (n > n_short) {
     a.slot0 = n_short;
@@ -937,9 +942,10 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->lds_rows = cfg->dtype == STC_F32 ? lda::estep_lds_rows<float>(L->k, L->kp, L->P)
                                         : lda::estep_lds_rows<double>(L->k, L->kp, L->P);
     const char* nw = std::getenv("STC_DISABLE_WAVE");
-    L->wave_cap = (cfg->dtype == STC_F32 && !(nw && nw[0] == '1') && lda::wave_row_cap(L->k) > 0)
-                      ? lda::wave_row_cap(L->k)
-                      : -1;  // −1: no slot is "short" (not even empty docs)
+    // docs with nnz <= wave_cap run the register-resident grid kernel (fp32: lda_grid.hip, fp64:
+    // lda_grid64.hip), the rest the workgroup kernel (lda.hip); −1: no slot is "short" (not even empty)
+    const int cap = cfg->dtype == STC_F32 ? lda::wave_row_cap(L->k) : lda::grid64_row_cap(L->k);
+    L->wave_cap = (!(nw && nw[0] == '1') && cap > 0) ? cap : -1;
     // α / η resolution ([U] OnlineLDAOptimizer.initialize)
     std::vector<double> alpha((size_t)L->k);
     const int alen = cfg->doc_concentration ? cfg->doc_concentration_len : 0;

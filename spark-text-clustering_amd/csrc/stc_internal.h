@@ -209,8 +209,24 @@ __device__ inline double digamma_fast_d(double x) {
   const double iy = rcp_nr(y);
   const double f = iy * iy;
   const double t = f * (-1.0 / 12.0 + f * (1.0 / 120.0 + f * (-1.0 / 252.0 + f * (1.0 / 240.0 +
-                   f * (-1.0 / 132.0 + f * (691.0 / 32760.0 + f * (-1.0 / 12.0 + f * 3617.0 / 8160.0)))))));
+                   f * (-1.0 / 132.0 + f * (691.0 / 32760.0 + f * (-1.0 / 12.0 + f * (3617.0 / 8160.0))))))));
   return (sh ? -c : 0.0) + log(y) - 0.5 * iy + t;
+}
+// exp(ψ(x) − cst) for the fp64 E-step's eθ = exp(ψ(γ) − ψ(Σγ)), without the logarithm: with ψ(x) =
+// ln y − 0.5/y + t(y) − s(x) as in digamma_fast_d, exp(ψ(x) − cst) = y · exp(t − 0.5/y − s − cst).
+__device__ inline double exp_digamma_minus_d(double x, double cst) {
+  const bool sh = x <= 5.0;
+  const double q = ((((((x + 15.0) * x + 85.0) * x + 225.0) * x + 274.0) * x + 120.0) * x);
+  const double p = (((((6.0 * x + 75.0) * x + 340.0) * x + 675.0) * x + 548.0) * x + 120.0);
+  const double iq = rcp_nr(sh ? q : 1.0);
+  double c = p * iq;
+  c = fma(fma(-q, c, p), iq, c);
+  const double y = sh ? x + 6.0 : x;
+  const double iy = rcp_nr(y);
+  const double f = iy * iy;
+  const double t = f * (-1.0 / 12.0 + f * (1.0 / 120.0 + f * (-1.0 / 252.0 + f * (1.0 / 240.0 +
+                   f * (-1.0 / 132.0 + f * (691.0 / 32760.0 + f * (-1.0 / 12.0 + f * (3617.0 / 8160.0))))))));
+  return y * exp(((sh ? -c : 0.0) - 0.5 * iy + t) - cst);
 }
 
 __host__ __device__ inline double trigamma_d(double x) {

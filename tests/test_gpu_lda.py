@@ -28,10 +28,12 @@ def _handle(ctx, corpus, k, dtype, lam=None, **kw):
 
 @pytest.mark.parametrize("dtype,k,kernel", [("f64", 16, "wg"), ("f32", 16, "wave"), ("f32", 16, "wg"),
                                              ("f32", 100, "wave"), ("f32", 100, "wg"), ("f32", 128, "wave"),
-                                             ("f32", 77, "wave")])
+                                             ("f32", 77, "wave"), ("f64", 100, "wave"), ("f64", 100, "wg"),
+                                             ("f64", 40, "wave"), ("f64", 20, "wave"), ("f64", 104, "wave")])
 def test_estep_gamma_and_stat(ctx, oracle, dtype, k, kernel, monkeypatch):
-    """Both E-step kernels (wave-per-doc for fp32 k<=128, workgroup-per-doc otherwise) vs the oracle,
-    including docs longer than the wave's VGPR capacity (routed to the workgroup kernel)."""
+    """Both E-step kernels (the register-resident grid kernels — fp32 k <= 128, fp64 k <= 104 with
+    R = 1..6 row sets, the sixth from LDS — and the workgroup-per-doc kernel otherwise) vs the oracle,
+    including docs longer than the grid's row capacity (routed to the workgroup kernel)."""
     if kernel == "wg":
         monkeypatch.setenv("STC_DISABLE_WAVE", "1")
     rng = np.random.default_rng(10 + k)

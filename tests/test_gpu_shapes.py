@@ -24,6 +24,19 @@ def _tiled_topics(rng, V, k, P=4099):
     return lam
 
 
+_CORPUS = {}
+
+
+def _full_corpus(D, L, V, k):
+    from stc import synth
+
+    key = (D, L, V, k)
+    if key not in _CORPUS:
+        _CORPUS.clear()
+        _CORPUS[key] = synth.make_corpus("zipf", D, L, V, k, 20261015)
+    return _CORPUS[key]
+
+
 def _eeb_rows(lam, ids, oracle):
     """Spark's expElogβ restricted to rows `ids` (column sums over the whole vocabulary)."""
     colsum = lam.sum(axis=0)
@@ -31,21 +44,23 @@ def _eeb_rows(lam, ids, oracle):
 
 
 @pytest.mark.parametrize("cfg", [
-    dict(name="config2", V=1 << 18, k=100, L=200, D=24),
-    dict(name="config4", V=1 << 20, k=500, L=500, D=4),
-    dict(name="config5", V=1 << 18, k=2000, L=50, D=6),
+    dict(name="config2", V=1 << 18, k=100, L=200, D=24, dtype="f32"),
+    dict(name="config2-f64", V=1 << 18, k=100, L=200, D=24, dtype="f64"),
+    dict(name="config4", V=1 << 20, k=500, L=500, D=4, dtype="f32"),
+    dict(name="config5", V=1 << 18, k=2000, L=50, D=6, dtype="f32"),
 ], ids=lambda c: c["name"])
 def test_estep_at_baseline_shapes(ctx, oracle, cfg):
     import stc
     from stc import synth
 
-    rng = np.random.default_rng(zlib.crc32(cfg["name"].encode()))  # stable across processes
+    rng = np.random.default_rng(zlib.crc32(cfg["name"].split("-")[0].encode()))  # stable across processes
     V, k, D = cfg["V"], cfg["k"], cfg["D"]
     corpus = synth.zipf_corpus(D, cfg["L"], V, seed=31 + k)
     lam = _tiled_topics(rng, V, k)
     g0 = rng.gamma(100.0, 0.01, size=(D, k))
-    h = stc.LdaHandle(ctx, k, V, dtype="f32")
-    dc = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F32)
+    f64 = cfg["dtype"] == "f64"
+    h = stc.LdaHandle(ctx, k, V, dtype=cfg["dtype"])
+    dc = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F64 if f64 else stc.STC_F32)
     h.set_corpus(dc, D)
     h.set_topics(lam)
     gamma, _, iters = h.estep(np.arange(D), g0)
@@ -54,6 +69,10 @@ def test_estep_at_baseline_shapes(ctx, oracle, cfg):
         cid, cts = corpus.row(i)
         eeb = _eeb_rows(lam, cid, oracle)
         g, _, it = oracle.variational_topic_inference(np.arange(cid.size), cts, eeb, alpha, g0[i])
+        if f64:  # Spark's precision: the same fixed point and the same iteration count
+            np.testing.assert_allclose(gamma[i], g, rtol=1e-9, err_msg=f"{cfg['name']} doc {i}")
+            assert int(iters[i]) == it, (iters[i], it)
+            continue
         # fp32 vs fp64: the fixed point is only defined up to Spark's own stopping rule (mean |Δγ| ≤
         # 1e-3, i.e. Σ|Δγ| ≤ 1e-3·k per iteration), and the two runs may stop an iteration apart: so
         # Σ|γ − γ_oracle| within two iterations' worth, and 2e-3 relative on every topic that holds
@@ -65,16 +84,17 @@ def test_estep_at_baseline_shapes(ctx, oracle, cfg):
         assert abs(int(iters[i]) - it) <= max(2, it // 20), (iters[i], it)
 
 
-def test_full_size_minibatch_properties(ctx, oracle):
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_full_size_minibatch_properties(ctx, oracle, dtype):
     """BASELINE configs[1] at full size: 1M docs × 200 tokens, V = 2^18, k = 100, f = 0.05."""
     import stc
     from stc import synth
 
     D, L, V, k = 1_000_000, 200, 1 << 18, 100
-    corpus = synth.make_corpus("zipf", D, L, V, k, 20261015)
-    dc = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F32)
+    corpus = _full_corpus(D, L, V, k)
+    dc = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F32 if dtype == "f32" else stc.STC_F64)
     h = stc.LdaHandle(ctx, k, V, mini_batch_fraction=0.05, optimize_doc_concentration=True, seed=1,
-                      dtype="f32")
+                      dtype=dtype)
     h.set_corpus(dc, D)
     h.init_random(1)
     for _ in range(3):
@@ -90,9 +110,9 @@ def test_full_size_minibatch_properties(ctx, oracle):
     tok = np.array([corpus.row(i)[1].sum() for i in ids])
     # Σ_t γ_t = Σα + Σ_n cts_n·(1 − ε/φ_n); ε/φ_n is negligible on this corpus
     rel = np.abs(gamma.sum(axis=1) - alpha.sum() - tok) / tok
-    assert rel.max() < 2e-4, rel.max()
+    assert rel.max() < (2e-4 if dtype == "f32" else 1e-11), rel.max()
     # Σ_{v,t} sstats_vt · expElogβ_vt = Σ_d Σ_n cts_n (φ normalisation)
     eeb = oracle.topics_exp_elog_beta(lam)
     tot = float(np.sum(stat * eeb))
-    assert abs(tot - tok.sum()) / tok.sum() < 1e-4, (tot, tok.sum())
+    assert abs(tot - tok.sum()) / tok.sum() < (1e-4 if dtype == "f32" else 1e-10), (tot, tok.sum())
     assert iters.min() >= 1
