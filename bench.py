@@ -1,26 +1,33 @@
 """Benchmark: online-LDA minibatch steps (E-step + sstats + [RCCL all-reduce] + M-step) on MI355X.
 
-Workload (BASELINE.json configs[1]): synthetic Zipfian corpus, 1M docs × 200 tokens per GPU,
-V = 2^18, online LDA k = 100, subsamplingRate 0.05 (≈50k docs per minibatch per GPU).  A "step" is
-one OnlineLDAOptimizer.next(): device-side membership sampling, the E-step over the minibatch, the
+Workload (BASELINE.json configs[1]): a synthetic Zipfian corpus of 1M docs × 200 tokens, V = 2^18,
+online LDA k = 100, subsamplingRate 0.05 (≈50k docs per minibatch).  A "step" is one
+OnlineLDAOptimizer.next(): device-side membership sampling, the E-step over the minibatch, the
 term-sorted sufficient statistics, the all-reduce (N > 1) and the λ / expElogβ / α update.  The
-corpus is resident in HBM before the timed region.  Weak scaling: every rank owns its own 1M-doc
-shard (corpusSize = N·1M for the λ update), one RCCL all-reduce of k×V sstats per step.
+corpus is resident in HBM before the timed region.  The headline computes in fp64 like Spark's
+Breeze Double E-step (--dtype f64); the fp32 path and the planted-topic (warm) model state are
+reported as secondary lines ("secondary") in the same JSON object at N = 1.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--docs D] [--corpus zipf|zipf-lda]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dtype f64|f32] [--scaling strong|weak]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N   (one rank per GPU)
 
-Rank 0 prints ONE JSON line.  value = Σ_ranks minibatch docs in the K timed steps ÷ max-over-ranks
-wall time.  Model state: timing starts after exactly --state-minibatches (20)
-minibatches from λ₀ (burn-in + warmup), so the inner-iteration count does not depend on --warmup;
-the first 3 minibatches from λ₀ are timed separately as the "cold" figure.
-roofline: the dominant kernel, k_estep_grid (one launch per minibatch): SURVEY.md §8(d) algorithmic
-bytes per doc (nnz·(4+4) + 2·nnz·k·4 + 4k) × the launch's docs ÷ its HIP-event time on the library
-stream; traffic: that kernel's PMC FETCH_SIZE(×2, gfx950)+WRITE_SIZE per launch from the committed
-rocprofv3 summary of this workload (profiles/, tools/gpu_prof.sh).  roofline_compute: the same
-kernel's fp32 flops (4·nnz·k per inner iteration) against the 157.3 TF fp32 peak.
-cpu_baseline: oracle/lda_oracle.c (fp64, OpenMP, all host cores) timed on a bounded sample of the
-same docs at the same model state.
+Multi-GPU (configs[2]: "the same 1M-doc corpus sharded at 2/4/8 GPUs"): --scaling strong (default)
+gives rank r the rows [r·D/N, (r+1)·D/N) of ONE corpus (corpusSize = D); --scaling weak gives every
+rank its own D-doc corpus (corpusSize = N·D).  One RCCL all-reduce of the k×V sstats per step.
+
+Rank 0 prints ONE JSON line.  value = Σ_ranks minibatch docs in the K timed steps ÷ the
+max-over-ranks wall time.  Model state: timing starts after exactly
+--state-minibatches (20) minibatches from λ₀ (burn-in + warmup), so the inner-iteration count does
+not depend on --warmup; the first 3 minibatches from λ₀ are timed separately as the "cold" figure.
+roofline: the dominant kernel (the training E-step: k_estep_grid64 for fp64, k_estep_grid for
+fp32; one launch per minibatch): SURVEY.md §8(d) algorithmic bytes per doc
+(nnz·(4 + s) + 2·nnz·k·s + s·k, s = 8 for fp64, 4 for fp32) × the launch's docs ÷ its HIP-event time
+on the library stream; traffic: the PMC FETCH_SIZE(×2, gfx950) + WRITE_SIZE per launch of that
+kernel from the committed rocprofv3 summary of this workload (profiles/, tools/gpu_prof.sh).
+roofline_compute: the same kernel's flops (4·nnz·k per inner iteration) against the dtype's peak.
+cpu_baseline: oracle/lda_oracle.c oracle_minibatch — one full submitMiniBatch + updateLambda +
+updateAlpha in Spark's structure (fp64, per-thread dense k×V stats, OpenMP on the host cores) —
+timed on whole minibatches of the same corpus at the GPU model's state after the timed steps.
 """
 import argparse
 import json
@@ -35,8 +42,9 @@ sys.path.insert(0, os.path.join(ROOT, "spark-text-clustering_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
-FP32_PEAK_TFS = 157.3  # MI355X dense fp32 (vector v_pk_fma_f32 = MFMA f32 rate; MI355X_MICROARCH.md)
+PEAK_TFS = {"f32": 157.3, "f64": 78.6}  # MI355X dense vector peaks (fp32 = MFMA f32 rate; fp64 vector)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+METRIC = "LDA E-step docs/sec (node) at k=100, V=2^18; % of HBM roofline"
 
 
 def parse():
@@ -44,28 +52,37 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--docs", type=int, default=1_000_000, help="documents per GPU")
+    p.add_argument("--docs", type=int, default=1_000_000, help="documents of the corpus (per GPU if weak)")
     p.add_argument("--tokens", type=int, default=200)
     p.add_argument("--vocab", type=int, default=1 << 18)
     p.add_argument("--k", type=int, default=100)
     p.add_argument("--fraction", type=float, default=0.05)
     p.add_argument("--corpus", default="zipf", choices=["zipf", "zipf-lda"])
-    p.add_argument("--dtype", default="f32", choices=["f32", "f64"])
+    p.add_argument("--dtype", default="f64", choices=["f32", "f64"])
+    p.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     p.add_argument("--seed", type=int, default=20261015)
     p.add_argument("--state-minibatches", type=int, default=20,
                    help="minibatches applied from λ₀ before timing (burn-in + warmup)")
+    p.add_argument("--workers", type=int, default=16, help="corpus-generation processes (before GPU init)")
+    p.add_argument("--no-secondary", action="store_true", help="headline only (no fp32 / planted lines)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-hbm-copy", action="store_true", help="skip the torch device-copy HBM probe")
+    p.add_argument("--no-hbm-copy", action="store_true", help="skip the device-copy HBM probe")
     return p.parse_args()
 
 
-def algorithmic_bytes(nnz, k, docs):
-    """ids + counts (4+4 B per nnz), one k-wide fp32 row gathered and one
-    scattered per nnz, γ out (4k B per doc)."""
-    return nnz * 8.0 + 2.0 * nnz * k * 4.0 + docs * 4.0 * k
+def bytes_per_doc(nnz, k, s):
+    """ids + counts (4 + s B per nnz), one k-wide row gathered and one scattered per
+    nnz, γ out (s·k B per doc); s = value size (8 fp64, 4 fp32)."""
+    return nnz * (4.0 + s), 2.0 * nnz * k * s, s * k
 
 
-def pmc_traffic(a):
+def algorithmic_bytes(nnz, k, docs, dtype):
+    s = 8.0 if dtype == "f64" else 4.0
+    a, b, c = bytes_per_doc(nnz, k, s)
+    return a + b + docs * c
+
+
+def pmc_traffic(a, dtype, corpus):
     """HBM bytes per launch of the training E-step kernel from the committed PMC summary
     (tools/pmc_summary.py over tools/gpu_prof.sh's separate FETCH_SIZE / WRITE_SIZE passes), if it
     was measured on this workload; FETCH_SIZE ×2 per the gfx950 correction (MI355X_MICROARCH.md)."""
@@ -75,8 +92,8 @@ def pmc_traffic(a):
     except (OSError, ValueError):
         return None, "no PMC summary committed"
     w = pm.get("workload", {})
-    if (w.get("docs"), w.get("k"), w.get("vocab"), w.get("tokens"), w.get("fraction"), w.get("corpus")) != \
-            (a.docs, a.k, a.vocab, a.tokens, a.fraction, a.corpus):
+    if (w.get("docs"), w.get("k"), w.get("vocab"), w.get("tokens"), w.get("fraction"), w.get("corpus"),
+            w.get("dtype", "f32")) != (a.docs, a.k, a.vocab, a.tokens, a.fraction, corpus, dtype):
         return None, "PMC summary is for a different workload"
     if "estep_kernel_bytes_per_launch" not in pm:
         return None, "PMC summary predates the per-launch E-step figure"
@@ -90,7 +107,6 @@ def hbm_copy_gbs(device):
 
     try:
         hip = C.CDLL("libamdhip64.so.7")  # the runtime libstc.so links (torch/lib carries its own copy)
-        ok = (lambda r: r == 0)
         n = 1 << 30
         a, b = C.c_void_p(), C.c_void_p()
         e0, e1 = C.c_void_p(), C.c_void_p()
@@ -99,7 +115,7 @@ def hbm_copy_gbs(device):
                          ("hipMalloc", lambda: hip.hipMalloc(C.byref(a), C.c_size_t(n))),
                          ("hipMalloc", lambda: hip.hipMalloc(C.byref(b), C.c_size_t(n)))):
             r = rc()
-            if not ok(r):
+            if r != 0:
                 return f"{what} failed: {r} {hip.hipGetErrorString(r).decode()}"
         hip.hipMemset(a, 1, C.c_size_t(n))
         hip.hipEventCreate(C.byref(e0))
@@ -122,84 +138,52 @@ def hbm_copy_gbs(device):
         return f"copy probe failed: {type(e).__name__}: {e}"[:200]
 
 
-def cpu_baseline(h, corpus, k, seed, budget_s=12.0):
-    """CPU restatement of variationalTopicInference (oracle/lda_oracle.c: fp64, Spark's unscaled
-    form, OpenMP over docs) on a bounded sample of the same corpus at the GPU model's state after the
-    timed steps.  Falls back to the NumPy oracle (1 thread) if the C oracle was not built."""
+def cpu_baseline(h, corpus, a, budget_s=12.0):
+    """oracle/lda_oracle.c oracle_minibatch: whole submitMiniBatch + updateLambda + updateAlpha steps
+    (fp64, Spark's structure: per-thread dense k×V stats summed like treeReduce, OpenMP over the
+    host cores) on Bernoulli(fraction) minibatches of the same corpus, starting from the GPU model
+    after the timed steps.  Only the oracle call is timed (membership and γ₀ generation are not)."""
     from oracle import c_oracle
-    from oracle import oracle as O
 
-    lam = h.topics()                      # V×k
-    alpha = h.alpha()
-    eeb = O.topics_exp_elog_beta(lam)     # Spark's expElogβ (V×k)
-    rng = np.random.default_rng(seed)
-    order = rng.permutation(corpus.num_rows)
-    done, iters, pos = 0, 0, 0
-    if c_oracle.available():
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-        chunk = 64 * threads
-        dt = 0.0  # only the E-step call is timed (γ₀ generation is not)
-        while dt < budget_s and pos < corpus.num_rows:
-            ids = order[pos:pos + chunk]
-            g0 = np.stack([O.gamma_init(seed, int(i), k) for i in ids])
-            t1 = time.perf_counter()
-            _, _, tot = c_oracle.estep(corpus.indptr, corpus.indices, corpus.values, ids, eeb, alpha, g0,
-                                       n_threads=threads)
-            dt += time.perf_counter() - t1
-            done += ids.size
-            iters += tot
-            pos += chunk
-        return {"value": done / dt, "unit": "docs/s", "cores": threads, "kind": "port",
-                "sample": f"{done} docs of the same corpus, E-step only (variationalTopicInference), "
-                          f"model state after the timed steps; oracle/lda_oracle.c fp64 OpenMP, "
-                          f"{threads} threads; mean inner iters {iters / max(1, done):.1f}; {dt:.1f} s"}
-    t0 = time.perf_counter()
-    for i in order:
-        cid, cts = corpus.row(i)
-        _, _, it = O.variational_topic_inference(cid, cts, eeb, alpha, O.gamma_init(seed, int(i), k))
-        iters += it
-        done += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "docs/s", "cores": 1, "kind": "port",
-            "sample": f"{done} docs, E-step only, NumPy oracle/oracle.py, 1 thread; "
+    if not c_oracle.available():
+        return None
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    lam = np.ascontiguousarray(h.topics().T)  # k×V, Spark's internal orientation
+    alpha = np.ascontiguousarray(h.alpha())
+    eta = h.eta()
+    rng = np.random.default_rng(a.seed + 1)
+    D = corpus.num_rows
+    batch_size = np.ceil(a.fraction * D)
+    done = iters = steps = 0
+    dt = 0.0
+    while dt < budget_s and steps < 8:
+        ids = np.flatnonzero(rng.random(D) < a.fraction)
+        g0 = rng.gamma(100.0, 0.01, size=(ids.size, a.k))
+        rho = (1024.0 + 21 + steps) ** -0.51
+        t1 = time.perf_counter()
+        tot = c_oracle.minibatch(corpus.indptr, corpus.indices, corpus.values, ids, g0, lam, alpha, eta, rho,
+                                 D / batch_size, True, n_threads=threads)
+        dt += time.perf_counter() - t1
+        done += ids.size
+        iters += max(tot, 0)
+        steps += 1
+    return {"value": done / dt, "unit": "docs/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} whole minibatch steps ({done} docs, Bernoulli({a.fraction}) of the same corpus; "
+                      f"E-step + per-thread dense k×V stats + reduce + λ/α update, fp64) from the GPU model "
+                      f"after the timed steps; oracle/lda_oracle.c oracle_minibatch, OpenMP {threads} threads; "
                       f"mean inner iters {iters / max(1, done):.1f}; {dt:.1f} s"}
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        a.gpus = world if world > 1 else a.gpus
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # control plane only (uid exchange, barrier, max time)
-
-        dist.init_process_group("gloo")
-    import stc
-    from stc import synth
-
-    ctx = stc.Context(local)
-    if world > 1:
-        obj = [stc.Context.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        ctx.comm_init(obj[0], world, rank)
-
-    t0 = time.perf_counter()
-    corpus = synth.make_corpus(a.corpus, a.docs, a.tokens, a.vocab, a.k, a.seed + 7919 * rank)
-    gen_s = time.perf_counter() - t0
-    log = (lambda msg: print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True))  # progress on stderr
-    log(f"corpus generated in {gen_s:.1f} s")
-    dcorp = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F32 if a.dtype == "f32" else stc.STC_F64)
+def run_state(stc, ctx, dcorp, a, dtype, total, lam0, barrier, log, steps, warmup):
+    """One training run: λ₀ (random Gamma, or the given topicsMatrix), 3 timed cold minibatches,
+    burn-in + warmup to the fixed state, then exactly `steps` timed minibatches."""
     h = stc.LdaHandle(ctx, a.k, a.vocab, mini_batch_fraction=a.fraction, optimize_doc_concentration=True,
-                      seed=a.seed, dtype=a.dtype)
-    h.set_corpus(dcorp, a.docs * world)
-    h.init_random(a.seed)
-
-    # cold: the first 3 minibatches from λ₀ (random Gamma topics), timed on their own
+                      seed=a.seed, dtype=dtype)
+    h.set_corpus(dcorp, total)
+    if lam0 is None:
+        h.init_random(a.seed)
+    else:
+        h.set_topics(lam0)
     ctx.synchronize()
     cc0 = h.counters()
     t0 = time.perf_counter()
@@ -209,116 +193,193 @@ def main():
     ctx.synchronize()
     cold_s = time.perf_counter() - t0
     cc1 = h.counters()
-    cold = {"docs_per_s": (cc1["docs"] - cc0["docs"]) / cold_s,
+    cold = {"docs_per_s_rank": (cc1["docs"] - cc0["docs"]) / cold_s,
             "mean_inner_iters": (cc1["inner_iters"] - cc0["inner_iters"]) / max(1, cc1["docs"] - cc0["docs"]),
             "minibatches": n_cold}
-    burn = max(0, a.state_minibatches - n_cold - a.warmup)
-    log("cold minibatches done; burn-in + warmup")
-    for _ in range(burn + a.warmup):
+    burn = max(0, a.state_minibatches - n_cold - warmup)
+    for _ in range(burn + warmup):
         h.next(stats=False)
     ctx.synchronize()
     c0 = h.counters()
     h.enable_timing(True)
-
-    def barrier():
-        ctx.synchronize()
-        try:
-            import torch
-
-            if torch.cuda.is_available():
-                torch.cuda.synchronize()
-        except Exception:
-            pass
-        if dist is not None:
-            dist.barrier()
-
     barrier()
-    log(f"timing {a.steps} steps")
+    log(f"timing {steps} steps ({dtype})")
     t_start = time.perf_counter()
-    for _ in range(a.steps):
+    for _ in range(steps):
         h.next(stats=False)
     barrier()
     elapsed = time.perf_counter() - t_start
     phases = h.phase_times()
     c1 = h.counters()
-    docs_local = c1["docs"] - c0["docs"]
-    entries_local = c1["entries"] - c0["entries"]
-    iters_local = c1["inner_iters"] - c0["inner_iters"]
-    if dist is not None:
-        import torch
+    return h, {"elapsed": elapsed, "phases": phases, "cold": cold, "docs": c1["docs"] - c0["docs"],
+               "entries": c1["entries"] - c0["entries"], "iters": c1["inner_iters"] - c0["inner_iters"],
+               "cap_hits": c1["cap_hits"] - c0["cap_hits"]}
 
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t[0])
-        s = torch.tensor([docs_local, entries_local, iters_local], dtype=torch.float64)
-        dist.all_reduce(s)
-        docs_all, entries_all, iters_all = (float(x) for x in s)
+
+def summarize(r, a, dtype, world, steps, corpus_kind, kernel):
+    """value / roofline / roofline_compute of one run (rank-0 view of the reduced counters)."""
+    estep_ms = r["phases"]["estep"]
+    per_step_docs = r["docs_local"] / max(1, steps)
+    per_step_nnz = r["entries_local"] / max(1, steps)
+    per_step_iters = r["iters_local"] / max(1, steps)
+    alg = algorithmic_bytes(per_step_nnz, a.k, per_step_docs, dtype)
+    achieved = alg / (estep_ms * 1e-3) / 1e9
+    mean_nnz = per_step_nnz / max(1.0, per_step_docs)
+    flops = 4.0 * mean_nnz * a.k * per_step_iters
+    tflops = flops / (estep_ms * 1e-3) / 1e12
+    traffic, traffic_note = pmc_traffic(a, dtype, corpus_kind)
+    s = 8 if dtype == "f64" else 4
+    return {
+        "value": r["docs_all"] / r["elapsed"],
+        "ms_per_step": r["elapsed"] * 1e3 / steps,
+        "mean_nnz_per_doc": r["entries_all"] / max(1.0, r["docs_all"]),
+        "mean_inner_iters": r["iters_all"] / max(1.0, r["docs_all"]),
+        "cap_hits": r["cap_hits"],
+        "phase_ms": {k: round(v, 4) for k, v in r["phases"].items() if k != "steps"},
+        "estep_only_docs_per_s": per_step_docs * world / (estep_ms * 1e-3),
+        "cold": r["cold"],
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": kernel, "algorithmic_bytes_per_launch": alg,
+            "algorithmic_bytes_per_doc": f"nnz*(4+{s}) + 2*nnz*k*{s} + {s}*k",
+            "kernel_ms_per_launch": estep_ms, "traffic_source": traffic_note,
+        },
+        "roofline_compute": {
+            "bound": f"valu_{dtype}", "achieved": tflops, "peak": PEAK_TFS[dtype], "unit": "TFLOP/s",
+            "frac": tflops / PEAK_TFS[dtype], "kernel": kernel.split(" ")[0], "flops_per_launch": flops,
+            "kernel_ms_per_launch": estep_ms,
+        },
+    }
+
+
+KERNEL = {"f64": "k_estep_grid64 (lda_grid64.hip): the fp64 training E-step, one launch per minibatch",
+          "f32": "k_estep_grid (lda_grid.hip): the fp32 training E-step, one launch per minibatch"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        a.gpus = world
+    log = (lambda msg: print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True))  # progress on stderr
+    from stc import synth  # no GPU touched yet: the corpus pool may fork
+
+    # corpus shard: strong = rows [r·D/N, (r+1)·D/N) of one corpus; weak = an own D-doc corpus per rank
+    if a.scaling == "strong":
+        lo, hi, seed, total = rank * a.docs // world, (rank + 1) * a.docs // world, a.seed, a.docs
     else:
-        docs_all, entries_all, iters_all = float(docs_local), float(entries_local), float(iters_local)
+        lo, hi, seed, total = 0, a.docs, a.seed + 7919 * rank, a.docs * world
+    workers = max(1, min(a.workers, (os.cpu_count() or 1)) // max(1, world))
+    t0 = time.perf_counter()
+    corpus = synth.make_corpus(a.corpus, a.docs, a.tokens, a.vocab, a.k, seed, lo, hi, workers)
+    gen_s = time.perf_counter() - t0
+    log(f"corpus rows [{lo}, {hi}) generated in {gen_s:.1f} s")
+    secondary = world == 1 and not a.no_secondary
+    planted = None
+    if secondary:
+        t0 = time.perf_counter()
+        planted = (synth.zipf_lda_corpus(a.docs, a.tokens, a.vocab, a.k, seed=a.seed + 1, workers=workers),
+                   synth.planted_topics(a.vocab, a.k, seed=a.seed + 1))
+        log(f"planted-topic corpus generated in {time.perf_counter() - t0:.1f} s")
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only (uid exchange, barrier, max time)
+
+        dist.init_process_group("gloo")
+    import stc
+
+    ctx = stc.Context(local)
+    if world > 1:
+        obj = [stc.Context.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ctx.comm_init(obj[0], world, rank)
+
+    def barrier():
+        ctx.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    def reduce_run(r):
+        el, d, e, it = r["elapsed"], float(r["docs"]), float(r["entries"]), float(r["iters"])
+        if dist is not None:
+            import torch
+
+            t = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            s = torch.tensor([d, e, it], dtype=torch.float64)
+            dist.all_reduce(s)
+            el, (d, e, it) = float(t[0]), (float(x) for x in s)
+        r.update(elapsed=el, docs_local=r["docs"], entries_local=r["entries"], iters_local=r["iters"],
+                 docs_all=d, entries_all=e, iters_all=it)
+        return r
+
+    DT = {"f32": stc.STC_F32, "f64": stc.STC_F64}
+    dcorp = {a.dtype: stc.DeviceCsr.upload(ctx, corpus, DT[a.dtype])}
+    h, r = run_state(stc, ctx, dcorp[a.dtype], a, a.dtype, total, None, barrier, log, a.steps, a.warmup)
+    head = summarize(reduce_run(r), a, a.dtype, world, a.steps, a.corpus, KERNEL[a.dtype])
+
+    lines = []
+    if secondary:
+        other = "f32" if a.dtype == "f64" else "f64"
+        dcorp[other] = stc.DeviceCsr.upload(ctx, corpus, DT[other])
+        _, r2 = run_state(stc, ctx, dcorp[other], a, other, total, None, barrier, log, a.steps, a.warmup)
+        s2 = summarize(reduce_run(r2), a, other, world, a.steps, a.corpus, KERNEL[other])
+        lines.append(dict(label=f"{other} E-step, same corpus and model state", dtype=other, corpus=a.corpus, **s2))
+        pc, lam_p = planted
+        for dt in (a.dtype, other):
+            dp = stc.DeviceCsr.upload(ctx, pc, DT[dt])
+            _, r3 = run_state(stc, ctx, dp, a, dt, a.docs, lam_p, barrier, log, a.steps, a.warmup)
+            s3 = summarize(reduce_run(r3), a, dt, world, a.steps, "zipf-lda", KERNEL[dt])
+            lines.append(dict(label=f"{dt} E-step, planted-topic corpus at the planted model (SURVEY §8(d) state B)",
+                              dtype=dt, corpus="zipf-lda", **s3))
+            dp.free()
+        dcorp[other].free()
 
     if rank != 0:
         if dist is not None:
             dist.barrier()
         return
-
-    value = docs_all / elapsed
-    # roofline of the dominant kernel: the training E-step (k_estep_grid), ONE launch per minibatch;
-    # SURVEY.md §8(d)'s bytes per doc × the docs of a launch ÷ its HIP-event time on the library stream
-    estep_ms = phases["estep"]
-    per_step_docs = docs_local / max(1, a.steps)
-    per_step_nnz = entries_local / max(1, a.steps)
-    per_step_iters = iters_local / max(1, a.steps)
-    alg = algorithmic_bytes(per_step_nnz, a.k, per_step_docs)
-    achieved = alg / (estep_ms * 1e-3) / 1e9
-    # E-step kernel flops: φ = B·eθ and Bᵀr, 2 FMAs per (entry, topic) per inner iteration
-    mean_nnz = per_step_nnz / max(1.0, per_step_docs)
-    flops = 4.0 * mean_nnz * a.k * per_step_iters
-    tflops = flops / (estep_ms * 1e-3) / 1e12
-    traffic, traffic_note = pmc_traffic(a)
     copy_gbs = None if a.no_hbm_copy else hbm_copy_gbs(local)
     cpu = None
-    if not a.no_cpu_baseline:
-        cpu = cpu_baseline(h, corpus, a.k, a.seed)
+    if not a.no_cpu_baseline and world == 1:
+        log("cpu baseline")
+        cpu = cpu_baseline(h, corpus, a)
+    roof = dict(head["roofline"], hbm_copy_measured_GBs=copy_gbs,
+                note="the E-step iterates a register-resident block (~150 fixed-point iterations per doc at this "
+                     "state), so it is VALU-bound and the HBM fraction is small by construction; see "
+                     "roofline_compute and the planted-state secondary line")
     line = {
-        "metric": "LDA E-step docs/sec (node) at k=100, V=2^18; % of HBM roofline",
-        "value": value,
+        "metric": METRIC,
+        "value": head["value"],
         "unit": "docs/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": elapsed * 1e3 / a.steps,
+        "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": a.scaling,
         "vs_baseline": None,
         "dtype": a.dtype,
         "data": f"synthetic {a.corpus} corpus (seeded, generated in {gen_s:.0f} s), resident in HBM",
         "config": {
-            "workload": f"online LDA minibatch steps: {a.docs} docs x {a.tokens} tokens per GPU, "
-                        f"V={a.vocab}, k={a.k}, subsamplingRate={a.fraction}",
-            "docs_per_gpu": a.docs, "tokens_per_doc": a.tokens, "vocab": a.vocab, "k": a.k,
+            "workload": f"online LDA minibatch steps: {a.docs} docs x {a.tokens} tokens"
+                        f"{' per GPU' if a.scaling == 'weak' else ' sharded over the GPUs'}, V={a.vocab}, k={a.k}, "
+                        f"subsamplingRate={a.fraction}",
+            "docs": a.docs, "tokens_per_doc": a.tokens, "vocab": a.vocab, "k": a.k,
             "subsampling_rate": a.fraction, "corpus": a.corpus, "parallelism": f"dp{world}",
-            "mean_nnz_per_doc": entries_all / max(1.0, docs_all),
-            "mean_inner_iters": iters_all / max(1.0, docs_all),
+            "mean_nnz_per_doc": head["mean_nnz_per_doc"], "mean_inner_iters": head["mean_inner_iters"],
             "model_state": f"after {a.state_minibatches} minibatches from lambda0 (Gamma(100,1/100))",
-            "cold": cold,
-            "phase_ms": {k: round(v, 4) for k, v in phases.items() if k != "steps"},
-            "estep_only_docs_per_s": per_step_docs * world / (estep_ms * 1e-3),
+            "cold": head["cold"], "phase_ms": head["phase_ms"],
+            "estep_only_docs_per_s": head["estep_only_docs_per_s"], "cap_hits": head["cap_hits"],
         },
-        "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "k_estep_grid (lda_grid.hip): the training E-step, one launch per minibatch",
-            "algorithmic_bytes_per_launch": alg, "kernel_ms_per_launch": estep_ms,
-            "traffic_source": traffic_note, "hbm_copy_measured_GBs": copy_gbs,
-            "note": "the E-step is VALU-bound (~150 fixed-point iterations per doc over a register-resident "
-                    "block), so the HBM fraction is small by construction; see roofline_compute",
-        },
-        "roofline_compute": {
-            "bound": "valu_fp32", "achieved": tflops, "peak": FP32_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": tflops / FP32_PEAK_TFS, "kernel": "k_estep_grid", "flops_per_launch": flops,
-            "kernel_ms_per_launch": estep_ms,
-        },
+        "roofline": roof,
+        "roofline_compute": head["roofline_compute"],
         "cpu_baseline": cpu,
+        "secondary": lines,
     }
     print(json.dumps(line), flush=True)
     if dist is not None:

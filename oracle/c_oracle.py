@@ -16,7 +16,30 @@ def lib():
         _LIB.oracle_estep.argtypes = [C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                       C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
         _LIB.oracle_max_threads.restype = C.c_int
+        _LIB.oracle_minibatch.restype = C.c_int64
+        _LIB.oracle_minibatch.argtypes = [C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_double, C.c_double,
+                                          C.c_double, C.c_int, C.c_int]
     return _LIB
+
+
+def minibatch(indptr, indices, values, doc_ids, gamma0, lam_kv, alpha, eta, rho, scale, optimize_alpha=True,
+              n_threads=0):
+    """One submitMiniBatch + updateLambda (+ updateAlpha) in Spark's structure (per-thread dense k×V
+    stats summed like treeReduce).  lam_kv (k×V, float64, C order) and alpha are updated IN PLACE.
+    Returns Σ inner iterations (−1 when the batch had no non-empty document)."""
+    indptr = np.ascontiguousarray(indptr, np.int64)
+    indices = np.ascontiguousarray(indices, np.int32)
+    values = np.ascontiguousarray(values, np.float64)
+    ids = np.ascontiguousarray(doc_ids, np.int64)
+    g0 = np.ascontiguousarray(gamma0, np.float64)
+    assert lam_kv.dtype == np.float64 and lam_kv.flags["C_CONTIGUOUS"]
+    assert alpha.dtype == np.float64 and alpha.flags["C_CONTIGUOUS"]
+    k, V = lam_kv.shape
+    return int(lib().oracle_minibatch(ids.size, indptr.ctypes.data, indices.ctypes.data, values.ctypes.data,
+                                      ids.ctypes.data, g0.ctypes.data, k, V, lam_kv.ctypes.data,
+                                      alpha.ctypes.data, float(eta), float(rho), float(scale),
+                                      int(bool(optimize_alpha)), int(n_threads)))
 
 
 def available():

@@ -45,3 +45,28 @@ def test_c_oracle_reference_books(co, oracle):
     p = g / g.sum(axis=1, keepdims=True)
     exp = np.array([[float(x) for x in r] for r in meta["Result_EN_1591723228815"]])
     assert np.abs(p - exp).max() < 1e-6
+
+
+@pytest.mark.parametrize("optimize_alpha", [True, False])
+def test_c_oracle_minibatch_matches_numpy_oracle(co, oracle, optimize_alpha):
+    """oracle_minibatch (the bench's full-step CPU baseline) = submit_minibatch of the NumPy oracle."""
+    rng = np.random.default_rng(1)
+    D, V, k = 60, 500, 8
+    c = random_corpus(rng, D, V, 1, 40, empty_every=7)
+    lam0 = rng.gamma(100, 0.01, size=(V, k))
+    ids = np.sort(rng.choice(D, size=25, replace=True))
+    g0 = rng.gamma(100, 0.01, size=(ids.size, k))
+    alpha, eta = oracle.resolve_alpha_eta(k)
+    st = oracle.OnlineLDAState(lam=lam0.T.copy(), alpha=alpha.copy(), eta=eta, corpus_size=D,
+                               mini_batch_fraction=0.4, optimize_doc_concentration=optimize_alpha)
+    st.iteration = 4
+    oracle.submit_minibatch(st, [c.row(i) for i in ids], list(g0))
+    lam = np.ascontiguousarray(lam0.T)
+    a = alpha.copy()
+    rho = (1024.0 + 5) ** -0.51
+    scale = D / np.ceil(0.4 * D)
+    tot = co.minibatch(c.indptr, c.indices, c.values, ids, g0, lam, a, eta, rho, scale, optimize_alpha,
+                       n_threads=4)
+    assert tot > 0
+    np.testing.assert_allclose(lam, st.lam, rtol=1e-12)
+    np.testing.assert_allclose(a, st.alpha, rtol=1e-12)

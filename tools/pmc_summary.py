@@ -27,7 +27,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # kernels of the E-step phase (the bench roofline's "kernel"): E-step, term sort, sstats SpMM,
 # the stat memset, and the partition scans (rocprim; tiny)
 PHASE = re.compile(r"k_estep|k_sstats|k_fixup|rocprim|fillBuffer|k_part_|k_fill_batch|k_batch_nnz")
-# the dominant kernel (bench.py's roofline): the training E-step launches (STATS variant), one per minibatch
+# the dominant kernel (bench.py's roofline): the training E-step launches (STATS variant), one per
+# minibatch — the grid kernel plus the workgroup kernel for the few docs past its row capacity, the
+# same launches the bench's HIP-event "estep" phase brackets
 ESTEP = re.compile(r"k_estep\w*<.*true, false>")
 
 
@@ -55,6 +57,7 @@ def main():
     p.add_argument("--k", type=int, default=100)
     p.add_argument("--fraction", type=float, default=0.05)
     p.add_argument("--corpus", default="zipf")
+    p.add_argument("--dtype", default="f64")
     p.add_argument("--tag", default="r01")
     a = p.parse_args()
     d = a.prof_dir
@@ -94,7 +97,7 @@ def main():
     est_bytes = sum((v["fetch_bytes_x2_per_dispatch"] + v["write_bytes_per_dispatch"]) * v["dispatches"]
                     for v in est.values()) / max(1, est_launches)
     wl = {"docs": a.docs, "tokens": a.tokens, "vocab": a.vocab, "k": a.k, "fraction": a.fraction,
-          "corpus": a.corpus}
+          "corpus": a.corpus, "dtype": a.dtype}
     detail = {"workload": wl, "minibatches_in_run": steps, "kernels": kernels, "sq_per_dispatch": sq,
               "estep_phase_bytes_per_step": per_step, "estep_kernel": sorted(est),
               "estep_kernel_bytes_per_launch": est_bytes}
