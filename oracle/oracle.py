@@ -131,10 +131,33 @@ def java_split_whitespace(s: str):
     return pieces
 
 
+# Spark 2.4.3 runs on Java 8 (Unicode 6.2): code points assigned later are unassigned there and
+# toLowerCase leaves them alone; Python's newer database lower-cases these (the ones below are the
+# cased additions in U+0000–U+07FF, the range the GPU kernel maps).  Case pairs are otherwise stable
+# across Unicode versions, and String.toLowerCase(Locale.ROOT)'s special casings (U+0130 → "i̇",
+# Final_Sigma for U+03A3) are Python's str.lower too.
+_JAVA8_UNASSIGNED = frozenset([0x37F] + list(range(0x528, 0x530)))
+
+
+def java_lower(text: str) -> str:
+    """[U] java.lang.String.toLowerCase(Locale.ROOT) on Java 8, restated with str.lower."""
+    if not any(ord(ch) in _JAVA8_UNASSIGNED for ch in text):
+        return text.lower()
+    out, seg = [], []
+    for ch in text:
+        if ord(ch) in _JAVA8_UNASSIGNED:
+            out.append("".join(seg).lower())
+            out.append(ch)
+            seg = []
+        else:
+            seg.append(ch)
+    out.append("".join(seg).lower())
+    return "".join(out)
+
+
 def tokenize(text: str):
-    """[U] Tokenizer: lower-case then split.  Python's str.lower agrees with Java's
-    toLowerCase(Locale.ROOT) on the ASCII/Latin-1 range the GPU kernel supports."""
-    return java_split_whitespace(text.lower())
+    """[U] Tokenizer: ``text.toLowerCase.split("\\s")`` (Java 8 lower-casing, Java split)."""
+    return java_split_whitespace(java_lower(text))
 
 
 def hashing_tf(docs, num_features=1 << 18, binary=False, variant=HASH_STANDARD):

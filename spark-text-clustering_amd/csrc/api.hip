@@ -803,8 +803,9 @@ void run_tokenizer(Ctx& c, Tokens& t, const uint8_t* text, int64_t n_bytes, cons
                       t.n_tok, t.n_bytes, bad);
   if (bad >= 0) {
     char msg[160];
-    snprintf(msg, sizeof msg, "Tokenizer: the GPU lower-casing covers ASCII, Latin-1 and caseless blocks only; "
-             "unsupported character at byte %lld (lead byte 0x%02X)", (long long)bad, (unsigned)text[bad]);
+    snprintf(msg, sizeof msg, "Tokenizer: the GPU lower-casing covers U+0000-U+07FF (except U+0130, U+03A3, "
+             "U+023A, U+023E) and caseless blocks; unsupported character at byte %lld (lead byte 0x%02X)",
+             (long long)bad, (unsigned)text[bad]);
     throw Error(STC_ERR_INVALID_ARG, msg);
   }
 }

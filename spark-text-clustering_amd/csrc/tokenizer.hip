@@ -7,12 +7,15 @@
 // limit 0), and return the whole string as one token when it holds no separator ("" → [""]).
 // The reference's own CoreNLP/OpenNLP front-end (LDAClustering.scala:116-139) stays out of scope.
 //
-// Lower-casing: ASCII and Latin-1 (U+00C0–U+00DE except U+00D7, the German/French/… capitals)
-// are mapped exactly as Java's String.toLowerCase (root/English locale) maps them; both keep the
-// UTF-8 length.  Code points whose case mapping needs tables this kernel does not carry (Latin
-// Extended, Greek, Cyrillic, fullwidth, …) are REJECTED loudly (STC_ERR_INVALID_ARG with the byte
-// position); caseless blocks that real text carries are accepted: U+0080–U+00FF, U+2000–U+20BF
-// (punctuation, quotes, dashes, currency), U+3000–U+9FFF (CJK), U+1F000–U+1FFFF (emoji).
+// Lower-casing as Java 8's String.toLowerCase (root locale) — the JVM Spark 2.4.3 runs on — for every
+// code point with a two-byte or shorter UTF-8 form: ASCII, Latin-1 (U+00C0–U+00DE except ×) and,
+// through the generated table case_table.h, U+0100–U+07FF (Latin Extended-A/B, IPA, Greek and Coptic,
+// Cyrillic + Supplement, Armenian, and the caseless Hebrew/Arabic/Syriac/Thaana/NKo blocks).  All of
+// these keep the UTF-8 length, so output byte i is a function of input bytes i−1, i, i+1.  Characters
+// whose Java mapping is not such a map (U+0130 İ, U+03A3 Σ with its Final_Sigma context rule, U+023A,
+// U+023E) and three-byte/four-byte code points outside the caseless blocks U+2000–U+20BF (punctuation,
+// quotes, dashes, currency), U+3000–U+9FFF (CJK) and U+1F000–U+1FFFF (emoji) are REJECTED loudly
+// (STC_ERR_INVALID_ARG with the byte position), never silently mis-cased.
 //
 // Layout: in = one UTF-8 blob + int64 text offsets per document.  Out = the lower-cased blob with
 // the separator bytes removed, so token t is the contiguous out[tok_off[t] .. tok_off[t+1]) and
@@ -23,6 +26,7 @@
 // HBM-bound: 2 reads + 1 write of the blob.
 #include <hipcub/hipcub.hpp>
 
+#include "case_table.h"
 #include "stc_internal.h"
 
 namespace stc {
@@ -34,18 +38,26 @@ __device__ __forceinline__ bool is_java_space(uint32_t b) {
   return b == 0x20u || (b >= 0x09u && b <= 0x0Du);  // \t \n \x0B \f \r and ' '
 }
 
+// the two-byte code point whose lead byte is b (0xC4–0xDF) and continuation byte c
+__device__ __forceinline__ uint32_t cp2(uint32_t b, uint32_t c) { return ((b & 0x1Fu) << 6) | (c & 0x3Fu); }
+
 // true when the UTF-8 lead byte `b` (followed by `nx`) starts a code point outside the supported set
 __device__ __forceinline__ bool unsupported(uint32_t b, uint32_t nx) {
   if (b < 0xC4u) return false;                           // ASCII, continuation, U+0080–U+00FF
+  if (b <= 0xDFu) return kLower2[cp2(b, nx) - kCaseLo] == 0;  // U+0100–U+07FF: the table's rejects
   if (b == 0xE2u) return nx < 0x80u || nx > 0x82u;       // U+2000–U+20BF only
   if (b >= 0xE3u && b <= 0xE9u) return false;            // U+3000–U+9FFF
   if (b == 0xF0u) return nx != 0x9Fu;                    // U+1F000–U+1FFFF only
   return true;
 }
 
-__device__ __forceinline__ uint32_t to_lower(uint32_t b, uint32_t prev) {
+// output byte for input byte b between prev and nx (same-length mappings only, see the header)
+__device__ __forceinline__ uint32_t to_lower(uint32_t b, uint32_t prev, uint32_t nx) {
   if (b >= 0x41u && b <= 0x5Au) return b + 0x20u;                                // A–Z
   if (prev == 0xC3u && b >= 0x80u && b <= 0x9Eu && b != 0x97u) return b + 0x20u;  // À–Þ except ×
+  if (b >= 0xC4u && b <= 0xDFu) return 0xC0u | (kLower2[cp2(b, nx) - kCaseLo] >> 6);       // lead byte
+  if (prev >= 0xC4u && prev <= 0xDFu && (b & 0xC0u) == 0x80u)                                // its tail
+    return 0x80u | (kLower2[cp2(prev, b) - kCaseLo] & 0x3Fu);
   return b;
 }
 
@@ -119,11 +131,12 @@ __global__ __launch_bounds__(64 * kWaves) void k_emit(const uint8_t* __restrict_
       const bool in = i < e;
       const uint32_t b = in ? text[i] : 0x20u;
       const uint32_t prev = (in && i > s) ? text[i - 1] : 0u;
+      const uint32_t nx = (in && i + 1 < e) ? text[i + 1] : 0x80u;  // (validated by k_count)
       const bool sep = is_java_space(b);
       const uint64_t sm = __ballot(in && sep);
       const int64_t j = seps + lanes_below(sm, lane);  // separators before byte i in this doc
       if (in) {
-        if (!sep) out[base + (i - s) - j] = (uint8_t)to_lower(b, prev);
+        if (!sep) out[base + (i - s) - j] = (uint8_t)to_lower(b, prev, nx);
         else if (j + 1 < nt) tok_off[tb + j + 1] = base + (i - s) - j;
       }
       seps += __popcll(sm);

@@ -24,6 +24,7 @@ F3 ``en_topicdist.json`` — LocalLDAModel.topicDistribution known answers: the 
     topic proportions printed by LDALoader.scala:108-135 in both Result files (two
     independent runs: their spread is the fixture's noise floor).
 F4 metadata (α, η, k, gammaShape) from ``metadata/part-00000`` is copied into the json.
+F5 ``en_vocab.txt`` and F6 ``books_text.json`` — see make_vocab / make_text_samples.
 """
 import glob
 import json
@@ -166,9 +167,56 @@ def make_en_model_fixtures(indptr, indices, tf, meta):
     print("describe/topicdist fixtures written")
 
 
+def make_vocab():
+    """F5 ``en_vocab.txt`` — the EN model's vocabulary (vocabArray, index = term id, one per line), the
+    strings behind en_idf.npz's term ids: the config-1 pipeline test hashes them (HashingTF)."""
+    model = "LdaModel_EN_1591049082850"
+    vocab = open(os.path.join(REF, "models", "vocabularies", model), encoding="utf-8").read().split(",")
+    assert all("\n" not in w for w in vocab)
+    with open(os.path.join(OUT, "en_vocab.txt"), "w", encoding="utf-8") as f:
+        f.write("\n".join(vocab) + "\n")
+    print(f"en_vocab.txt: {len(vocab)} terms")
+
+
+def _kernel_supported(ch):
+    """The tokenizer kernel's accepted set (tokenizer.hip header): U+0000–U+07FF except the four
+    rejected capitals, and the caseless blocks U+2000–U+20BF, U+3000–U+9FFF, U+1F000–U+1FFFF."""
+    o = ord(ch)
+    if o < 0x800:
+        return o not in (0x130, 0x3A3, 0x23A, 0x23E)
+    return 0x2000 <= o <= 0x20BF or 0x3000 <= o <= 0x9FFF or 0x1F000 <= o <= 0x1FFFF
+
+
+def make_text_samples(per_lang=3, width=2500):
+    """F6 ``books_text.json`` — raw text slices of the reference's own corpora (resources/books/<Lang>,
+    three books per language, ``width`` characters from a third of the way in, moved forward past any
+    character the GPU tokenizer rejects): the Cyrillic (Russian, Ukrainian) and Latin-script inputs
+    of the tokenizer's lower-casing tests."""
+    out = {}
+    base = os.path.join(REF, "books")
+    for lang in sorted(os.listdir(base)):
+        books = sorted(os.listdir(os.path.join(base, lang)))[:per_lang]
+        samples = []
+        for b in books:
+            t = open(os.path.join(base, lang, b), encoding="utf-8").read()
+            p = len(t) // 3
+            while p + width < len(t) and not all(_kernel_supported(c) for c in t[p:p + width]):
+                p += 97
+            samples.append({"book": b, "offset": p, "text": t[p:p + width]})
+        out[lang] = samples
+    json.dump(out, open(os.path.join(OUT, "books_text.json"), "w", encoding="utf-8"), ensure_ascii=False, indent=0)
+    print("books_text.json:", {k: len(v) for k, v in out.items()})
+
+
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit("reference not present: fixtures are generated only in the build container")
+    if sys.argv[1:] == ["--text"]:  # the F5/F6 fixtures only (the npz files stay byte-identical)
+        make_vocab()
+        make_text_samples()
+        sys.exit(0)
     ip, ix, tf, meta = make_idf("LdaModel_EN_1591049082850", "en")
     make_idf("LdaModel_GE_1591070442475", "ge")
     make_en_model_fixtures(ip, ix, tf, meta)
+    make_vocab()
+    make_text_samples()

@@ -9,7 +9,8 @@ from test_tokenizer_oracle import JAVA_SPLIT_KNOWN
 pytestmark = pytest.mark.gpu
 
 _ALPHABET = list("abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789.,;'\"-") + \
-    ["Ä", "Ö", "Ü", "ß", "é", "È", "Ç", "×", "Þ", "µ", "\u00a0", "—", "“", "”", "€", "漢", "字", "😀"]
+    ["Ä", "Ö", "Ü", "ß", "é", "È", "Ç", "×", "Þ", "µ", "\u00a0", "—", "“", "”", "€", "漢", "字", "😀",
+     "Ж", "ж", "Ё", "Ї", "Ґ", "Ω", "ς", "Ğ", "Ł", "Ŋ", "Ǆ", "ǅ", "Ա", "Ͳ", "Ϳ", "Ԩ", "\u0301", "א", "ب"]
 _SPACES = [" ", " ", " ", "\t", "\n", "\x0b", "\f", "\r"]
 
 
@@ -48,12 +49,47 @@ def test_random_texts_bit_exact(ctx, oracle, n, max_len):
 
 
 def test_unsupported_case_mapping_fails_loudly(ctx):
+    """Characters whose Java mapping is not a same-length 1:1 map (İ → "i̇", Σ's Final_Sigma rule,
+    Ⱥ → U+2C65), and cased blocks past U+07FF (fullwidth, Greek Extended), raise — never mis-cased."""
     import stc
 
     tok = stc.Tokenizer(ctx=ctx)
-    for bad in ["İstanbul", "ĞÜZEL", "Ωmega", "Москва", "ＡＢＣ"]:
+    for bad in ["İstanbul", "ΣΟΦΙΑ", "Ⱥx", "ＡＢＣ", "Ἀθῆναι"]:
         with pytest.raises(ValueError, match="Tokenizer"):
             tok.transform(["fine text", bad])
+
+
+def test_two_byte_scripts_lower_cased(ctx, oracle):
+    """Cyrillic, Greek, Latin Extended-A/B and Armenian capitals follow Java 8's toLowerCase."""
+    import stc
+
+    texts = ["Москва ПРИВЕТ Ёлка", "ЇЖАК Ґанок", "ΑΘΗΝΑ Ωμέγα", "ĞÜZEL ŁÓDŹ ǄEMAL Ǆ", "ԱՐԱՐԱՏ",
+             "Ϳ Ԩ Ԯ", "Źdźbło\tŻÓŁW"]
+    got = stc.Tokenizer(ctx=ctx).transform(texts)
+    assert got == [oracle.tokenize(t) for t in texts]
+    assert got[0] == ["москва", "привет", "ёлка"] and got[2] == ["αθηνα", "ωμέγα"]
+    assert got[5] == ["Ϳ", "Ԩ", "Ԯ"]  # assigned after Unicode 6.2: Java 8 leaves them as they are
+
+
+def test_reference_books_bit_exact(ctx, oracle):
+    """Text of the reference's own corpora (resources/books/<Lang>, tests/golden/books_text.json):
+    Russian and Ukrainian (Cyrillic) and the five Latin-script languages, tokens bit-exact."""
+    import stc
+    from helpers import golden_json
+
+    books = golden_json("books_text.json")
+    texts = [s["text"] for lang in sorted(books) for s in books[lang]]
+    assert any("\u0400" <= ch <= "\u04ff" for ch in "".join(texts))
+    got = stc.Tokenizer(ctx=ctx).transform(texts)
+    assert got == [oracle.tokenize(t) for t in texts]
+    htf = stc.HashingTF(ctx=ctx)  # Spark 2.4.3's tail
+    d = htf.transform_text_device(texts)
+    try:
+        m = d.download()
+    finally:
+        d.free()
+    ip, ix, vv = oracle.hashing_tf([oracle.tokenize(t) for t in texts], 1 << 18, False, oracle.HASH_SPARK24)
+    assert np.array_equal(m.indptr, ip) and np.array_equal(m.indices, ix) and np.array_equal(m.values, vv)
 
 
 @pytest.mark.parametrize("binary", [False, True])
