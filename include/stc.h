@@ -129,8 +129,9 @@ int stc_hash_tokens(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const in
  * tokens kept, trailing empty tokens dropped, a separator-free string is one token ("" → [""]) —
  * laid out as stc_hashing_tf's input: the separator-free lower-cased blob utf8_out (capacity
  * n_bytes), tok_off_out (capacity n_bytes + n_docs + 1) and doc_off_out[n_docs+1].
- * Lower-casing covers ASCII and Latin-1; a character that needs other case tables fails with
- * STC_ERR_INVALID_ARG (caseless punctuation/CJK/emoji blocks pass through).                 */
+ * Lower-casing is Java 8's String.toLowerCase (root locale) for every code point up to U+07FF
+ * (Latin, Greek, Cyrillic, Armenian, …); U+0130, U+03A3, U+023A, U+023E and cased characters past
+ * U+07FF fail with STC_ERR_INVALID_ARG (caseless punctuation/CJK/emoji blocks pass through).   */
 int stc_tokenize(stc_ctx* ctx, const uint8_t* text, int64_t n_bytes, const int64_t* text_off,
                  int64_t n_docs, uint8_t* utf8_out, int64_t* n_out_bytes, int64_t* tok_off_out,
                  int64_t* n_tok_out, int64_t* doc_off_out);
@@ -164,7 +165,7 @@ typedef struct stc_lda_config {
   int32_t optimize_doc_concentration; /* ml.LDA default 1, mllib default 0 */
   int32_t sample_with_replacement;    /* mllib default 1 */
   uint64_t seed;                 /* λ₀ / membership / γ₀ counter-RNG seed */
-  int32_t dtype;                 /* STC_F32 (default, fp32 E-step) or STC_F64 */
+  int32_t dtype;                 /* STC_F64 (default: Spark's Double E-step) or STC_F32 */
   int32_t max_inner_iter;        /* E-step safety cap (upstream has none); 0 ⇒ 100000 */
 } stc_lda_config;
 

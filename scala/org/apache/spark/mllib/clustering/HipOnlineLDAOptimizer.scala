@@ -1,0 +1,136 @@
+package org.apache.spark.mllib.clustering
+
+import org.apache.spark.mllib.linalg.{Matrices, Vector, Vectors}
+import org.apache.spark.rdd.RDD
+
+/**
+ * OnlineLDAOptimizer whose whole next() — minibatch sampling, the variationalTopicInference E-step,
+ * the sufficient statistics, updateLambda / expElogβ and updateAlpha — runs on MI355X through
+ * libstc.so (StcNative → jni/stcjni.c → include/stc.h).  Spark's own optimizer is
+ * [U] spark-mllib 2.4.3 OnlineLDAOptimizer (TextClustering/build.sbt:10).
+ *
+ * Drop-in at the reference's optimizer switch (TextClustering/src/main/scala/LDAClustering.scala:40-46):
+ * {{{
+ *   case "hip-online" => new HipOnlineLDAOptimizer().setMiniBatchFraction(0.05 + 1.0 / actualCorpusSize)
+ * }}}
+ * Everything else in the file stays: `lda.setOptimizer(optimizer).setK(..)...` (:49-54) and
+ * `lda.run(corpus)` (:61), which calls initialize / next × maxIterations / getLDAModel below.
+ * LDAOptimizer's three methods are private[clustering]; Scala package-private compiles to public
+ * bytecode, so this class works from the application jar in this package.
+ *
+ * Defaults and setters are OnlineLDAOptimizer's (tau0 1024, kappa 0.51, miniBatchFraction 0.05,
+ * optimizeDocConcentration false, gammaShape 100, sampleWithReplacement true); α/η resolution
+ * (−1 ⇒ 1/k) happens in stc_lda_create exactly as OnlineLDAOptimizer.initialize does it.  The
+ * E-step computes in Double like Breeze (setDtype("f32") selects the fp32 kernels).
+ *
+ * Layout: the reference runs Spark local[*] (LDATraining.scala:7), one JVM: initialize collects the
+ * corpus once into CSR arrays and uploads it to the GPU, where it stays for every next().  In a
+ * multi-executor deployment each executor owns one GPU and a partition: rank 0's
+ * StcNative.commUniqueId is broadcast, every executor calls commInit, uploads its partition and
+ * passes the global corpus size to ldaSetCorpus — stc_lda_next then all-reduces the sstats over RCCL.
+ */
+final class HipOnlineLDAOptimizer extends LDAOptimizer {
+  private var tau0: Double = 1024
+  private var kappa: Double = 0.51
+  private var miniBatchFraction: Double = 0.05
+  private var optimizeDocConcentration: Boolean = false
+  private var gammaShape: Double = 100
+  private var sampleWithReplacement: Boolean = true
+  private var dtype: Int = StcNative.F64
+  private var device: Int = 0
+
+  private var ctx: Long = 0L
+  private var corpus: Long = 0L
+  private var handle: Long = 0L
+  private var k: Int = 0
+  private var vocabSize: Int = 0
+
+  def getTau0: Double = tau0
+  def setTau0(tau0: Double): this.type = {
+    require(tau0 > 0, s"LDA tau0 must be positive, but was set to $tau0")
+    this.tau0 = tau0
+    this
+  }
+
+  def getKappa: Double = kappa
+  def setKappa(kappa: Double): this.type = {
+    require(kappa >= 0, s"Online LDA kappa must be nonnegative, but was set to $kappa")
+    this.kappa = kappa
+    this
+  }
+
+  def getMiniBatchFraction: Double = miniBatchFraction
+  def setMiniBatchFraction(miniBatchFraction: Double): this.type = {
+    require(miniBatchFraction > 0.0 && miniBatchFraction <= 1.0,
+      s"Online LDA miniBatchFraction must be in range (0,1], but was set to $miniBatchFraction")
+    this.miniBatchFraction = miniBatchFraction
+    this
+  }
+
+  def getOptimizeDocConcentration: Boolean = optimizeDocConcentration
+  def setOptimizeDocConcentration(optimizeDocConcentration: Boolean): this.type = {
+    this.optimizeDocConcentration = optimizeDocConcentration
+    this
+  }
+
+  def getGammaShape: Double = gammaShape
+  def setGammaShape(gammaShape: Double): this.type = { this.gammaShape = gammaShape; this }
+
+  def setSampleWithReplacement(b: Boolean): this.type = { this.sampleWithReplacement = b; this }
+
+  /** "f64" (default, Spark's Double arithmetic) or "f32" */
+  def setDtype(d: String): this.type = {
+    dtype = d.toLowerCase match {
+      case "f64" | "double" => StcNative.F64
+      case "f32" | "float" => StcNative.F32
+      case other => throw new IllegalArgumentException(s"dtype must be f64 or f32 but got $other")
+    }
+    this
+  }
+
+  def setDevice(d: Int): this.type = { device = d; this }
+
+  override private[clustering] def initialize(docs: RDD[(Long, Vector)], lda: LDA): HipOnlineLDAOptimizer = {
+    k = lda.getK
+    vocabSize = docs.first()._2.size
+    val alpha = lda.getAsymmetricDocConcentration.toArray  // length 1 (−1 ⇒ 1/k) or k, resolved in C
+    val rows = docs.sortByKey().values.collect()
+    val csr = StcNative.toCsr(rows)
+    ctx = StcNative.init(device)
+    corpus = StcNative.dcsrUpload(ctx, rows.length, vocabSize, csr(0).asInstanceOf[Array[Long]],
+      csr(1).asInstanceOf[Array[Int]], csr(2).asInstanceOf[Array[Double]], dtype)
+    handle = StcNative.ldaCreate(ctx, k, vocabSize, alpha, lda.getTopicConcentration, tau0, kappa,
+      miniBatchFraction, gammaShape, optimizeDocConcentration, sampleWithReplacement, lda.getSeed, dtype, 0)
+    StcNative.ldaSetCorpus(handle, corpus, rows.length)
+    StcNative.ldaInitRandom(handle, lda.getSeed)  // λ₀ ~ Gamma(gammaShape, 1/gammaShape)
+    this
+  }
+
+  /** One OnlineLDAOptimizer.next(): sample → E-step → sstats → (RCCL) → λ / α update, on the GPU. */
+  override private[clustering] def next(): HipOnlineLDAOptimizer = {
+    StcNative.ldaNext(handle, null)
+    this
+  }
+
+  override private[clustering] def getLDAModel(iterationTimes: Array[Double]): LDAModel = {
+    val topics = new Array[Double](vocabSize * k)  // k×V row-major = V×k column-major (Matrices.dense)
+    StcNative.ldaGetTopics(handle, topics, StcNative.LAYOUT_KV)
+    val alpha = new Array[Double](k)
+    StcNative.ldaGetAlpha(handle, alpha)
+    val eta = StcNative.ldaGetEta(handle)
+    new LocalLDAModel(Matrices.dense(vocabSize, k, topics), Vectors.dense(alpha), eta, gammaShape)
+  }
+
+  /** The live GPU model (describeTopics / topicDistribution / logLikelihood on the device). */
+  def deviceHandle: Long = handle
+
+  /** Releases the device model, corpus and context. */
+  def close(): Unit = {
+    if (handle != 0L) StcNative.ldaDestroy(handle)
+    if (corpus != 0L) StcNative.dcsrFree(corpus)
+    if (ctx != 0L) StcNative.destroy(ctx)
+    handle = 0L
+    corpus = 0L
+    ctx = 0L
+  }
+}

@@ -910,7 +910,7 @@ void stc_lda_config_default(stc_lda_config* c) {
   c->optimize_doc_concentration = 1;
   c->sample_with_replacement = 1;
   c->seed = 0;
-  c->dtype = STC_F32;
+  c->dtype = STC_F64;  // Spark computes the E-step in Double
   c->max_inner_iter = 0;
 }
 

@@ -39,7 +39,7 @@ class LdaHandle:
     def __init__(self, ctx: Context, k, vocab_size, doc_concentration=None, topic_concentration=-1.0,
                  tau0=1024.0, kappa=0.51, mini_batch_fraction=0.05, gamma_shape=100.0,
                  optimize_doc_concentration=True, sample_with_replacement=True, seed=0,
-                 dtype="f32", max_inner_iter=0):
+                 dtype="f64", max_inner_iter=0):
         self.ctx = ctx
         cfg = L.LdaConfig()
         ctx.lib.stc_lda_config_default(C.byref(cfg))
@@ -266,7 +266,7 @@ class LDAModel:
                       self._h.gamma_shape, overwrite=overwrite)
 
     @staticmethod
-    def load(path, dtype="f32", seed=0, ctx: Context | None = None) -> "LDAModel":
+    def load(path, dtype="f64", seed=0, ctx: Context | None = None) -> "LDAModel":
         """Read a Spark mllib LocalLDAModel directory onto the GPU."""
         from . import io
 
@@ -323,7 +323,7 @@ class LDA:
     def __init__(self, k=10, maxIter=20, optimizer="online", learningOffset=1024.0, learningDecay=0.51,
                  subsamplingRate=0.05, optimizeDocConcentration=True, docConcentration=None,
                  topicConcentration=None, seed=ML_LDA_DEFAULT_SEED, featuresCol="features",
-                 topicDistributionCol="topicDistribution", dtype="f32", maxInnerIter=0,
+                 topicDistributionCol="topicDistribution", dtype="f64", maxInnerIter=0,
                  ctx: Context | None = None):
         self.setK(k).setMaxIter(maxIter).setOptimizer(optimizer).setLearningOffset(learningOffset)
         self.setLearningDecay(learningDecay).setSubsamplingRate(subsamplingRate)
@@ -449,7 +449,7 @@ class MllibLDA:
         self.seed = _java_string_hash("org.apache.spark.mllib.clustering.LDA")
         self.optimizer = OnlineLDAOptimizer()
         self.checkpointInterval = 10
-        self.dtype = "f32"
+        self.dtype = "f64"
         self._ctx = ctx
 
     def setOptimizer(self, opt):

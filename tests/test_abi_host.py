@@ -67,7 +67,7 @@ def test_config_default_matches_spark_ml():
     assert cfg.k == 10 and cfg.vocab_size == 1 << 18
     assert cfg.tau0 == 1024.0 and cfg.kappa == 0.51 and cfg.mini_batch_fraction == 0.05
     assert cfg.gamma_shape == 100.0 and cfg.optimize_doc_concentration == 1
-    assert cfg.topic_concentration == -1.0 and cfg.dtype == stc.STC_F32
+    assert cfg.topic_concentration == -1.0 and cfg.dtype == stc.STC_F64
 
 
 def test_csr_container_and_rows():

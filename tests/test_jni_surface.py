@@ -1,0 +1,42 @@
+"""CPU: the JVM boundary files (jni/stcjni.c, scala/…/StcNative.java) cover include/stc.h.
+
+No JDK exists in this container, so the shim cannot be compiled here (jni/Makefile skips without
+jni.h); these checks keep it in step with the C ABI: every stc.h entry point is called by a JNI
+wrapper, every JNI wrapper has its `native` declaration in StcNative.java and vice versa.
+"""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JNI = os.path.join(ROOT, "jni", "stcjni.c")
+JAVA = os.path.join(ROOT, "scala", "org", "apache", "spark", "mllib", "clustering", "StcNative.java")
+
+
+def _header_symbols():
+    txt = open(os.path.join(ROOT, "include", "stc.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const char\*|int|void)\s+(stc_\w+)\s*\(", txt, re.M)))
+
+
+def test_every_c_entry_point_has_a_jni_wrapper():
+    src = open(JNI).read()
+    called = set(re.findall(r"\b(stc_\w+)\s*\(", src))
+    missing = [s for s in _header_symbols() if s not in called]
+    assert not missing, missing
+
+
+def test_jni_wrappers_match_java_natives():
+    src = open(JNI).read()
+    wrappers = set(re.findall(r"JNICALL FN\((\w+)\)", src))
+    natives = set(re.findall(r"public static native \S+ (\w+)\(", open(JAVA).read()))
+    assert wrappers == natives, (sorted(wrappers - natives), sorted(natives - wrappers))
+    assert len(wrappers) == len(_header_symbols()) - 1  # stc_lda_config_default is used inside ldaCreate
+
+
+def test_optimizer_plugs_into_the_reference_switch():
+    opt = open(os.path.join(ROOT, "scala", "org", "apache", "spark", "mllib", "clustering",
+                            "HipOnlineLDAOptimizer.scala")).read()
+    assert "package org.apache.spark.mllib.clustering" in opt
+    assert "extends LDAOptimizer" in opt
+    for m in ("initialize(docs: RDD[(Long, Vector)], lda: LDA)", "next()", "getLDAModel(iterationTimes: Array[Double])"):
+        assert m in opt
+    assert "LDAClustering.scala:40-46" in opt
