@@ -44,18 +44,26 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 PEAK_TFS = {"f32": 157.3, "f64": 78.6}  # MI355X dense vector peaks (fp32 = MFMA f32 rate; fp64 vector)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-METRIC = "LDA E-step docs/sec (node) at k=100, V=2^18; % of HBM roofline"
+METRIC = "LDA E-step docs/sec (node) at k=100, V=2^18; % of HBM roofline"  # the configs[1] metric
+
+
+# BASELINE.json configs: 2 (the headline), 4 (its per-GPU shard: 10M docs over 8 GPUs), 5
+PRESETS = {2: dict(docs=1_000_000, tokens=200, vocab=1 << 18, k=100),
+           4: dict(docs=1_250_000, tokens=500, vocab=1 << 20, k=500),
+           5: dict(docs=1_000_000, tokens=50, vocab=1 << 18, k=2000)}
 
 
 def parse():
     p = argparse.ArgumentParser()
+    p.add_argument("--config", type=int, default=2, choices=sorted(PRESETS),
+                   help="BASELINE.json configs[n-1] shape preset (docs/tokens/vocab/k); explicit flags override")
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--docs", type=int, default=1_000_000, help="documents of the corpus (per GPU if weak)")
-    p.add_argument("--tokens", type=int, default=200)
-    p.add_argument("--vocab", type=int, default=1 << 18)
-    p.add_argument("--k", type=int, default=100)
+    p.add_argument("--docs", type=int, default=None, help="documents of the corpus (per GPU if weak)")
+    p.add_argument("--tokens", type=int, default=None)
+    p.add_argument("--vocab", type=int, default=None)
+    p.add_argument("--k", type=int, default=None)
     p.add_argument("--fraction", type=float, default=0.05)
     p.add_argument("--corpus", default="zipf", choices=["zipf", "zipf-lda"])
     p.add_argument("--dtype", default="f64", choices=["f32", "f64"])
@@ -64,10 +72,14 @@ def parse():
     p.add_argument("--state-minibatches", type=int, default=20,
                    help="minibatches applied from λ₀ before timing (burn-in + warmup)")
     p.add_argument("--workers", type=int, default=16, help="corpus-generation processes (before GPU init)")
-    p.add_argument("--no-secondary", action="store_true", help="headline only (no fp32 / planted lines)")
+    p.add_argument("--no-secondary", action="store_true", help="headline only (no fp32 / planted / featurisation)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-hbm-copy", action="store_true", help="skip the device-copy HBM probe")
-    return p.parse_args()
+    a = p.parse_args()
+    for key, v in PRESETS[a.config].items():
+        if getattr(a, key) is None:
+            setattr(a, key, v)
+    return a
 
 
 def bytes_per_doc(nnz, k, s):
@@ -172,6 +184,60 @@ def cpu_baseline(h, corpus, a, budget_s=12.0):
                       f"E-step + per-thread dense k×V stats + reduce + λ/α update, fp64) from the GPU model "
                       f"after the timed steps; oracle/lda_oracle.c oracle_minibatch, OpenMP {threads} threads; "
                       f"mean inner iters {iters / max(1, done):.1f}; {dt:.1f} s"}
+
+
+def featurization(stc, ctx, a, log, tokens, reps=3):
+    """HashingTF (2^18 buckets, Spark 2.4.3's murmur3 tail) → IDF(minDocFreq = 2) fit → TF·IDF transform
+    with the reference's 1e-4 floor (LDAClustering.scala:154-192), all on the GPU over a token corpus
+    already resident in HBM (stc_tokens_upload before timing).  One pass = the three calls, each
+    synchronised; tokens/s over the mean of `reps` passes after one warm-up pass."""
+    (blob, tok_off, doc_off), _ = tokens
+    n_tok, n_docs = tok_off.size - 1, doc_off.size - 1
+    dt = stc.DeviceTokens(ctx, blob, tok_off, doc_off)
+    htf = stc.HashingTF(numFeatures=a.vocab, ctx=ctx)
+    idf = stc.IDF(minDocFreq=2, ctx=ctx)
+
+    def one():
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        d = htf.transform_tokens_device(dt, stc.STC_F64)
+        ctx.synchronize()
+        t1 = time.perf_counter()
+        m = idf.fit_device(d)
+        t2 = time.perf_counter()
+        m.transform_device(d, zero_floor=1e-4)
+        ctx.synchronize()
+        t3 = time.perf_counter()
+        nnz = d.nnz
+        d.free()
+        return np.array([t1 - t0, t2 - t1, t3 - t2]), nnz
+
+    one()
+    ts, nnz = [], 0
+    for _ in range(reps):
+        t, nnz = one()
+        ts.append(t)
+    t = np.mean(ts, axis=0)
+    dt.free()
+    V = a.vocab
+    # algorithmic bytes: HashingTF reads the blob + offsets once and writes the CSR; IDF fit reads the
+    # CSR (indices + values) and writes df + idf; the transform reads indices + idf[j] + values, writes values
+    b_hash = blob.size + 8.0 * (n_tok + 1) + 8.0 * (n_docs + 1) + nnz * (4 + 8) + 8.0 * (n_docs + 1)
+    b_fit = nnz * (4 + 8) + 2 * 8.0 * V
+    b_tr = nnz * (4 + 8 + 8) + 8.0 * V
+    total = float(t.sum())
+    return {
+        "label": "featurisation: HashingTF(2^18, spark24 murmur3) -> IDF(2).fit -> transform(1e-4 floor), "
+                 "tokens resident in HBM",
+        "value": n_tok / total, "unit": "tokens/s", "dtype": "f64 (values), int32 (indices)",
+        "corpus": f"{n_docs} docs x {n_tok // max(1, n_docs)} tokens, Zipf(1) over a seeded 2^18-word "
+                  f"dictionary (1-12 chars, 1-4 byte UTF-8: every murmur3 tail length)",
+        "tokens": n_tok, "utf8_bytes": int(blob.size), "nnz": int(nnz),
+        "ms": {"hashing_tf": round(t[0] * 1e3, 3), "idf_fit": round(t[1] * 1e3, 3), "idf_transform": round(t[2] * 1e3, 3)},
+        "roofline": {"bound": "hbm", "achieved": (b_hash + b_fit + b_tr) / total / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": (b_hash + b_fit + b_tr) / total / 1e9 / HBM_PEAK_GBS,
+                     "algorithmic_bytes": {"hashing_tf": b_hash, "idf_fit": b_fit, "idf_transform": b_tr}},
+    }
 
 
 def run_state(stc, ctx, dcorp, a, dtype, total, lam0, barrier, log, steps, warmup):
@@ -284,6 +350,9 @@ def main():
         planted = (synth.zipf_lda_corpus(a.docs, a.tokens, a.vocab, a.k, seed=a.seed + 1, workers=workers),
                    synth.planted_topics(a.vocab, a.k, seed=a.seed + 1))
         log(f"planted-topic corpus generated in {time.perf_counter() - t0:.1f} s")
+        t0 = time.perf_counter()
+        tokens = synth.token_corpus(a.docs, a.tokens, seed=a.seed + 2, workers=workers)
+        log(f"token corpus generated in {time.perf_counter() - t0:.1f} s")
 
     dist = None
     if world > 1:
@@ -338,6 +407,9 @@ def main():
                               dtype=dt, corpus="zipf-lda", **s3))
             dp.free()
         dcorp[other].free()
+        log("featurisation")
+        lines.append(featurization(stc, ctx, a, log, tokens))
+        del tokens
 
     if rank != 0:
         if dist is not None:
@@ -366,6 +438,7 @@ def main():
         "dtype": a.dtype,
         "data": f"synthetic {a.corpus} corpus (seeded, generated in {gen_s:.0f} s), resident in HBM",
         "config": {
+            "baseline_config": f"configs[{a.config - 1}]",
             "workload": f"online LDA minibatch steps: {a.docs} docs x {a.tokens} tokens"
                         f"{' per GPU' if a.scaling == 'weak' else ' sharded over the GPUs'}, V={a.vocab}, k={a.k}, "
                         f"subsamplingRate={a.fraction}",

@@ -119,6 +119,14 @@ int stc_hashing_tf(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int
                    int64_t n_tok, const int64_t* doc_off, int64_t n_docs, int32_t num_features,
                    int binary, int hash_variant, int64_t* indptr_out /* n_docs+1 */,
                    int32_t* indices_out, double* values_out);
+/* device-resident token input: the same (utf8, tok_off, doc_off) triple uploaded once, for callers that
+ * keep the corpus on the GPU between calls (and for timing the kernels without the PCIe upload) */
+typedef struct stc_dtok stc_dtok;
+int stc_tokens_upload(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int64_t* tok_off,
+                      int64_t n_tok, const int64_t* doc_off, int64_t n_docs, stc_dtok** out);
+int stc_tokens_free(stc_dtok* t);
+int stc_hashing_tf_tokens(stc_ctx* ctx, const stc_dtok* tokens, int32_t num_features, int binary,
+                          int hash_variant, int value_dtype, stc_dcsr** out);
 /* raw per-token bucket indices (test hook for K1): idx_out[n_tok] */
 int stc_hash_tokens(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int64_t* tok_off,
                     int64_t n_tok, int32_t num_features, int hash_variant, int32_t* idx_out);

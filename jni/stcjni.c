@@ -186,6 +186,34 @@ JNIEXPORT void JNICALL FN(hashTokens)(JNIEnv* env, jclass c, jlong ctx, jbyteArr
   check(env, st);
 }
 
+JNIEXPORT jlong JNICALL FN(tokensUpload)(JNIEnv* env, jclass c, jlong ctx, jbyteArray utf8, jlongArray tok_off,
+                                         jlongArray doc_off) {
+  stc_dtok* out = NULL;
+  jbyte* u = PIN(jbyte, Byte, utf8);
+  jlong* to = PIN(jlong, Long, tok_off);
+  jlong* dof = PIN(jlong, Long, doc_off);
+  int st = stc_tokens_upload(CTX(ctx), (const uint8_t*)u, LEN(utf8), (const int64_t*)to, LEN(tok_off) - 1,
+                             (const int64_t*)dof, LEN(doc_off) - 1, &out);
+  UNPIN(Long, doc_off, dof, JNI_ABORT);
+  UNPIN(Long, tok_off, to, JNI_ABORT);
+  UNPIN(Byte, utf8, u, JNI_ABORT);
+  if (check(env, st)) return 0;
+  return (jlong)(intptr_t)out;
+}
+
+JNIEXPORT void JNICALL FN(tokensFree)(JNIEnv* env, jclass c, jlong tokens) {
+  check(env, stc_tokens_free((stc_dtok*)(intptr_t)tokens));
+}
+
+JNIEXPORT jlong JNICALL FN(hashingTfTokens)(JNIEnv* env, jclass c, jlong ctx, jlong tokens, jint num_features,
+                                            jboolean binary, jint variant, jint dtype) {
+  stc_dcsr* out = NULL;
+  if (check(env, stc_hashing_tf_tokens(CTX(ctx), (const stc_dtok*)(intptr_t)tokens, num_features, binary,
+                                       variant, dtype, &out)))
+    return 0;
+  return (jlong)(intptr_t)out;
+}
+
 /* ---- Tokenizer -------------------------------------------------------------------------- */
 /* outputs sized by the caller: utf8Out ≥ text.length, tokOffOut ≥ text.length + nDocs + 1,
  * docOffOut = nDocs + 1; returns {nOutBytes, nTok} */

@@ -48,6 +48,11 @@ public final class StcNative {
                                       double[] valuesOut);
   public static native void hashTokens(long ctx, byte[] utf8, long[] tokOff, int numFeatures, int hashVariant,
                                        int[] idxOut);
+  /** tokens kept on the GPU between calls (stc_tokens_upload / stc_hashing_tf_tokens) */
+  public static native long tokensUpload(long ctx, byte[] utf8, long[] tokOff, long[] docOff);
+  public static native void tokensFree(long tokens);
+  public static native long hashingTfTokens(long ctx, long tokens, int numFeatures, boolean binary, int hashVariant,
+                                            int valueDtype);
 
   // ---- Tokenizer (ml.feature.Tokenizer: toLowerCase.split("\\s")); returns {nOutBytes, nTok}
   public static native long[] tokenize(long ctx, byte[] text, long[] textOff, byte[] utf8Out, long[] tokOffOut,

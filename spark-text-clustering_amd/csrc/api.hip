@@ -27,6 +27,11 @@ using namespace stc;
 
 struct stc_ctx : Ctx {};
 struct stc_dcsr : DCsr {};
+struct stc_dtok {
+  Ctx* ctx = nullptr;
+  DevBuf utf8, tok_off, doc_off;
+  int64_t n_bytes = 0, n_tok = 0, n_docs = 0;
+};
 
 // ---------------------------------------------------------------------------------------
 // LDA state
@@ -209,24 +214,21 @@ lda::EStepArgs<T> estep_args(stc_lda& L) {
   return a;
 }
 
-// wave kernel on slots [0, n_short), workgroup kernel on [n_short, n)
+// the register-resident kernel for the (k, dtype): the grid kernels up to k = 128 (fp32) / 104 (fp64),
+// the topics-across-lanes kernel (lda_wide.hip) beyond
+bool use_wide(int k, int dtype) { return dtype == STC_F32 ? lda::wave_row_cap(k) == 0 : lda::grid64_row_cap(k) == 0; }
+
+// fast kernel on slots [0, n_short), workgroup kernel on [n_short, n)
 template <typename T>
 void launch_split(stc_lda& L, lda::EStepArgs<T> a, int64_t n, int64_t n_short, bool stats, bool bound) {
   hipStream_t s = L.ctx->stream;
-  if constexpr (std::is_same<T, float>::value) {
-    if (n_short > 0) {
-      lda::EStepArgs<float> w = a;
-      w.slot0 = 0;
-      w.n = n_short;
-      lda::launch_estep_wave(s, w, stats, bound);
-    }
-  } else {
-    if (n_short > 0) {
-      lda::EStepArgs<double> w = a;
-      w.slot0 = 0;
-      w.n = n_short;
-      lda::launch_estep_grid64(s, w, stats, bound);
-    }
+  if (n_short > 0) {
+    lda::EStepArgs<T> w = a;
+    w.slot0 = 0;
+    w.n = n_short;
+    if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
+    else if constexpr (std::is_same<T, float>::value) lda::launch_estep_wave(s, w, stats, bound);
+    else lda::launch_estep_grid64(s, w, stats, bound);
   }
   if (n > n_short) {
     a.slot0 = n_short;
@@ -730,6 +732,54 @@ void upload_tokens(Ctx& c, TokenUpload& u, const uint8_t* utf8, int64_t n_bytes,
 }
 }  // namespace
 
+int stc_tokens_upload(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int64_t* tok_off,
+                      int64_t n_tok, const int64_t* doc_off, int64_t n_docs, stc_dtok** out) {
+  return guard([&] {
+    STC_REQUIRE(ctx && doc_off && out, "ctx/doc_off/out");
+    ctx->use();
+    auto t = std::make_unique<stc_dtok>();
+    t->ctx = ctx;
+    TokenUpload u;
+    upload_tokens(*ctx, u, utf8, n_bytes, tok_off, n_tok, doc_off, n_docs);
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    std::swap(t->utf8.p, u.utf8.p);
+    std::swap(t->utf8.bytes, u.utf8.bytes);
+    std::swap(t->tok_off.p, u.tok_off.p);
+    std::swap(t->tok_off.bytes, u.tok_off.bytes);
+    std::swap(t->doc_off.p, u.doc_off.p);
+    std::swap(t->doc_off.bytes, u.doc_off.bytes);
+    t->n_bytes = n_bytes;
+    t->n_tok = n_tok;
+    t->n_docs = n_docs;
+    *out = t.release();
+  });
+}
+
+int stc_tokens_free(stc_dtok* t) {
+  return guard([&] {
+    if (!t) return;
+    if (t->ctx) (void)hipSetDevice(t->ctx->device);
+    delete t;
+  });
+}
+
+int stc_hashing_tf_tokens(stc_ctx* ctx, const stc_dtok* tokens, int32_t num_features, int binary,
+                          int hash_variant, int value_dtype, stc_dcsr** out) {
+  return guard([&] {
+    STC_REQUIRE(ctx && tokens && out, "ctx/tokens/out");
+    STC_REQUIRE(num_features > 0, "numFeatures must be > 0");
+    STC_REQUIRE(hash_variant == STC_HASH_STANDARD || hash_variant == STC_HASH_SPARK24, "hash_variant");
+    STC_REQUIRE(value_dtype == STC_F32 || value_dtype == STC_F64, "value_dtype");
+    ctx->use();
+    auto m = std::make_unique<stc_dcsr>();
+    m->ctx = ctx;
+    hashing::build_csr(*ctx, tokens->utf8.as<uint8_t>(), tokens->tok_off.as<int64_t>(), tokens->n_tok,
+                       tokens->doc_off.as<int64_t>(), tokens->n_docs, num_features, binary, hash_variant,
+                       value_dtype, *m);
+    *out = m.release();
+  });
+}
+
 int stc_hash_tokens(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const int64_t* tok_off,
                     int64_t n_tok, int32_t num_features, int hash_variant, int32_t* idx_out) {
   return guard([&] {
@@ -945,7 +995,8 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     const char* nw = std::getenv("STC_DISABLE_WAVE");
     // docs with nnz <= wave_cap run the register-resident grid kernel (fp32: lda_grid.hip, fp64:
     // lda_grid64.hip), the rest the workgroup kernel (lda.hip); −1: no slot is "short" (not even empty)
-    const int cap = cfg->dtype == STC_F32 ? lda::wave_row_cap(L->k) : lda::grid64_row_cap(L->k);
+    const int cap = use_wide(L->k, L->dtype) ? lda::wide_row_cap(L->k)
+                    : cfg->dtype == STC_F32 ? lda::wave_row_cap(L->k) : lda::grid64_row_cap(L->k);
     L->wave_cap = (!(nw && nw[0] == '1') && cap > 0) ? cap : -1;
     // α / η resolution ([U] OnlineLDAOptimizer.initialize)
     std::vector<double> alpha((size_t)L->k);

@@ -28,6 +28,66 @@ __device__ __forceinline__ float rs_dpp(float x, float y, bool hi) {
 constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141, DPP_ROW_ROR8 = 0x128,
               DPP_QP_3210 = 0x1B, DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E;
 
+// ---- fp64 cross-lane helpers (lda_grid64.hip, lda_wide.hip): a double moves as two dwords
+typedef unsigned long long u64;
+
+__device__ __forceinline__ unsigned lo32(double v) { return (unsigned)__builtin_bit_cast(u64, v); }
+__device__ __forceinline__ unsigned hi32(double v) { return (unsigned)(__builtin_bit_cast(u64, v) >> 32); }
+__device__ __forceinline__ double mkd(unsigned lo, unsigned hi) {
+  return __builtin_bit_cast(double, ((u64)hi << 32) | lo);
+}
+// 64-bit DPP move as two 32-bit moves (all-lanes-valid permutations only)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)lo32(v), CTRL, 0xF, 0xF, true);
+  const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)hi32(v), CTRL, 0xF, 0xF, true);
+  return mkd(lo, hi);
+}
+template <int CTRL>
+__device__ __forceinline__ double rs_dpp_d(double x, double y, bool hi) {
+  const double keep = hi ? y : x;
+  const double send = hi ? x : y;
+  return keep + dpp_d<CTRL>(send);
+}
+// reduce-scatter over lane distance 32 (D32) or 16 for N double pairs: both dwords of each value go
+// through one v_permlane*_swap each (two values per hazard nop)
+template <bool D32, int N>
+__device__ __forceinline__ void swap_add_nd(const double* xs, const double* ys, double* out) {
+  unsigned xl[N], xh[N], yl[N], yh[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    xl[i] = lo32(xs[i]);
+    xh[i] = hi32(xs[i]);
+    yl[i] = lo32(ys[i]);
+    yh[i] = hi32(ys[i]);
+  }
+  constexpr int N2 = N / 2 * 2;
+#pragma unroll
+  for (int b = 0; b < N2; b += 2)
+    pswap_4<D32>(xl[b], yl[b], xh[b], yh[b], xl[b + 1], yl[b + 1], xh[b + 1], yh[b + 1]);
+  if constexpr (N % 2 == 1) pswap_2<D32>(xl[N - 1], yl[N - 1], xh[N - 1], yh[N - 1]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = mkd(xl[i], xh[i]) + mkd(yl[i], yh[i]);
+}
+// fp64 wave64 all-reduce (sum) without LDS
+__device__ __forceinline__ double wave_sum_d(double v) {
+  {
+    unsigned a = lo32(v), b = a, c = hi32(v), d = c;
+    pswap_2<true>(a, b, c, d);
+    v = mkd(a, c) + mkd(b, d);
+  }
+  {
+    unsigned a = lo32(v), b = a, c = hi32(v), d = c;
+    pswap_2<false>(a, b, c, d);
+    v = mkd(a, c) + mkd(b, d);
+  }
+  v += dpp_d<DPP_ROW_MIRROR>(v);
+  v += dpp_d<DPP_ROW_HALF_MIRROR>(v);
+  v += dpp_d<DPP_QP_1032>(v);
+  v += dpp_d<DPP_QP_2301>(v);
+  return v;
+}
+
 // Diagnostic build only (make stamp → libstc_stamp.so, tools/stamp_estep.py): s_memtime stamps at
 // the phase boundaries of the inner loop, summed per phase over every wave of a launch.  The
 // product library compiles STAMP(i) to nothing.

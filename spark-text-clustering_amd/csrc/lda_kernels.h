@@ -79,6 +79,10 @@ void launch_estep_grid(hipStream_t s, const EStepArgs<float>& a, bool stats, boo
 // fp64 grid E-step (lda_grid64.hip): k <= 104, nnz <= grid64_row_cap(k) (0 if n/a).
 int grid64_row_cap(int k);
 void launch_estep_grid64(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound);
+// many-topic E-step (lda_wide.hip): topics across a 512-thread workgroup, k <= 2048, nnz <= wide_row_cap(k)
+int wide_row_cap(int k);
+template <typename T>
+void launch_estep_wide(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound);
 
 // Batch partition: slots [0, n_short) = members with nnz <= cap (wave kernel), then the rest.
 void launch_part_flags(hipStream_t s, const int64_t* indptr, const int32_t* batch, int64_t n,

@@ -9,7 +9,7 @@ from . import io
 from .clustering import (LDA, ML_LDA_DEFAULT_SEED, DistributedLDAModel, LdaHandle, LDAModel, MllibLDA,
                          OnlineLDAOptimizer, reference_mini_batch_fraction)
 from .core import Context, CsrMatrix, DeviceCsr
-from .feature import IDF, HashingTF, IDFModel, Tokenizer, encode_texts, encode_tokens
+from .feature import IDF, DeviceTokens, HashingTF, IDFModel, Tokenizer, encode_texts, encode_tokens
 
 __all__ = [
     "Context", "CsrMatrix", "DeviceCsr", "HashingTF", "IDF", "IDFModel", "Tokenizer", "encode_texts", "encode_tokens", "LDA",

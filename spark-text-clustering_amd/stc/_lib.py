@@ -83,6 +83,9 @@ SIGNATURES = {
     "stc_hashing_tf": (_int, [_p, _pu8, _i64, _pi64, _i64, _pi64, _i64, _i32, _int, _int, _pi64,
                               _pi32, _pdbl]),
     "stc_hash_tokens": (_int, [_p, _pu8, _i64, _pi64, _i64, _i32, _int, _pi32]),
+    "stc_tokens_upload": (_int, [_p, _pu8, _i64, _pi64, _i64, _pi64, _i64, C.POINTER(_p)]),
+    "stc_tokens_free": (_int, [_p]),
+    "stc_hashing_tf_tokens": (_int, [_p, _p, _i32, _int, _int, _int, C.POINTER(_p)]),
     "stc_tokenize": (_int, [_p, _pu8, _i64, _pi64, _i64, _pu8, _pi64, _pi64, _pi64, _pi64]),
     "stc_tokenize_hashing_tf_dev": (_int, [_p, _pu8, _i64, _pi64, _i64, _i32, _int, _int, _int,
                                            C.POINTER(_p)]),

@@ -43,6 +43,32 @@ def encode_texts(texts):
     return np.ascontiguousarray(blob), off
 
 
+class DeviceTokens:
+    """Token input resident on the GPU (stc_dtok): the (utf8, tok_off, doc_off) triple uploaded once."""
+
+    def __init__(self, ctx: Context, blob, tok_off, doc_off):
+        blob = np.ascontiguousarray(blob, np.uint8)
+        tok_off = L.as_i64(tok_off)
+        doc_off = L.as_i64(doc_off)
+        h = C.c_void_p()
+        L.check(ctx.lib.stc_tokens_upload(ctx.handle, L.ptr(blob, C.c_uint8), blob.size, L.ptr(tok_off, C.c_int64),
+                                          tok_off.size - 1, L.ptr(doc_off, C.c_int64), doc_off.size - 1,
+                                          C.byref(h)))
+        self.ctx, self.handle = ctx, h
+        self.n_bytes, self.n_tok, self.n_docs = blob.size, tok_off.size - 1, doc_off.size - 1
+
+    def free(self):
+        if self.handle:
+            self.ctx.lib.stc_tokens_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class Tokenizer:
     """Lower-cases each document and splits it on Java whitespace, on the GPU (kernel K0).
 
@@ -143,6 +169,13 @@ class HashingTF:
             self.ctx.handle, L.ptr(blob, C.c_uint8), blob.size, L.ptr(tok_off, C.c_int64),
             tok_off.size - 1, L.ptr(doc_off, C.c_int64), doc_off.size - 1, self.numFeatures,
             int(self.binary), _VARIANTS[self.hashAlgorithm], int(value_dtype), C.byref(h)))
+        return DeviceCsr(self.ctx, h)
+
+    def transform_tokens_device(self, tokens: "DeviceTokens", value_dtype=L.STC_F64) -> DeviceCsr:
+        """Term frequencies of tokens already resident on the GPU (no host → device copy)."""
+        h = C.c_void_p()
+        L.check(self.ctx.lib.stc_hashing_tf_tokens(self.ctx.handle, tokens.handle, self.numFeatures, int(self.binary),
+                                                   _VARIANTS[self.hashAlgorithm], int(value_dtype), C.byref(h)))
         return DeviceCsr(self.ctx, h)
 
     def transform_text_device(self, texts, value_dtype=L.STC_F64) -> DeviceCsr:

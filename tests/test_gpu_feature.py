@@ -118,3 +118,21 @@ def test_pipeline_hashing_idf_device_resident(ctx, oracle):
     idf_o, _, _ = oracle.idf_fit(ip, ix, vv, 1 << 12, 2)
     assert np.array_equal(got.indices, ix)
     np.testing.assert_allclose(got.values, oracle.idf_transform(ix, vv, idf_o), rtol=1e-15, atol=0)
+
+
+def test_device_resident_tokens_synthetic_dictionary(ctx, oracle):
+    """stc_tokens_upload + stc_hashing_tf_tokens (the featurisation bench's path) on the bench's own
+    synthetic token generator (every UTF-8 tail length) vs the oracle, bit-exact."""
+    import stc
+    from stc import synth
+
+    (blob, tok_off, doc_off), _ = synth.token_corpus(300, 40, n_words=5000, seed=9)
+    dt = stc.DeviceTokens(ctx, blob, tok_off, doc_off)
+    d = stc.HashingTF(numFeatures=1 << 18, ctx=ctx).transform_tokens_device(dt)
+    got = d.download()
+    d.free()
+    dt.free()
+    raw = blob.tobytes()
+    docs = [[raw[tok_off[t]:tok_off[t + 1]] for t in range(doc_off[i], doc_off[i + 1])] for i in range(300)]
+    ip, ix, vv = oracle.hashing_tf(docs, 1 << 18, False, oracle.HASH_SPARK24)
+    assert np.array_equal(got.indptr, ip) and np.array_equal(got.indices, ix) and np.array_equal(got.values, vv)

@@ -29,16 +29,19 @@ def _handle(ctx, corpus, k, dtype, lam=None, **kw):
 @pytest.mark.parametrize("dtype,k,kernel", [("f64", 16, "wg"), ("f32", 16, "wave"), ("f32", 16, "wg"),
                                              ("f32", 100, "wave"), ("f32", 100, "wg"), ("f32", 128, "wave"),
                                              ("f32", 77, "wave"), ("f64", 100, "wave"), ("f64", 100, "wg"),
-                                             ("f64", 40, "wave"), ("f64", 20, "wave"), ("f64", 104, "wave")])
+                                             ("f64", 40, "wave"), ("f64", 20, "wave"), ("f64", 104, "wave"),
+                                             ("f32", 300, "wave"), ("f64", 300, "wave"), ("f32", 700, "wave"),
+                                             ("f64", 700, "wave"), ("f32", 1500, "wave"), ("f64", 1500, "wave")])
 def test_estep_gamma_and_stat(ctx, oracle, dtype, k, kernel, monkeypatch):
-    """Both E-step kernels (the register-resident grid kernels — fp32 k <= 128, fp64 k <= 104 with
-    R = 1..6 row sets, the sixth from LDS — and the workgroup-per-doc kernel otherwise) vs the oracle,
-    including docs longer than the grid's row capacity (routed to the workgroup kernel)."""
+    """Every E-step kernel vs the oracle: the register-resident grid kernels (fp32 k <= 128, fp64
+    k <= 104 with R = 1..6 row sets, the sixth from LDS), the many-topic kernel (k > 128 / 104: Q = 1, 2,
+    4 topics per lane; rows in VGPRs, then LDS, then streamed from global memory — docs up to 600 terms
+    reach all three) and the workgroup-per-doc kernel (docs past the fast kernels' row capacity)."""
     if kernel == "wg":
         monkeypatch.setenv("STC_DISABLE_WAVE", "1")
     rng = np.random.default_rng(10 + k)
     D, V = 48, 2048
-    corpus = random_corpus(rng, D, V, 1, 300, empty_every=13)
+    corpus = random_corpus(rng, D, V, 1, 600 if k > 128 else 300, empty_every=13)
     lam = rng.gamma(100.0, 0.01, size=(V, k))
     g0 = rng.gamma(100.0, 0.01, size=(D, k))
     h, _ = _handle(ctx, corpus, k, dtype, lam)
@@ -53,9 +56,14 @@ def test_estep_gamma_and_stat(ctx, oracle, dtype, k, kernel, monkeypatch):
             assert np.all(gamma[i] == 0) and iters[i] == 0
             continue
         g, ss, it = oracle.variational_topic_inference(cid, cts, eeb, alpha, g0[i])
-        np.testing.assert_allclose(gamma[i], g, rtol=TOL[dtype]["gamma"])
         if dtype == "f64":
+            np.testing.assert_allclose(gamma[i], g, rtol=TOL[dtype]["gamma"])
             assert iters[i] == it
+        else:  # fp32 vs fp64: the runs may stop an iteration apart (Spark's mean |Δγ| ≤ 1e-3 rule), so
+            # Σ|γ − γ_oracle| within two iterations' worth, 2e-3 relative on topics holding a token's mass
+            assert np.abs(gamma[i] - g).sum() <= 2e-3 * k, (i, np.abs(gamma[i] - g).sum())
+            big = g >= 1.0
+            np.testing.assert_allclose(gamma[i][big], g[big], rtol=TOL[dtype]["gamma"])
         np.add.at(stat_o, cid, ss.T)
     nz = stat_o > 1e-8 * stat_o.max()
     rel = np.abs(stat[nz] - stat_o[nz]) / stat_o[nz]

@@ -48,6 +48,8 @@ def _eeb_rows(lam, ids, oracle):
     dict(name="config2-f64", V=1 << 18, k=100, L=200, D=24, dtype="f64"),
     dict(name="config4", V=1 << 20, k=500, L=500, D=4, dtype="f32"),
     dict(name="config5", V=1 << 18, k=2000, L=50, D=6, dtype="f32"),
+    dict(name="config5-f64", V=1 << 18, k=2000, L=50, D=6, dtype="f64"),
+    dict(name="config4-f64", V=1 << 20, k=500, L=500, D=4, dtype="f64"),
 ], ids=lambda c: c["name"])
 def test_estep_at_baseline_shapes(ctx, oracle, cfg):
     import stc

@@ -10,5 +10,5 @@ step() {  # step NAME SECONDS CMD...
   echo "$name rc=$rc" >> gpurun_out/status.log
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-step pytest_gpu ${PYTEST_SECS:-900} python -u -m pytest tests -x -v -m gpu --timeout 150 --timeout-method thread ${PYTEST_ARGS:-}
+step pytest_gpu ${PYTEST_SECS:-900} python -u -m pytest tests -x -v -m gpu --timeout 150 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
