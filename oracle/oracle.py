@@ -311,11 +311,13 @@ def train_doc_key(iteration: int, rank: int, batch_pos: int) -> int:
 # ---------------------------------------------------------------------------------------
 # OnlineLDAOptimizer   [U] mllib.clustering.OnlineLDAOptimizer
 # ---------------------------------------------------------------------------------------
-def variational_topic_inference(ids, cts, exp_elog_beta, alpha, gamma0, max_iter=None):
+def variational_topic_inference(ids, cts, exp_elog_beta, alpha, gamma0, max_iter=None, n_iter=None):
     """[U] OnlineLDAOptimizer.variationalTopicInference (the E-step fixed point).
 
     exp_elog_beta is V×k.  Returns (gamma[k], sstats[k, nnz], n_iter).  The loop has no cap
-    upstream; ``max_iter`` exists only so a test can bound a pathological case.
+    upstream; ``max_iter`` exists only so a test can bound a pathological case, and ``n_iter`` runs
+    exactly that many iterations (ignoring the stop rule) so a test can compare a run that stopped
+    an iteration earlier or later than the oracle's at the same iteration.
     """
     cts = np.asarray(cts, np.float64)
     alpha = np.asarray(alpha, np.float64)
@@ -326,7 +328,7 @@ def variational_topic_inference(ids, cts, exp_elog_beta, alpha, gamma0, max_iter
     phi_norm = B @ e_theta + 1e-100
     mean_change = 1.0
     it = 0
-    while mean_change > 1e-3:
+    while (mean_change > 1e-3) if n_iter is None else (it < n_iter):
         last = gamma.copy()
         gamma = e_theta * (B.T @ (cts / phi_norm)) + alpha
         e_theta = np.exp(dirichlet_expectation(gamma))

@@ -194,10 +194,24 @@ __device__ __forceinline__ double rcp_nr(double q) {
   r = fma(r, fma(-q, r, 1.0), r);
   return fma(r, fma(-q, r, 1.0), r);
 }
+// Breeze evaluates its 8-term asymptotic series S8 at y_B = x + ⌊5 − x⌋ + 1 ∈ (5, 6]; the fast forms
+// below evaluate it at x + 6 ∈ (6, 11] (one rational for the six recurrence terms).  S8's truncation
+// error E(y) = ψ(y) − S8(y) reaches 8e-13 at y = 5, which a slowly-dying topic of a long E-step
+// amplifies past 1e-7 relative, so the difference E(x + 6) − E(y_B) is added back: E(y) = f⁹·P(f),
+// f = 1/y², P fitted to 7e-18 absolute on y ∈ [5, 11.5] (tools/fit_breeze_digamma.py).
+__device__ __forceinline__ double breeze_trunc(double iy) {
+  const double f = iy * iy, f2 = f * f, f4 = f2 * f2;
+  return f4 * f4 * f * (-3.053401198888146 + f * (26.284421368293753 + f * (-260.94994774566294 +
+                        f * (2372.137971404805 + f * -12318.55039822477))));
+}
+__device__ __forceinline__ double breeze_shift_fix(double x, double iy6, bool sh) {
+  const double yb = sh ? x + (floor(5.0 - x) + 1.0) : 6.0;  // E needs ~1e-4 relative: raw v_rcp_f64
+  return breeze_trunc(iy6) - breeze_trunc(__builtin_amdgcn_rcp(yb));
+}
 // fp64 digamma for the M-step's V×k elements, branch-free: Breeze's recurrence Σ_{i<6} 1/(x+i) for
-// x ≤ 5 as one rational Q'(x)/Q(x), Q = x(x+1)…(x+5), and the same 8-term asymptotic series at
-// y = x + 6 (or y = x when x > 5, where Breeze does not shift).  Agrees with digamma_t<double> to a
-// few ulp; the loop form costs a divergent chain of up to six fp64 divisions per element.
+// x ≤ 5 as one rational Q'(x)/Q(x), Q = x(x+1)…(x+5), the same 8-term asymptotic series at y = x + 6
+// (or y = x when x > 5, where Breeze does not shift) and breeze_shift_fix.  Agrees with
+// digamma_t<double> to a few ulp; the loop form costs a divergent chain of up to six fp64 divisions.
 __device__ inline double digamma_fast_d(double x) {
   const bool sh = x <= 5.0;
   const double q = ((((((x + 15.0) * x + 85.0) * x + 225.0) * x + 274.0) * x + 120.0) * x);
@@ -210,7 +224,7 @@ __device__ inline double digamma_fast_d(double x) {
   const double f = iy * iy;
   const double t = f * (-1.0 / 12.0 + f * (1.0 / 120.0 + f * (-1.0 / 252.0 + f * (1.0 / 240.0 +
                    f * (-1.0 / 132.0 + f * (691.0 / 32760.0 + f * (-1.0 / 12.0 + f * (3617.0 / 8160.0))))))));
-  return (sh ? -c : 0.0) + log(y) - 0.5 * iy + t;
+  return (sh ? breeze_shift_fix(x, iy, sh) - c : 0.0) + log(y) - 0.5 * iy + t;
 }
 // exp(ψ(x) − cst) for the fp64 E-step's eθ = exp(ψ(γ) − ψ(Σγ)), without the logarithm: with ψ(x) =
 // ln y − 0.5/y + t(y) − s(x) as in digamma_fast_d, exp(ψ(x) − cst) = y · exp(t − 0.5/y − s − cst).
@@ -226,7 +240,7 @@ __device__ inline double exp_digamma_minus_d(double x, double cst) {
   const double f = iy * iy;
   const double t = f * (-1.0 / 12.0 + f * (1.0 / 120.0 + f * (-1.0 / 252.0 + f * (1.0 / 240.0 +
                    f * (-1.0 / 132.0 + f * (691.0 / 32760.0 + f * (-1.0 / 12.0 + f * (3617.0 / 8160.0))))))));
-  return y * exp(((sh ? -c : 0.0) - 0.5 * iy + t) - cst);
+  return y * exp(((sh ? breeze_shift_fix(x, iy, sh) - c : 0.0) - 0.5 * iy + t) - cst);
 }
 
 __host__ __device__ inline double trigamma_d(double x) {

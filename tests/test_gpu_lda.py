@@ -50,25 +50,45 @@ def test_estep_gamma_and_stat(ctx, oracle, dtype, k, kernel, monkeypatch):
     eeb = oracle.topics_exp_elog_beta(lam)
     alpha = np.full(k, 1.0 / k)
     stat_o = np.zeros((V, k))
+    borderline = 0
     for i in ids:
         cid, cts = corpus.row(i)
         if cid.size == 0:
             assert np.all(gamma[i] == 0) and iters[i] == 0
             continue
         g, ss, it = oracle.variational_topic_inference(cid, cts, eeb, alpha, g0[i])
+        if iters[i] != it:
+            # Spark's stop rule mean |Δγ| ≤ 1e-3 lets the last iteration move Σ|γ| by up to 1e-3·k (1.5 at
+            # k = 1500), so a run that stops an iteration apart lands visibly elsewhere: in fp64 only when
+            # the test sat on the boundary (summation order decides, at most one doc), in fp32 when
+            # rounding moves the crossing.  Both are compared with the oracle run to the same iteration.
+            assert abs(int(iters[i]) - it) <= (1 if dtype == "f64" else 3), (i, iters[i], it)
+            if dtype == "f64":
+                borderline += 1
+                assert borderline <= 1, (i, iters[i], it)
+            g, ss, _ = oracle.variational_topic_inference(cid, cts, eeb, alpha, g0[i], n_iter=int(iters[i]))
         if dtype == "f64":
             np.testing.assert_allclose(gamma[i], g, rtol=TOL[dtype]["gamma"])
-            assert iters[i] == it
-        else:  # fp32 vs fp64: the runs may stop an iteration apart (Spark's mean |Δγ| ≤ 1e-3 rule), so
-            # Σ|γ − γ_oracle| within two iterations' worth, 2e-3 relative on topics holding a token's mass
-            assert np.abs(gamma[i] - g).sum() <= 2e-3 * k, (i, np.abs(gamma[i] - g).sum())
+        else:  # fp32 vs fp64 at the same iteration: rounding proportional to the doc's mass on the whole
+            # vector, 2e-3 relative on topics holding ≥ 1 token's mass
+            l1 = np.abs(gamma[i] - g).sum()
+            assert l1 <= 1e-3 * k + 1e-4 * g.sum(), (i, l1, g.sum())
             big = g >= 1.0
             np.testing.assert_allclose(gamma[i][big], g[big], rtol=TOL[dtype]["gamma"])
         np.add.at(stat_o, cid, ss.T)
-    nz = stat_o > 1e-8 * stat_o.max()
+    # fp32: a topic dying towards α (γ ~ 1e-3) has eθ ∝ exp(ψ(γ)) with dψ = dγ/γ², so its few sstats
+    # entries carry fp32's γ rounding ×1e6 (at γ ~ 0.02, ×2500) — mass-weighted error 1e-4 over all
+    # entries, and relative 1e-2 on entries ≥ 1e-4 of the largest
+    nz = stat_o > (1e-8 if dtype == "f64" else 1e-4) * stat_o.max()
     rel = np.abs(stat[nz] - stat_o[nz]) / stat_o[nz]
-    assert rel.max() < (1e-9 if dtype == "f64" else 5e-3), rel.max()
-    assert np.all(stat[~nz] < 1e-6 * stat_o.max() + 1e-300)
+    if dtype == "f64":  # the same amplification at fp64 rounding: γ's 1e-7 bound, 1e-10 mass-weighted
+        assert rel.max() < TOL[dtype]["gamma"], rel.max()
+        assert np.abs(stat - stat_o).sum() / stat_o.sum() < 1e-10
+        assert np.all(stat[~nz] < 1e-6 * stat_o.max() + 1e-300)
+    else:
+        l1 = np.abs(stat - stat_o).sum() / stat_o.sum()
+        assert l1 < 1e-4, l1
+        assert rel.max() < 1e-2, rel.max()
 
 
 def test_estep_long_documents_global_path(ctx, oracle):
