@@ -74,6 +74,8 @@ def parse():
     p.add_argument("--workers", type=int, default=16, help="corpus-generation processes (before GPU init)")
     p.add_argument("--no-secondary", action="store_true", help="headline only (no fp32 / planted / featurisation)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--featurisation-only", action="store_true",
+                   help="only the HashingTF -> IDF line (for profiling its kernels)")
     p.add_argument("--no-hbm-copy", action="store_true", help="skip the device-copy HBM probe")
     a = p.parse_args()
     for key, v in PRESETS[a.config].items():
@@ -103,13 +105,13 @@ def pmc_traffic(a, dtype, corpus):
             pm = json.load(f)
     except (OSError, ValueError):
         return None, "no PMC summary committed"
-    w = pm.get("workload", {})
-    if (w.get("docs"), w.get("k"), w.get("vocab"), w.get("tokens"), w.get("fraction"), w.get("corpus"),
-            w.get("dtype", "f32")) != (a.docs, a.k, a.vocab, a.tokens, a.fraction, corpus, dtype):
-        return None, "PMC summary is for a different workload"
-    if "estep_kernel_bytes_per_launch" not in pm:
-        return None, "PMC summary predates the per-launch E-step figure"
-    return pm["estep_kernel_bytes_per_launch"], f"{os.path.basename(PMC_SUMMARY)} ({pm.get('note', '')})"
+    want = (a.docs, a.k, a.vocab, a.tokens, a.fraction, corpus, dtype)
+    for e in pm.get("entries", [pm]):
+        w = e.get("workload", {})
+        if (w.get("docs"), w.get("k"), w.get("vocab"), w.get("tokens"), w.get("fraction"), w.get("corpus"),
+                w.get("dtype", "f32")) == want and "estep_kernel_bytes_per_launch" in e:
+            return e["estep_kernel_bytes_per_launch"], f"{os.path.basename(PMC_SUMMARY)} ({e.get('note', '')})"
+    return None, "no PMC summary committed for this workload"
 
 
 def hbm_copy_gbs(device):
@@ -319,8 +321,14 @@ def summarize(r, a, dtype, world, steps, corpus_kind, kernel):
     }
 
 
-KERNEL = {"f64": "k_estep_grid64 (lda_grid64.hip): the fp64 training E-step, one launch per minibatch",
-          "f32": "k_estep_grid (lda_grid.hip): the fp32 training E-step, one launch per minibatch"}
+def kernel_name(dtype, k):
+    """The training E-step kernel libstc dispatches (api.hip use_wide: grid kernels up to their topic
+    capacity, fp32 k <= 128 / fp64 k <= 104, the many-topic kernel past it)."""
+    if k > (128 if dtype == "f32" else 104):
+        return "k_estep_wide (lda_wide.hip): the many-topic training E-step, one launch per minibatch"
+    if dtype == "f64":
+        return "k_estep_grid64 (lda_grid64.hip): the fp64 training E-step, one launch per minibatch"
+    return "k_estep_grid (lda_grid.hip): the fp32 training E-step, one launch per minibatch"
 
 
 def main():
@@ -332,6 +340,13 @@ def main():
         a.gpus = world
     log = (lambda msg: print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True))  # progress on stderr
     from stc import synth  # no GPU touched yet: the corpus pool may fork
+
+    if a.featurisation_only:
+        tokens = synth.token_corpus(a.docs, a.tokens, seed=a.seed + 2, workers=a.workers)
+        import stc
+
+        print(json.dumps(featurization(stc, stc.Context(local), a, log, tokens, reps=max(1, a.steps))), flush=True)
+        return
 
     # corpus shard: strong = rows [r·D/N, (r+1)·D/N) of one corpus; weak = an own D-doc corpus per rank
     if a.scaling == "strong":
@@ -389,20 +404,20 @@ def main():
     DT = {"f32": stc.STC_F32, "f64": stc.STC_F64}
     dcorp = {a.dtype: stc.DeviceCsr.upload(ctx, corpus, DT[a.dtype])}
     h, r = run_state(stc, ctx, dcorp[a.dtype], a, a.dtype, total, None, barrier, log, a.steps, a.warmup)
-    head = summarize(reduce_run(r), a, a.dtype, world, a.steps, a.corpus, KERNEL[a.dtype])
+    head = summarize(reduce_run(r), a, a.dtype, world, a.steps, a.corpus, kernel_name(a.dtype, a.k))
 
     lines = []
     if secondary:
         other = "f32" if a.dtype == "f64" else "f64"
         dcorp[other] = stc.DeviceCsr.upload(ctx, corpus, DT[other])
         _, r2 = run_state(stc, ctx, dcorp[other], a, other, total, None, barrier, log, a.steps, a.warmup)
-        s2 = summarize(reduce_run(r2), a, other, world, a.steps, a.corpus, KERNEL[other])
+        s2 = summarize(reduce_run(r2), a, other, world, a.steps, a.corpus, kernel_name(other, a.k))
         lines.append(dict(label=f"{other} E-step, same corpus and model state", dtype=other, corpus=a.corpus, **s2))
         pc, lam_p = planted
         for dt in (a.dtype, other):
             dp = stc.DeviceCsr.upload(ctx, pc, DT[dt])
             _, r3 = run_state(stc, ctx, dp, a, dt, a.docs, lam_p, barrier, log, a.steps, a.warmup)
-            s3 = summarize(reduce_run(r3), a, dt, world, a.steps, "zipf-lda", KERNEL[dt])
+            s3 = summarize(reduce_run(r3), a, dt, world, a.steps, "zipf-lda", kernel_name(dt, a.k))
             lines.append(dict(label=f"{dt} E-step, planted-topic corpus at the planted model (SURVEY §8(d) state B)",
                               dtype=dt, corpus="zipf-lda", **s3))
             dp.free()

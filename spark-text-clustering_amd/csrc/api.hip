@@ -57,10 +57,27 @@ struct stc_lda {
   DevBuf s_counts, s_weights, s_short, s_cincl, s_wincl, s_sincl;
   int64_t wave_cap = 0;  // docs with nnz <= wave_cap run the wave-per-document E-step
 
+  // M-step sharding over the vocabulary (multi-GPU): rank r owns λ / expElogβ rows [r·Vs, (r+1)·Vs);
+  // Vs is a multiple of the λ-update block so the per-block colsum partials (and hence colsum) are
+  // bit-identical to the one-GPU reduction.  virt > 1 runs the same slices on one GPU without
+  // collectives (STC_VIRTUAL_SHARDS, for testing the slicing).
+  int shards = 1, virt = 1;
+  int64_t Vs = 0, vpad = 0;
+  bool lam_stale = false;  // rows outside this rank's slice are out of date (sharded M-step)
+
+  // minibatch draws: Spark's next() advances its generator on every call, empty batches included
+  int64_t draws = 0;
+  // prefetch: the next draw's membership is sampled during this step and its global size rides on
+  // this step's collective, so the next call waits on an event instead of draining the stream
+  bool pre_valid = false, pre_inflight = false;
+  int64_t pre_draw = 0;
+  hipEvent_t ev_pre = nullptr;
+  int64_t* hpre = nullptr;
+
   bool timing = false;
-  hipEvent_t ev[2][6] = {};
+  hipEvent_t ev[3][6] = {};
   int ev_set = 0;
-  bool ev_pending[2] = {false, false};
+  bool ev_pending[3] = {false, false, false};
   double acc_ms[5] = {0, 0, 0, 0, 0};
   int64_t timed_steps = 0;
   int64_t cum_docs = 0, cum_entries = 0;
@@ -73,6 +90,8 @@ struct stc_lda {
       for (auto& e : s)
         if (e) (void)hipEventDestroy(e);
     if (hcnt) (void)hipHostFree(hcnt);
+    if (hpre) (void)hipHostFree(hpre);
+    if (ev_pre) (void)hipEventDestroy(ev_pre);
   }
 };
 
@@ -99,9 +118,10 @@ void record(stc_lda& L, int slot) {
   if (L.timing) HIP_CHECK(hipEventRecord(L.ev[L.ev_set][slot], L.ctx->stream));
 }
 
-// add the phase times of an event set whose step is known to have completed
+// add the phase times of an event set whose step has completed (left pending otherwise)
 void harvest(stc_lda& L, int set) {
   if (!L.ev_pending[set]) return;
+  if (hipEventQuery(L.ev[set][5]) != hipSuccess) return;
   for (int p = 0; p < 5; ++p) {
     float ms = 0.f;
     HIP_CHECK(hipEventElapsedTime(&ms, L.ev[set][p], L.ev[set][p + 1]));
@@ -109,6 +129,51 @@ void harvest(stc_lda& L, int set) {
   }
   L.timed_steps += 1;
   L.ev_pending[set] = false;
+}
+void harvest_all(stc_lda& L) {
+  for (int set = 0; set < 3; ++set) harvest(L, set);
+}
+// before a step records into the current set: a set is reused three steps later, long complete
+void claim_event_set(stc_lda& L) {
+  if (!L.timing || !L.ev_pending[L.ev_set]) return;
+  HIP_CHECK(hipEventSynchronize(L.ev[L.ev_set][5]));
+  harvest(L, L.ev_set);
+}
+
+// the vocabulary slices of the M-step: shards = the RCCL ranks (or STC_VIRTUAL_SHARDS on one GPU).
+// λ, expElogβ', logscale and stat are padded to shards·Vs rows (the RCCL reduce-scatter / all-gather
+// chunks); the padded rows of stat are zero, those of λ / Bp never read.  Called before a step; a
+// change of shard count (comm initialised after the handle) keeps λ and recomputes the rest.
+void ensure_layout(stc_lda& L) {
+  const int want = L.ctx->comm && L.ctx->n_ranks > 1 ? L.ctx->n_ranks : L.virt;
+  if (want == L.shards && L.Vs > 0) return;
+  if (L.lam_stale) throw Error(STC_ERR_STATE, "the shard count changed after sharded steps");
+  const int64_t RB = lda::kRowsPerBlock;
+  const int64_t Vs = ceil_div(ceil_div(L.V, (int64_t)want), RB) * RB;
+  const int64_t vpad = Vs * want;
+  if ((size_t)(8 * vpad * L.k) > L.lam.bytes) {  // grow λ, keeping its V·k prefix
+    DevBuf tmp;
+    tmp.reserve(8 * vpad * L.k);
+    HIP_CHECK(hipMemcpyAsync(tmp.p, L.lam.p, 8 * L.V * L.k, hipMemcpyDeviceToDevice, L.ctx->stream));
+    HIP_CHECK(hipStreamSynchronize(L.ctx->stream));
+    std::swap(tmp.p, L.lam.p);
+    std::swap(tmp.bytes, L.lam.bytes);
+  }
+  L.Bp.reserve(L.tsize * vpad * L.kp);
+  L.stat.reserve(L.tsize * vpad * L.kp);
+  L.logscale.reserve(8 * vpad);
+  L.colpart.reserve(8 * (vpad / RB) * L.k);
+  L.shards = want;
+  L.Vs = Vs;
+  L.vpad = vpad;
+  L.lam_stale = false;
+}
+void refresh(stc_lda& L);
+void relayout(stc_lda& L) {
+  const int old = L.shards;
+  const int64_t vs = L.Vs;
+  ensure_layout(L);
+  if ((old != L.shards || vs != L.Vs) && L.has_topics) refresh(L);
 }
 
 template <typename T>
@@ -277,7 +342,7 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   record(L, 1);
   launch_split<T>(L, a, n, n_short, true, false);
   record(L, 2);
-  HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.V * L.kp, s));
+  HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.vpad * L.kp, s));  // padded rows stay zero
   if (E > 0) {
     size_t tb = L.sort_tmp.bytes;
     HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(L.sort_tmp.p, tb, L.keys.as<uint32_t>(),
@@ -299,15 +364,54 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   record(L, 3);
 }
 
+// the λ update, colsum and expElogβ' of one vocabulary slice r: rows [r·Vs, r·Vs + vn); its colsum
+// partials land at λ-update block r·Vs/RB, where the one-GPU reduction has them
+template <typename T>
+void mstep_slice(stc_lda& L, int r, double rho, double scale, const double* gate) {
+  const int64_t v0 = (int64_t)r * L.Vs, vn = std::max<int64_t>(0, std::min(L.V - v0, L.Vs));
+  const int64_t nbs = L.Vs / lda::kRowsPerBlock;
+  lda::launch_lambda_update<T>(L.ctx->stream, L.lam.as<double>() + v0 * L.k, L.stat.as<T>() + v0 * L.kp,
+                               L.Bp.as<T>() + v0 * L.kp, vn, L.k, L.kp, rho, scale, L.eta, gate,
+                               L.colpart.as<double>() + (int64_t)r * nbs * L.k, nbs);
+}
+template <typename T>
+void eeb_slice(stc_lda& L, int r, const double* gate) {
+  const int64_t v0 = (int64_t)r * L.Vs, vn = std::max<int64_t>(0, std::min(L.V - v0, L.Vs));
+  if (vn > 0)
+    lda::launch_expelogbeta<T>(L.ctx->stream, L.lam.as<double>() + v0 * L.k, L.colsum.as<double>(), vn, L.k,
+                               L.kp, gate, L.Bp.as<T>() + v0 * L.kp, L.logscale.as<double>() + v0);
+}
+
+// [U] submitMiniBatch tail: the stats merge (treeReduce ≙ RCCL), updateLambda, updateAlpha.
+//  * one GPU: λ update over all rows, colsum, expElogβ'.
+//  * N ranks: reduce-scatter of stat (each rank receives the summed rows of its vocabulary slice) and
+//    the logphat / count all-reduce in one group; the slice's λ update; an all-gather of the per-block
+//    colsum partials (k doubles per 64 rows), reduced in the one-GPU order, so colsum is identical on
+//    every rank; the slice's expElogβ'; an all-gather of expElogβ' and logscale for the next E-step.
+//    λ stays sharded (lam_stale) until a reader gathers it.  Per rank: stat (N−1)/N·V·kp·T bytes
+//    out, expElogβ' the same in, against 2(N−1)/N for an all-reduce, and 1/N of the M-step work.
 template <typename T>
 void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
   Ctx& c = *L.ctx;
   hipStream_t s = c.stream;
-  if (c.comm) {  // treeReduce(elementWiseSum) ≙ one grouped RCCL all-reduce over xGMI
+  const bool ranks = c.comm && c.n_ranks > 1;
+  if (c.comm) {
     RCCL_CHECK(ncclGroupStart());
-    RCCL_CHECK(ncclAllReduce(L.stat.p, L.stat.p, (size_t)(L.V * L.kp), RcclType<T>::v, ncclSum, c.comm, s));
+    if (ranks) {
+      const size_t cnt = (size_t)(L.Vs * L.kp);
+      RCCL_CHECK(ncclReduceScatter(L.stat.p, L.stat.as<T>() + (size_t)c.rank * cnt, cnt, RcclType<T>::v, ncclSum,
+                                   c.comm, s));
+    }
     RCCL_CHECK(ncclAllReduce(L.small.p, L.small.p, (size_t)(L.k + 1), ncclFloat64, ncclSum, c.comm, s));
+    if (L.pre_inflight)  // the next draw's global batch size (word 3), for the next call
+      RCCL_CHECK(ncclAllReduce(L.dcnt.as<int64_t>() + 3, L.dcnt.as<int64_t>() + 3, 1, ncclInt64, ncclSum, c.comm, s));
     RCCL_CHECK(ncclGroupEnd());
+  }
+  if (L.pre_inflight) {
+    HIP_CHECK(hipMemcpyAsync(L.hpre, L.dcnt.p, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipEventRecord(L.ev_pre, s));
+    L.pre_inflight = false;
+    L.pre_valid = true;
   }
   record(L, 4);
   L.iteration += 1;
@@ -315,17 +419,32 @@ void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
   const double batch_size = std::ceil(L.cfg.mini_batch_fraction * (double)L.corpus_total);
   const double scale = (double)L.corpus_total / batch_size;
   const double* gate = L.small.as<double>() + L.k;
-  lda::launch_lambda_update<T>(s, L.lam.as<double>(), L.stat.as<T>(), L.Bp.as<T>(), L.V, L.k, L.kp,
-                               rho, scale, L.eta, gate, L.colpart.as<double>(), L.nblocks_m);
-  lda::launch_colsum_reduce(s, L.colpart.as<double>(), L.nblocks_m, L.k, gate, L.colsum.as<double>());
-  lda::launch_expelogbeta<T>(s, L.lam.as<double>(), L.colsum.as<double>(), L.V, L.k, L.kp, gate,
-                             L.Bp.as<T>(), L.logscale.as<double>());
+  const int64_t nb_all = L.shards * (L.Vs / lda::kRowsPerBlock);
+  if (ranks) {
+    const size_t nbs = (size_t)(L.Vs / lda::kRowsPerBlock);
+    mstep_slice<T>(L, c.rank, rho, scale, gate);
+    RCCL_CHECK(ncclAllGather(L.colpart.as<double>() + (size_t)c.rank * nbs * L.k, L.colpart.p, nbs * L.k,
+                             ncclFloat64, c.comm, s));
+    lda::launch_colsum_reduce(s, L.colpart.as<double>(), nb_all, L.k, gate, L.colsum.as<double>());
+    eeb_slice<T>(L, c.rank, gate);
+    const size_t cnt = (size_t)(L.Vs * L.kp);
+    RCCL_CHECK(ncclGroupStart());
+    RCCL_CHECK(ncclAllGather(L.Bp.as<T>() + (size_t)c.rank * cnt, L.Bp.p, cnt, RcclType<T>::v, c.comm, s));
+    RCCL_CHECK(ncclAllGather(L.logscale.as<double>() + (size_t)c.rank * L.Vs, L.logscale.p, (size_t)L.Vs,
+                             ncclFloat64, c.comm, s));
+    RCCL_CHECK(ncclGroupEnd());
+    L.lam_stale = true;
+  } else {  // one GPU: all slices here (one unless STC_VIRTUAL_SHARDS)
+    for (int r = 0; r < L.shards; ++r) mstep_slice<T>(L, r, rho, scale, gate);
+    lda::launch_colsum_reduce(s, L.colpart.as<double>(), nb_all, L.k, gate, L.colsum.as<double>());
+    for (int r = 0; r < L.shards; ++r) eeb_slice<T>(L, r, gate);
+  }
   if (L.cfg.optimize_doc_concentration)
     lda::launch_update_alpha(s, L.alpha.as<double>(), L.small.as<double>(), L.k, rho);
   record(L, 5);
   if (L.timing) {
     L.ev_pending[L.ev_set] = true;
-    L.ev_set ^= 1;
+    L.ev_set = (L.ev_set + 1) % 3;
   }
   L.cum_docs += n;
   L.cum_entries += E;
@@ -370,17 +489,48 @@ Part upload_members(stc_lda& L, const int64_t* ids, int64_t n) {
 template <typename T>
 void step_ids(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, stc_step_stats* st) {
   require_ready(L);
+  relayout(L);
+  claim_event_set(L);
   record(L, 0);
   const Part p = upload_members<T>(L, ids, n);
-  if (L.timing) harvest(L, L.ev_set ^ 1);  // the previous step has completed (stream order)
+  if (L.timing) harvest_all(L);  // partition() drained the stream
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
   estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1);
   train_tail<T>(L, n, p.E, st);
 }
 
+// sample draw `draw` on the device: per-doc counts (Poisson / Bernoulli), their scans, and (n, E,
+// n_short) into dcnt words 0–2, word 3 = n (all-reduced to the global n by the caller)
+void sample_draw(stc_lda& L, int64_t draw) {
+  Ctx& c = *L.ctx;
+  hipStream_t s = c.stream;
+  const int64_t D = L.corpus->rows;
+  if (D > 0) {
+    lda::launch_sample(s, L.corpus->indptr.as<int64_t>(), D, L.cfg.mini_batch_fraction,
+                       L.cfg.sample_with_replacement, L.cfg.seed, draw, c.rank, L.wave_cap,
+                       L.s_counts.as<int32_t>(), L.s_weights.as<int64_t>(), L.s_short.as<int32_t>());
+    incl_scan<int32_t>(L, L.s_counts.as<int32_t>(), L.s_cincl.as<int32_t>(), D);
+    incl_scan<int64_t>(L, L.s_weights.as<int64_t>(), L.s_wincl.as<int64_t>(), D);
+    incl_scan<int32_t>(L, L.s_short.as<int32_t>(), L.s_sincl.as<int32_t>(), D);
+    // (n, E, n_short) from the scans' last elements: one kernel packs them, one copy to pinned memory
+    lda::launch_last3(s, L.s_cincl.as<int32_t>() + (D - 1), L.s_wincl.as<int64_t>() + (D - 1),
+                      L.s_sincl.as<int32_t>() + (D - 1), L.dcnt.as<int64_t>());
+  } else {  // a rank without documents still takes part in every collective
+    HIP_CHECK(hipMemsetAsync(L.dcnt.p, 0, 3 * sizeof(int64_t), s));
+  }
+  HIP_CHECK(hipMemcpyAsync(L.dcnt.as<int64_t>() + 3, L.dcnt.p, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+}
+
+// [U] OnlineLDAOptimizer.next(): sample a minibatch (device-side), `if (batch.isEmpty()) return this`
+// on the GLOBAL batch, else submitMiniBatch.  Draw d's membership is sampled while step d−1 runs
+// (after its fill_batch, so the count buffers are free) and its global size is all-reduced with
+// step d−1's statistics; the host then waits only on that collective's event — the GPU is still
+// busy with step d−1's M-step when step d is enqueued.  The first draw (or one after an empty
+// batch, set_corpus or init_random) is sampled and counted synchronously.
 template <typename T>
 void next_impl(stc_lda& L, stc_step_stats* st) {
   require_ready(L);
+  relayout(L);
   Ctx& c = *L.ctx;
   hipStream_t s = c.stream;
   const int64_t D = L.corpus->rows;
@@ -390,33 +540,28 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
   L.s_cincl.reserve(4 * D);
   L.s_wincl.reserve(8 * D);
   L.s_sincl.reserve(4 * D);
-  const int64_t it = L.iteration + 1;
-  record(L, 0);
   if (!L.hcnt) HIP_CHECK(hipHostMalloc((void**)&L.hcnt, 4 * sizeof(int64_t), hipHostMallocDefault));
+  if (!L.hpre) HIP_CHECK(hipHostMalloc((void**)&L.hpre, 4 * sizeof(int64_t), hipHostMallocDefault));
+  if (!L.ev_pre) HIP_CHECK(hipEventCreateWithFlags(&L.ev_pre, hipEventDisableTiming));
   L.dcnt.reserve(4 * sizeof(int64_t));
-  if (D > 0) {
-    lda::launch_sample(s, L.corpus->indptr.as<int64_t>(), D, L.cfg.mini_batch_fraction,
-                       L.cfg.sample_with_replacement, L.cfg.seed, it, c.rank, L.wave_cap,
-                       L.s_counts.as<int32_t>(), L.s_weights.as<int64_t>(), L.s_short.as<int32_t>());
-    incl_scan<int32_t>(L, L.s_counts.as<int32_t>(), L.s_cincl.as<int32_t>(), D);
-    incl_scan<int64_t>(L, L.s_weights.as<int64_t>(), L.s_wincl.as<int64_t>(), D);
-    incl_scan<int32_t>(L, L.s_short.as<int32_t>(), L.s_sincl.as<int32_t>(), D);
-    // (n, E, n_short) from the scans' last elements: one kernel packs them, one copy into pinned
-    // memory (three pageable copies cost ≈ 90 µs of idle GPU per step), one sync
-    lda::launch_last3(s, L.s_cincl.as<int32_t>() + (D - 1), L.s_wincl.as<int64_t>() + (D - 1),
-                      L.s_sincl.as<int32_t>() + (D - 1), L.dcnt.as<int64_t>());
-  } else {  // a rank without documents still takes part in every collective below
-    HIP_CHECK(hipMemsetAsync(L.dcnt.p, 0, 3 * sizeof(int64_t), s));
+  const int64_t draw = ++L.draws;
+  claim_event_set(L);
+  record(L, 0);
+  int64_t cnt[4];
+  if (L.pre_valid && L.pre_draw == draw) {
+    HIP_CHECK(hipEventSynchronize(L.ev_pre));
+    std::copy(L.hpre, L.hpre + 4, cnt);
+  } else {
+    sample_draw(L, draw);
+    if (c.comm)
+      RCCL_CHECK(ncclAllReduce(L.dcnt.as<int64_t>() + 3, L.dcnt.as<int64_t>() + 3, 1, ncclInt64, ncclSum, c.comm, s));
+    HIP_CHECK(hipMemcpyAsync(L.hcnt, L.dcnt.p, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    std::copy(L.hcnt, L.hcnt + 4, cnt);
   }
-  // Spark skips a step only when the GLOBAL batch is empty (`batch.isEmpty()` over the whole RDD):
-  // word 3 = Σ_ranks n, so every rank takes the same decision and the collectives stay paired
-  HIP_CHECK(hipMemcpyAsync(L.dcnt.as<int64_t>() + 3, L.dcnt.p, sizeof(int64_t), hipMemcpyDeviceToDevice, s));
-  if (c.comm)
-    RCCL_CHECK(ncclAllReduce(L.dcnt.as<int64_t>() + 3, L.dcnt.as<int64_t>() + 3, 1, ncclInt64, ncclSum, c.comm, s));
-  HIP_CHECK(hipMemcpyAsync(L.hcnt, L.dcnt.p, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
-  const int64_t n = L.hcnt[0], E = L.hcnt[1], ns32 = L.hcnt[2], n_global = L.hcnt[3];
-  if (L.timing) harvest(L, L.ev_set ^ 1);  // the previous step's events have completed
+  L.pre_valid = false;
+  const int64_t n = cnt[0], E = cnt[1], ns32 = cnt[2], n_global = cnt[3];
+  if (L.timing) harvest_all(L);
   // Spark's next(): `if (batch.isEmpty()) return this` — no iteration increment
   if (n_global == 0) {
     if (st) *st = stc_step_stats{};
@@ -428,7 +573,10 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
                            L.s_cincl.as<int32_t>(), L.s_sincl.as<int32_t>(), ns32, L.batch.as<int32_t>(),
                            L.orig.as<int32_t>(), L.nnzp.as<int64_t>());
   slot_offsets(L, n);
-  estep_and_stats<T>(L, n, ns32, E, nullptr, it);
+  sample_draw(L, draw + 1);  // the next draw, counted with this step's collective
+  L.pre_inflight = true;
+  L.pre_draw = draw + 1;
+  estep_and_stats<T>(L, n, ns32, E, nullptr, L.iteration + 1);
   train_tail<T>(L, n, E, st);
 }
 
@@ -436,6 +584,7 @@ template <typename T>
 void estep_only(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, double* gamma_out,
                 double* stat_out, int32_t* iters_out) {
   require_ready(L);
+  relayout(L);
   hipStream_t s = L.ctx->stream;
   const Part p = upload_members<T>(L, ids, n);
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
@@ -508,25 +657,47 @@ void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const
   }
 }
 
+// the full λ on every rank after sharded M-steps: an all-gather of the slices (collective — every
+// rank calls the reader, as every executor calls ldaNext)
+void gather_lambda(stc_lda& L) {
+  if (!L.lam_stale) return;
+  Ctx& c = *L.ctx;
+  const size_t cnt = (size_t)(L.Vs * L.k);
+  RCCL_CHECK(ncclAllGather(L.lam.as<double>() + (size_t)c.rank * cnt, L.lam.p, cnt, ncclFloat64, c.comm, c.stream));
+  HIP_CHECK(hipStreamSynchronize(c.stream));
+  L.lam_stale = false;
+}
+
+// [U] logLikelihoodBound topicsPart: the per-element sum over the rows this rank holds current (its
+// slice when λ is sharded — the caller all-reduces it — else all rows), and separately the
+// per-topic normaliser terms Σ_k (lgamma(η·V) − lgamma(Σ_v λ_vk)) from the global colsum (added once).
 template <typename T>
-double topics_part(stc_lda& L) {
+void topics_part(stc_lda& L, double* elem_part, double* norm_part) {
   hipStream_t s = L.ctx->stream;
   const int64_t nb = 1024;
   L.dtmp.reserve(sizeof(double) * (nb + 1));
   L.scal.reserve(sizeof(double) * 8);
-  lda::launch_topics_bound<T>(s, L.lam.as<double>(), L.colsum.as<double>(), L.V, L.k, L.eta,
-                              L.dtmp.as<double>(), nb);
+  int64_t v0 = 0, vn = L.V;
+  if (L.lam_stale) {
+    v0 = (int64_t)L.ctx->rank * L.Vs;
+    vn = std::max<int64_t>(0, std::min(L.V - v0, L.Vs));
+  }
+  HIP_CHECK(hipMemsetAsync(L.dtmp.p, 0, sizeof(double) * nb, s));
+  if (vn > 0)
+    lda::launch_topics_bound<T>(s, L.lam.as<double>() + v0 * L.k, L.colsum.as<double>(), vn, L.k, L.eta,
+                                L.dtmp.as<double>(), nb);
   lda::launch_sum_f64(s, L.dtmp.as<double>(), nb, L.scal.as<double>() + 3);
   double part = 0.0;
   std::vector<double> cs((size_t)L.k);
   HIP_CHECK(hipMemcpyAsync(&part, L.scal.as<double>() + 3, sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipMemcpyAsync(cs.data(), L.colsum.p, sizeof(double) * L.k, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  // [U] logLikelihoodBound topicsPart, last term: Σ_k (lgamma(sumEta) − lgamma(Σ_v λ_vk)),
   // sumEta = η·V (Dirichlet normaliser of q(β_k|λ_k) minus that of p(β_k|η))
   const double lg_sum_eta = std::lgamma(L.eta * (double)L.V);
-  for (int t = 0; t < L.k; ++t) part += lg_sum_eta - std::lgamma(cs[(size_t)t]);
-  return part;
+  double norm = 0.0;
+  for (int t = 0; t < L.k; ++t) norm += lg_sum_eta - std::lgamma(cs[(size_t)t]);
+  *elem_part = part;
+  *norm_part = norm;
 }
 
 void allreduce_host(Ctx& c, double* x, int64_t n) {
@@ -852,7 +1023,7 @@ void run_tokenizer(Ctx& c, Tokens& t, const uint8_t* text, int64_t n_bytes, cons
   tokenizer::tokenize(c, d_text.as<uint8_t>(), d_off.as<int64_t>(), n_docs, t.utf8, t.tok_off, t.doc_off,
                       t.n_tok, t.n_bytes, bad);
   if (bad >= 0) {
-    char msg[160];
+    char msg[256];
     snprintf(msg, sizeof msg, "Tokenizer: the GPU lower-casing covers U+0000-U+07FF (except U+0130, U+03A3, "
              "U+023A, U+023E) and caseless blocks; unsupported character at byte %lld (lead byte 0x%02X)",
              (long long)bad, (unsigned)text[bad]);
@@ -1021,12 +1192,10 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->cfg.doc_concentration = nullptr;
     L->cfg.doc_concentration_len = 0;
     L->nblocks_m = ceil_div(L->V, lda::kRowsPerBlock);
-    L->lam.reserve(8 * L->V * L->k);
-    L->Bp.reserve(L->tsize * L->V * L->kp);
-    L->stat.reserve(L->tsize * L->V * L->kp);
-    L->logscale.reserve(8 * L->V);
+    const char* vs = std::getenv("STC_VIRTUAL_SHARDS");
+    L->virt = vs ? std::max(1, std::min(64, std::atoi(vs))) : 1;
+    ensure_layout(*L);  // λ, Bp, stat, logscale, colpart for the current shard count
     L->colsum.reserve(8 * L->k);
-    L->colpart.reserve(8 * L->nblocks_m * L->k);
     L->alpha.reserve(8 * L->k);
     L->small.reserve(8 * (L->k + 1));
     L->stats4.reserve(8 * 4);
@@ -1059,6 +1228,7 @@ int stc_lda_set_corpus(stc_lda* L, const stc_dcsr* corpus, int64_t corpus_size_t
                 "corpus_size_total must be >= this rank's rows and > 0");
     L->corpus = corpus;
     L->corpus_total = corpus_size_total;
+    L->pre_valid = false;  // a prefetched draw sampled the previous corpus
   });
 }
 
@@ -1067,8 +1237,11 @@ int stc_lda_init_random(stc_lda* L, uint64_t seed) {
     STC_REQUIRE(L, "lda");
     L->ctx->use();
     lda::launch_init_lambda(L->ctx->stream, L->lam.as<double>(), L->V, L->k, seed, L->cfg.gamma_shape);
+    L->lam_stale = false;
     refresh(*L);
     L->iteration = 0;
+    L->draws = 0;  // a fresh generator, as Spark's initialize()
+    L->pre_valid = false;
     HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
   });
 }
@@ -1087,6 +1260,7 @@ int stc_lda_set_topics(stc_lda* L, const double* topics, int layout) {
         h[(size_t)(v * L->k + t)] = x;
       }
     HIP_CHECK(hipMemcpyAsync(L->lam.p, h.data(), 8 * n, hipMemcpyHostToDevice, L->ctx->stream));
+    L->lam_stale = false;
     refresh(*L);
     HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
   });
@@ -1098,6 +1272,7 @@ int stc_lda_get_topics(stc_lda* L, double* out, int layout) {
     STC_REQUIRE(layout == STC_LAYOUT_VK || layout == STC_LAYOUT_KV, "layout");
     STC_REQUIRE(L->has_topics, "no topics yet");
     L->ctx->use();
+    gather_lambda(*L);
     const int64_t n = L->V * L->k;
     if (layout == STC_LAYOUT_VK) {
       HIP_CHECK(hipMemcpyAsync(out, L->lam.p, 8 * n, hipMemcpyDeviceToHost, L->ctx->stream));
@@ -1179,16 +1354,20 @@ int stc_lda_bound(stc_lda* L, const stc_dcsr* docs, uint64_t gamma_seed, int64_t
   return guard([&] {
     STC_REQUIRE(L && docs, "lda/docs");
     L->ctx->use();
-    double h[2] = {0, 0};
-    double tp = 0;
+    double h[3] = {0, 0, 0};
+    double norm = 0;
+    const bool sharded = L->lam_stale;
     if (L->dtype == STC_F32) {
       infer_impl<float>(*L, *docs, gamma_seed, doc_id_base, gamma0, true, nullptr, h);
-      tp = topics_part<float>(*L);
+      topics_part<float>(*L, h + 2, &norm);
     } else {
       infer_impl<double>(*L, *docs, gamma_seed, doc_id_base, gamma0, true, nullptr, h);
-      tp = topics_part<double>(*L);
+      topics_part<double>(*L, h + 2, &norm);
     }
-    allreduce_host(*L->ctx, h, 2);  // corpusPart and token count are sums over all ranks
+    // corpusPart and the token count are sums over the ranks' documents; the topics part's element
+    // sum too when λ is sharded (each rank holds its slice), else it is already complete everywhere
+    allreduce_host(*L->ctx, h, sharded ? 3 : 2);
+    const double tp = h[2] + norm;
     if (bound_out) *bound_out = h[0] + tp;
     if (corpus_part_out) *corpus_part_out = h[0];
     if (topics_part_out) *topics_part_out = tp;
@@ -1222,6 +1401,7 @@ int stc_lda_describe(stc_lda* L, int32_t max_terms, int32_t* idx_out, double* we
     STC_REQUIRE(L->has_topics, "no topics yet");
     STC_REQUIRE(L->V * L->k < (int64_t(1) << 31), "describe: V*k must be < 2^31");
     L->ctx->use();
+    gather_lambda(*L);
     hipStream_t s = L->ctx->stream;
     const int64_t n = L->V * L->k;
     const int N = (int)std::min<int64_t>(max_terms, L->V);
@@ -1265,7 +1445,7 @@ int stc_lda_enable_timing(stc_lda* L, int on) {
     L->timing = on != 0;
     for (double& a : L->acc_ms) a = 0.0;
     L->timed_steps = 0;
-    L->ev_pending[0] = L->ev_pending[1] = false;
+    L->ev_pending[0] = L->ev_pending[1] = L->ev_pending[2] = false;
   });
 }
 
@@ -1274,8 +1454,7 @@ int stc_lda_phase_times(stc_lda* L, double* ms_out, int64_t* steps_out) {
     STC_REQUIRE(L && ms_out, "lda/ms_out");
     L->ctx->use();
     HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
-    harvest(*L, 0);
-    harvest(*L, 1);
+    harvest_all(*L);
     for (int p = 0; p < 5; ++p) ms_out[p] = L->timed_steps ? L->acc_ms[p] / (double)L->timed_steps : 0.0;
     if (steps_out) *steps_out = L->timed_steps;
   });

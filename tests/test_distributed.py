@@ -2,9 +2,12 @@
 
 The product shards a minibatch by document.  Each rank:
 * runs the E-step on its members;
-* accumulates its partial `stat` (k×V), logphat and non-empty count;
-* joins ONE all-reduce (api.hip train_tail: grouped ncclAllReduce of stat + small);
-* applies the replicated M-step.
+* accumulates its partial `stat` (V×k), logphat and non-empty count;
+* joins a reduce-scatter of `stat` over vocabulary slices of Vs rows (Vs a multiple of the 64-row
+  λ-update block) grouped with the all-reduce of logphat / count (api.hip train_tail);
+* updates λ on its slice, all-gathers the per-block colsum partials (reduced in block order, so every
+  rank holds the same colsum), computes its slice of expElogβ and all-gathers it for the next E-step;
+* gathers λ only when a reader asks (gather_lambda); the bound sums each slice's topics part.
 
 IDF reduces df and m the same way (stc_idf_fit), and the bound reduces its corpus part.  These
 tests run exactly that decomposition with the oracle's per-document primitives on two gloo ranks.
@@ -76,15 +79,42 @@ def _worker(rank, world, port, out_dir):
     docs = [corpus.row(int(batch[i])) for i in mine]
     stat, logphat, n, eeb = _partial_stats(O, lam, alpha, docs, g0[mine])
     small = torch.from_numpy(np.concatenate([logphat, [float(n)]]))
-    st = torch.from_numpy(stat.copy())
-    dist.all_reduce(st)          # ≙ ncclAllReduce(stat)
-    dist.all_reduce(small)       # ≙ ncclAllReduce(small)  (grouped with the above on the GPU)
-    stat_g, logphat_g, n_g = st.numpy(), small.numpy()[:k], int(small.numpy()[k])
-    state = O.OnlineLDAState(lam=lam.copy(), alpha=alpha.copy(), eta=1.0 / k, corpus_size=corpus.num_rows,
-                             mini_batch_fraction=batch.size / corpus.num_rows, optimize_doc_concentration=True)
+    # vocabulary slices: Vs = ⌈⌈V/N⌉/64⌉·64 rows per rank, stat padded with zero rows to N·Vs
+    RB = 64
+    Vs = -(-(-(-V // world)) // RB) * RB
+    v0, vn = rank * Vs, max(0, min(V - rank * Vs, Vs))
+    st = torch.zeros((world * Vs, k), dtype=torch.float64)
+    st[:V] = torch.from_numpy(stat.T)
+    mine_st = torch.zeros((Vs, k), dtype=torch.float64)
+    dist.reduce_scatter_tensor(mine_st, st)   # ≙ ncclReduceScatter(stat)
+    dist.all_reduce(small)                    # ≙ ncclAllReduce(small)  (same group on the GPU)
+    logphat_g, n_g = small.numpy()[:k], int(small.numpy()[k])
+    # the slice's λ update (the oracle's updateLambda on the slice's columns)
+    state = O.OnlineLDAState(lam=lam[:, v0:v0 + vn].copy(), alpha=alpha.copy(), eta=1.0 / k,
+                             corpus_size=corpus.num_rows, mini_batch_fraction=batch.size / corpus.num_rows,
+                             optimize_doc_concentration=True)
     state.iteration += 1
-    O.update_lambda(state, stat_g * eeb.T, int(math.ceil(state.mini_batch_fraction * state.corpus_size)))
+    O.update_lambda(state, mine_st.numpy()[:vn].T * eeb.T[:, v0:v0 + vn],
+                    int(math.ceil(state.mini_batch_fraction * state.corpus_size)))
     O.update_alpha(state, logphat_g / n_g, n_g)
+    # colsum: per-64-row-block partials all-gathered, reduced in block order (identical on all ranks)
+    lam_slice = np.zeros((k, Vs))
+    lam_slice[:, :vn] = state.lam
+    part = torch.from_numpy(np.ascontiguousarray(lam_slice.reshape(k, Vs // RB, RB).sum(axis=2).T))
+    parts = torch.zeros((world * (Vs // RB), k), dtype=torch.float64)
+    dist.all_gather_into_tensor(parts, part)
+    colsum = np.zeros(k)
+    for b in range(parts.shape[0]):
+        colsum += parts[b].numpy()
+    # the slice's expElogβ = exp(ψ(λ) − ψ(colsum)), all-gathered (≙ ncclAllGather of Bp)
+    eeb_slice = np.zeros((Vs, k))
+    eeb_slice[:vn] = np.exp(O.digamma(state.lam) - O.digamma(colsum)[:, None]).T
+    eeb_all = torch.zeros((world * Vs, k), dtype=torch.float64)
+    dist.all_gather_into_tensor(eeb_all, torch.from_numpy(eeb_slice))
+    # a reader's λ (gather_lambda)
+    lam_all = torch.zeros((world * Vs, k), dtype=torch.float64)
+    dist.all_gather_into_tensor(lam_all, torch.from_numpy(np.ascontiguousarray(lam_slice.T)))
+    state.lam = lam_all.numpy()[:V].T.copy()
 
     # --- IDF: df and m reduced over the ranks (stc_idf_fit with a communicator)
     rows = np.array_split(np.arange(corpus.num_rows), world)[rank]
@@ -97,12 +127,19 @@ def _worker(rank, world, port, out_dir):
     mdf = 2
     idf = np.where(df.numpy() >= mdf, np.log((int(m) + 1.0) / (df.numpy() + 1.0)), 0.0)
 
-    # --- bound: corpus part summed over ranks, topics part computed once (replicated λ)
+    # --- bound: corpus part over the rank's documents; topics part: the element sum over the rank's
+    # vocabulary slice (λ sharded), both all-reduced, plus the per-topic normaliser once (api.hip
+    # topics_part / stc_lda_bound)
     bdocs = [corpus.row(int(r)) for r in rows]
     bg0 = np.stack([O.gamma_init(11, int(r), k) for r in rows])
-    _, part, topics_only = O.log_likelihood_bound(bdocs, bg0, lam.T, alpha, 1.0 / k)
-    cp = torch.tensor([part], dtype=torch.float64)
+    _, part, _ = O.log_likelihood_bound(bdocs, bg0, lam.T, alpha, 1.0 / k)
+    eta = 1.0 / k
+    elog_beta = O.dirichlet_expectation(lam)[:, v0:v0 + vn]   # k × slice, ψ(colsum) of the whole λ
+    ls = lam[:, v0:v0 + vn]
+    elem = np.sum((eta - ls) * elog_beta) + np.sum(O.gammaln(ls) - O.gammaln(eta))
+    cp = torch.tensor([part, elem], dtype=torch.float64)
     dist.all_reduce(cp)
+    topics_only = float(cp[1]) + np.sum(O.gammaln(eta * V) - O.gammaln(lam.sum(axis=1)))
 
     # --- RNG independence of the ranks' γ₀ streams (train_doc_key carries the rank)
     key0 = O.gamma_init(5, O.train_doc_key(3, rank, 0), k)
@@ -112,6 +149,7 @@ def _worker(rank, world, port, out_dir):
     dist.broadcast_object_list(uid, src=0)
 
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), lam=state.lam, alpha=state.alpha, idf=idf,
+             eeb=eeb_all.numpy()[:V], colsum=colsum,
              bound=float(cp[0]) + topics_only, key0=key0, uid=np.frombuffer(uid[0], np.uint8))
     dist.barrier()
     dist.destroy_process_group()
@@ -136,9 +174,13 @@ def test_sharded_minibatch_matches_single_process(two_rank_results, oracle):
     r0, r1 = two_rank_results
     # λ and α replicated bit-for-bit on both ranks (same reduced inputs, same M-step)
     assert np.array_equal(r0["lam"], r1["lam"]) and np.array_equal(r0["alpha"], r1["alpha"])
-    # and equal to the unsharded step up to the all-reduce's summation order
+    # and equal to the unsharded step up to the reduction's summation order
     np.testing.assert_allclose(r0["lam"], ref.lam, rtol=1e-12, atol=0)
     np.testing.assert_allclose(r0["alpha"], ref.alpha, rtol=1e-12, atol=0)
+    # the sharded colsum / expElogβ the next E-step reads: identical on both ranks, and the model's
+    assert np.array_equal(r0["colsum"], r1["colsum"]) and np.array_equal(r0["eeb"], r1["eeb"])
+    np.testing.assert_allclose(r0["colsum"], ref.lam.sum(axis=1), rtol=1e-13)
+    np.testing.assert_allclose(r0["eeb"], np.exp(O.dirichlet_expectation(ref.lam)).T, rtol=1e-12)
 
 
 def test_sharded_idf_is_bit_exact(two_rank_results, oracle):

@@ -305,3 +305,60 @@ def test_distributed_model_load_to_local_on_gpu(ctx, oracle, tmp_path):
         cid, cts = docs.row(i)
         exp_t = oracle.topic_distribution(cid, cts, nwk, np.full(k, 11.0), g0[i], eeb)
         np.testing.assert_allclose(theta[i], exp_t, rtol=1e-7, atol=1e-12)
+
+
+def _train(ctx, corpus, k, dtype, steps, reset_each=False, **kw):
+    h, d = _handle(ctx, corpus, k, dtype, None, mini_batch_fraction=0.3, seed=9, **kw)
+    h.init_random(4)
+    for _ in range(steps):
+        if reset_each:  # set_corpus drops the prefetched draw: every step samples synchronously
+            h.set_corpus(d, corpus.num_rows)
+        h.next(stats=False)
+    return h, d
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+@pytest.mark.parametrize("V,shards", [(1000, 3), (100, 4), (4096, 2)])
+def test_sharded_mstep_slices_bit_identical(ctx, monkeypatch, dtype, V, shards):
+    """The multi-GPU M-step's vocabulary slices (ranks' λ / expElogβ rows, colsum partials placed
+    where the one-GPU reduction has them), run on one GPU with STC_VIRTUAL_SHARDS: λ, α, the bound
+    and topicDistribution are bit-identical to the unsliced M-step — including a ragged last slice
+    and slices past V (V = 100 over 4 shards of 64 rows)."""
+    rng = np.random.default_rng(40 + V)
+    corpus = random_corpus(rng, 300, V, 1, 40, empty_every=17)
+    k = 12
+    h1, d1 = _train(ctx, corpus, k, dtype, 6)
+    monkeypatch.setenv("STC_VIRTUAL_SHARDS", str(shards))
+    h2, d2 = _train(ctx, corpus, k, dtype, 6)
+    assert h1.iteration() == h2.iteration() > 0
+    np.testing.assert_array_equal(h1.topics(), h2.topics())
+    np.testing.assert_array_equal(h1.alpha(), h2.alpha())
+    assert h1.bound(d1, gamma_seed=3) == h2.bound(d2, gamma_seed=3)
+    np.testing.assert_array_equal(h1.topic_distribution(d1, gamma_seed=3), h2.topic_distribution(d2, gamma_seed=3))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_prefetched_draws_match_synchronous(ctx, dtype):
+    """next() samples draw d+1 during step d and counts it with step d's collective; dropping the
+    prefetch before every step (set_corpus) samples each draw synchronously: identical models."""
+    rng = np.random.default_rng(44)
+    corpus = random_corpus(rng, 500, 2048, 1, 60, empty_every=11)
+    h1, _ = _train(ctx, corpus, 8, dtype, 7)
+    h2, _ = _train(ctx, corpus, 8, dtype, 7, reset_each=True)
+    assert h1.iteration() == h2.iteration() == 7
+    np.testing.assert_array_equal(h1.topics(), h2.topics())
+    np.testing.assert_array_equal(h1.alpha(), h2.alpha())
+
+
+def test_empty_draws_advance(ctx):
+    """Spark's next() draws a new sample on every call: an empty batch returns without an iteration
+    (`if (batch.isEmpty()) return this`), and the following call samples afresh — a 4-doc corpus at
+    fraction 0.05 is empty most of the time, yet iterations accrue."""
+    rng = np.random.default_rng(45)
+    corpus = random_corpus(rng, 4, 256, 5, 20)
+    h, _ = _handle(ctx, corpus, 3, "f64", None, mini_batch_fraction=0.05, seed=2)
+    h.init_random(1)
+    sizes = [h.next()["batch_docs"] for _ in range(200)]
+    nonempty = sum(1 for x in sizes if x > 0)
+    assert 5 <= nonempty <= 60, nonempty  # Poisson(0.2) over 200 draws: mean ≈ 36
+    assert h.iteration() == nonempty

@@ -6,7 +6,7 @@
 Writes:
   profiles/<tag>_kernel_stats.csv   the --kernel-trace --stats summary (copied)
   profiles/<tag>_pmc.json           per-kernel FETCH/WRITE bytes + SQ counters per dispatch
-  profiles/pmc_traffic.json         E-step-phase HBM bytes per minibatch (bench.py's `traffic`)
+  profiles/pmc_traffic.json         per workload: E-step HBM bytes per launch (bench.py's `traffic`)
 
 FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB from the L2's fabric-side request
 counters, measured in SEPARATE --pmc passes (they do not fit one pass on gfx950).  On gfx950
@@ -103,12 +103,22 @@ def main():
               "estep_kernel_bytes_per_launch": est_bytes}
     with open(os.path.join(out_dir, f"{a.tag}_pmc.json"), "w") as f:
         json.dump(detail, f, indent=1)
-    with open(os.path.join(out_dir, "pmc_traffic.json"), "w") as f:
-        json.dump({"workload": wl, "estep_kernel": sorted(est), "estep_kernel_bytes_per_launch": est_bytes,
-                   "estep_phase_bytes_per_step": per_step, "minibatches_in_run": steps,
-                   "note": f"{a.tag}: FETCH_SIZE x2 + WRITE_SIZE per launch of the training E-step kernel "
-                           f"(and of the whole E-step phase per minibatch), averaged over {steps} minibatches "
-                           f"(incl. burn-in)"}, f, indent=1)
+    # pmc_traffic.json holds one entry per workload (bench.py picks the one matching its run)
+    tp = os.path.join(out_dir, "pmc_traffic.json")
+    try:
+        with open(tp) as f:
+            entries = json.load(f)
+        entries = entries.get("entries", [entries]) if isinstance(entries, dict) else entries
+    except (OSError, ValueError):
+        entries = []
+    entries = [e for e in entries if e.get("workload") != wl]
+    entries.append({"workload": wl, "estep_kernel": sorted(est), "estep_kernel_bytes_per_launch": est_bytes,
+                    "estep_phase_bytes_per_step": per_step, "minibatches_in_run": steps,
+                    "note": f"{a.tag}: FETCH_SIZE x2 + WRITE_SIZE per launch of the training E-step kernel "
+                            f"(and of the whole E-step phase per minibatch), averaged over {steps} minibatches "
+                            f"(incl. burn-in)"})
+    with open(tp, "w") as f:
+        json.dump({"entries": entries}, f, indent=1)
     print(json.dumps({"minibatches": steps, "estep_kernel_bytes_per_launch": est_bytes,
                       "estep_phase_bytes_per_step": per_step}))
     for kn, v in kernels.items():
