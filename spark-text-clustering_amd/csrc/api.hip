@@ -154,8 +154,10 @@ void ensure_layout(stc_lda& L) {
   if ((size_t)(8 * vpad * L.k) > L.lam.bytes) {  // grow λ, keeping its V·k prefix
     DevBuf tmp;
     tmp.reserve(8 * vpad * L.k);
-    HIP_CHECK(hipMemcpyAsync(tmp.p, L.lam.p, 8 * L.V * L.k, hipMemcpyDeviceToDevice, L.ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(L.ctx->stream));
+    if (L.lam.p) {
+      HIP_CHECK(hipMemcpyAsync(tmp.p, L.lam.p, 8 * L.V * L.k, hipMemcpyDeviceToDevice, L.ctx->stream));
+      HIP_CHECK(hipStreamSynchronize(L.ctx->stream));
+    }
     std::swap(tmp.p, L.lam.p);
     std::swap(tmp.bytes, L.lam.bytes);
   }

@@ -7,8 +7,9 @@
 // Layout: the corpus arrives as ONE UTF-8 byte blob + int64 token offsets + int64 doc offsets
 // (plain arrays a JNI caller can hand over without per-string objects).  K1 is one lane per token
 // (byte-wise reads: tokens are 1–20 bytes, the blob is read once, HBM-bound).  K2 sorts each
-// document's bucket ids with a segmented radix sort, flags run heads, scans them, and emits the
-// sorted distinct ids + run lengths — no atomics, so hot terms ("the") cost nothing extra.
+// document's bucket ids inside one wave (registers; hipcub's segmented sort only for documents past
+// 1024 tokens) and emits the sorted distinct ids + run lengths — no atomics on the CSR, so hot terms
+// ("the") cost nothing extra.
 #include <hipcub/hipcub.hpp>
 
 #include "stc_internal.h"
@@ -93,121 +94,260 @@ void hash_tokens(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_
   KERNEL_CHECK();
 }
 
-// head[t] = 1 iff sorted key t starts a run inside its document
-__global__ __launch_bounds__(256) void k_mark_doc_starts(const int64_t* __restrict__ doc_off,
-                                                         int64_t n_docs, int32_t* __restrict__ head) {
-  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d < n_docs; d += (int64_t)gridDim.x * 256) {
-    const int64_t s = doc_off[d];
-    if (s < doc_off[d + 1]) head[s] = 1;
-  }
-}
-__global__ __launch_bounds__(256) void k_heads(const int32_t* __restrict__ keys, int64_t n,
-                                               int32_t* __restrict__ head) {
-  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
-    if (t == 0 || keys[t] != keys[t - 1]) head[t] = 1;  // doc starts were set before
-  }
-}
-// incl = inclusive scan of head; for head tokens write index + run start
-__global__ __launch_bounds__(256) void k_emit(const int32_t* __restrict__ keys,
-                                              const int32_t* __restrict__ head,
-                                              const int32_t* __restrict__ incl, int64_t n,
-                                              int32_t* __restrict__ out_idx,
-                                              int64_t* __restrict__ run_start) {
-  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (int64_t)gridDim.x * 256) {
-    if (head[t]) {
-      const int64_t pos = (int64_t)incl[t] - 1;
-      out_idx[pos] = keys[t];
-      run_start[pos] = t;
+// ---------------------------------------------------------------------------------------
+// K2: per-document sort + run-length count → CSR.  One wave per document.
+//  pass A (k_doc_sort): documents of ≤ kSortCap tokens are bitonic-sorted in registers (P = m/64
+//    keys per lane, m = the next power of two ≥ max(n, 64); partners j ≥ P across lanes by
+//    __shfl_xor, j < P inside the lane), written back sorted, and their distinct ids counted
+//    (ballot popcounts) into nnz[d].  Longer documents are appended to a list for the segmented
+//    radix sort (hipcub), then counted by k_doc_runs<COUNT>.
+//  scan nnz → indptr; pass B (k_doc_runs<EMIT>): each document's sorted keys in 64-key chunks; run
+//    heads by ballot, output slots by mbcnt, run lengths from the next head in the chunk, or, for a
+//    chunk's last run, when the next chunk's first head (or the document end) arrives.
+// No atomics on the output; the large-document list is an atomic append whose order only permutes
+// hipcub's segments, so the CSR is bit-identical run to run.
+// ---------------------------------------------------------------------------------------
+constexpr int kSortCap = 1024;  // ≤ 16 keys per lane
+
+template <int P>
+__device__ __forceinline__ void bitonic_regs(int32_t (&x)[P], int lane, int m) {
+  for (int k = 2; k <= m; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= P) {  // partner in lane ^ (j / P), same register
+        const int lx = j / P;
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+          const int e = lane * P + p;
+          const int32_t o = __shfl_xor(x[p], lx, 64);
+          const bool lower = (e & j) == 0, asc = (e & k) == 0;
+          x[p] = (lower == asc) ? min(x[p], o) : max(x[p], o);
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+          const int q = p ^ j;
+          if (q > p) {
+            const int e = lane * P + p;
+            const bool asc = (e & k) == 0;
+            const int32_t a = x[p], b = x[q];
+            x[p] = asc ? min(a, b) : max(a, b);
+            x[q] = asc ? max(a, b) : min(a, b);
+          }
+        }
+      }
     }
   }
 }
-template <typename V>
-__global__ __launch_bounds__(256) void k_counts(const int64_t* __restrict__ run_start, int64_t nnz,
-                                                int64_t n_tok, int binary, V* __restrict__ vals) {
-  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * 256) {
-    const int64_t e = (p + 1 < nnz) ? run_start[p + 1] : n_tok;
-    vals[p] = binary ? V(1) : V(e - run_start[p]);
+
+template <int P>
+__device__ __forceinline__ int64_t sort_doc(const int32_t* __restrict__ keys, int32_t* __restrict__ sorted,
+                                            int64_t s, int n, int lane) {
+  int32_t x[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int e = lane * P + p;
+    x[p] = e < n ? keys[s + e] : INT32_MAX;  // pads sort last (bucket ids < numFeatures ≤ 2^31 − 1)
   }
+  bitonic_regs<P>(x, lane, P * 64);
+  const int32_t prev_last = __shfl_up(x[P - 1], 1, 64);
+  int heads = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int e = lane * P + p;
+    if (e < n) {
+      sorted[s + e] = x[p];
+      const int32_t prev = p == 0 ? prev_last : x[p - 1];
+      heads += (e == 0 || x[p] != prev) ? 1 : 0;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) heads += __shfl_xor(heads, o, 64);
+  return heads;
 }
-__global__ __launch_bounds__(256) void k_indptr(const int64_t* __restrict__ doc_off, int64_t n_docs,
-                                                const int32_t* __restrict__ incl,
-                                                int64_t* __restrict__ indptr) {
-  for (int64_t d = (int64_t)blockIdx.x * 256 + threadIdx.x; d <= n_docs; d += (int64_t)gridDim.x * 256) {
-    const int64_t s = doc_off[d];
-    indptr[d] = s > 0 ? (int64_t)incl[s - 1] : 0;
+
+__global__ __launch_bounds__(64) void k_doc_sort(const int32_t* __restrict__ keys, const int64_t* __restrict__ doc_off,
+                                                 int64_t n_docs, int32_t* __restrict__ sorted,
+                                                 int64_t* __restrict__ nnz, int32_t* __restrict__ large,
+                                                 int32_t* __restrict__ n_large) {
+  const int lane = threadIdx.x;
+  for (int64_t d = blockIdx.x; d < n_docs; d += gridDim.x) {
+    const int64_t s = doc_off[d], n64 = doc_off[d + 1] - s;
+    if (n64 > kSortCap) {
+      if (lane == 0) large[atomicAdd(n_large, 1)] = (int32_t)d;
+      continue;
+    }
+    const int n = (int)n64;
+    int64_t h = 0;
+    if (n <= 64) h = sort_doc<1>(keys, sorted, s, n, lane);
+    else if (n <= 128) h = sort_doc<2>(keys, sorted, s, n, lane);
+    else if (n <= 256) h = sort_doc<4>(keys, sorted, s, n, lane);
+    else if (n <= 512) h = sort_doc<8>(keys, sorted, s, n, lane);
+    else h = sort_doc<16>(keys, sorted, s, n, lane);
+    if (lane == 0) nnz[d] = h;
   }
 }
 
-static int bits_for(int64_t n) {
-  int b = 1;
-  while ((int64_t(1) << b) < n) ++b;
-  return b;
+// segment bounds of the listed long documents (for hipcub's segmented sort) and their flags
+__global__ __launch_bounds__(256) void k_large_segments(const int32_t* __restrict__ large, int32_t n_large,
+                                                        const int64_t* __restrict__ doc_off,
+                                                        int64_t* __restrict__ beg, int64_t* __restrict__ end,
+                                                        uint8_t* __restrict__ is_large) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n_large) {
+    const int32_t d = large[i];
+    beg[i] = doc_off[d];
+    end[i] = doc_off[d + 1];
+    is_large[d] = 1;
+  }
+}
+
+// the runs of one document's sorted keys, 64 at a time: COUNT → nnz[d]; EMIT → ids + run lengths at
+// indptr[d] (the value is 1 when binary)
+template <bool EMIT, typename V>
+__device__ __forceinline__ void doc_runs(const int32_t* __restrict__ src, int64_t s, int64_t n, int lane,
+                                         int64_t out0, int binary, int32_t* __restrict__ idx,
+                                         V* __restrict__ vals, int64_t* nnz_out) {
+  int64_t done = 0;                  // runs started so far (wave-uniform)
+  int64_t pend_start = -1, pend_slot = 0;
+  int32_t last = 0;                  // the previous chunk's last key
+  for (int64_t c0 = 0; c0 < n; c0 += 64) {
+    const int64_t i = c0 + lane;
+    const bool valid = i < n;
+    const int32_t key = valid ? src[s + i] : 0;
+    int32_t prev = __shfl_up(key, 1, 64);
+    if (lane == 0) prev = last;
+    const bool head = valid && (i == 0 || key != prev);
+    const uint64_t mask = __ballot(head);
+    const int nh = __popcll(mask);
+    if (EMIT) {
+      if (mask != 0 && pend_start >= 0 && lane == 0)  // the open run ends at this chunk's first head
+        vals[out0 + pend_slot] = binary ? V(1) : V(c0 + __ffsll((unsigned long long)mask) - 1 - pend_start);
+      if (head) {
+        const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        const int64_t slot = done + rank;
+        idx[out0 + slot] = key;
+        const uint64_t after = lane == 63 ? 0ull : (mask >> (lane + 1));
+        if (after) vals[out0 + slot] = binary ? V(1) : V(__ffsll((unsigned long long)after));
+      }
+      if (mask != 0) {
+        const int lh = 63 - __clzll((long long)mask);
+        pend_start = c0 + lh;
+        pend_slot = done + nh - 1;
+      }
+    }
+    done += nh;
+    last = __shfl(key, 63, 64);
+  }
+  if (EMIT) {
+    if (pend_start >= 0 && lane == 0) vals[out0 + pend_slot] = binary ? V(1) : V(n - pend_start);
+  } else if (lane == 0) {
+    *nnz_out = done;
+  }
+}
+
+template <bool EMIT, typename V>
+__global__ __launch_bounds__(64) void k_doc_runs(const int32_t* __restrict__ sorted,
+                                                 const int32_t* __restrict__ sorted_l,
+                                                 const uint8_t* __restrict__ is_large,
+                                                 const int32_t* __restrict__ large, int32_t n_large,
+                                                 const int64_t* __restrict__ doc_off, int64_t n_docs,
+                                                 const int64_t* __restrict__ indptr, int binary,
+                                                 int32_t* __restrict__ idx, V* __restrict__ vals,
+                                                 int64_t* __restrict__ nnz) {
+  const int lane = threadIdx.x;
+  const int64_t count = EMIT ? n_docs : n_large;  // COUNT runs over the long documents only
+  for (int64_t w = blockIdx.x; w < count; w += gridDim.x) {
+    const int64_t d = EMIT ? w : large[w];
+    const int64_t s = doc_off[d], n = doc_off[d + 1] - s;
+    const int32_t* src = (is_large && is_large[d]) ? sorted_l : sorted;
+    doc_runs<EMIT, V>(src, s, n, lane, EMIT ? indptr[d] : 0, binary, idx, vals, nnz + d);
+  }
 }
 
 void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t n_tok,
                const int64_t* d_doc_off, int64_t n_docs, int32_t num_features, int binary,
                int variant, int value_dtype, DCsr& out) {
   STC_REQUIRE(n_tok < (int64_t(1) << 31), "at most 2^31-1 tokens per call (split the corpus)");
+  hipStream_t st = c.stream;
   out.rows = n_docs;
   out.cols = num_features;
   out.dtype = value_dtype;
   out.indptr.reserve(sizeof(int64_t) * (n_docs + 1));
   if (n_tok == 0) {
-    HIP_CHECK(hipMemsetAsync(out.indptr.p, 0, sizeof(int64_t) * (n_docs + 1), c.stream));
+    HIP_CHECK(hipMemsetAsync(out.indptr.p, 0, sizeof(int64_t) * (n_docs + 1), st));
     out.nnz = 0;
     return;
   }
-  DevBuf keys, sorted, head, incl, runs, tmp;
+  // grow-only scratch kept on the context (the featurisation of one corpus reuses it)
+  DevBuf& keys = c.scratch[0];
+  DevBuf& sorted = c.scratch[1];
+  DevBuf& nnz = c.scratch[2];
+  DevBuf& small = c.scratch[3];
   keys.reserve(sizeof(int32_t) * n_tok);
   sorted.reserve(sizeof(int32_t) * n_tok);
-  head.reserve(sizeof(int32_t) * n_tok);
-  incl.reserve(sizeof(int32_t) * n_tok);
+  nnz.reserve(sizeof(int64_t) * (n_docs + 1));
+  small.reserve(sizeof(int32_t) * (n_docs + 16));
+  int32_t* n_large_d = small.as<int32_t>();
+  int32_t* large = small.as<int32_t>() + 16;
   hash_tokens(c, d_utf8, d_tok_off, n_tok, num_features, variant, keys.as<int32_t>());
-
-  const int nbits = bits_for(num_features);
-  size_t tb = 0;
-  HIP_CHECK(hipcub::DeviceSegmentedRadixSort::SortKeys(
-      nullptr, tb, keys.as<int32_t>(), sorted.as<int32_t>(), (int)n_tok, (int)n_docs, d_doc_off,
-      d_doc_off + 1, 0, nbits, c.stream));
-  size_t tb2 = 0;
-  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, tb2, head.as<int32_t>(), incl.as<int32_t>(),
-                                             (int)n_tok, c.stream));
-  tmp.reserve(tb > tb2 ? tb : tb2);
-  HIP_CHECK(hipcub::DeviceSegmentedRadixSort::SortKeys(
-      tmp.p, tb, keys.as<int32_t>(), sorted.as<int32_t>(), (int)n_tok, (int)n_docs, d_doc_off,
-      d_doc_off + 1, 0, nbits, c.stream));
-
-  HIP_CHECK(hipMemsetAsync(head.p, 0, sizeof(int32_t) * n_tok, c.stream));
-  k_mark_doc_starts<<<grid_for(n_docs), 256, 0, c.stream>>>(d_doc_off, n_docs, head.as<int32_t>());
+  HIP_CHECK(hipMemsetAsync(n_large_d, 0, sizeof(int32_t), st));
+  const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(n_docs, 1), 1 << 20);
+  k_doc_sort<<<g, 64, 0, st>>>(keys.as<int32_t>(), d_doc_off, n_docs, sorted.as<int32_t>(),
+                               nnz.as<int64_t>() + 1, large, n_large_d);
   KERNEL_CHECK();
-  k_heads<<<grid_for(n_tok), 256, 0, c.stream>>>(sorted.as<int32_t>(), n_tok, head.as<int32_t>());
-  KERNEL_CHECK();
-  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tmp.p, tb2, head.as<int32_t>(), incl.as<int32_t>(),
-                                             (int)n_tok, c.stream));
-  int32_t nnz32 = 0;
-  HIP_CHECK(hipMemcpyAsync(&nnz32, incl.as<int32_t>() + (n_tok - 1), sizeof(int32_t),
-                           hipMemcpyDeviceToHost, c.stream));
-  HIP_CHECK(hipStreamSynchronize(c.stream));
-  const int64_t nnz = nnz32;
-  out.nnz = nnz;
-  out.indices.reserve(sizeof(int32_t) * nnz);
-  out.values.reserve((value_dtype == STC_F32 ? 4 : 8) * nnz);
-  runs.reserve(sizeof(int64_t) * nnz);
-  k_emit<<<grid_for(n_tok), 256, 0, c.stream>>>(sorted.as<int32_t>(), head.as<int32_t>(),
-                                                incl.as<int32_t>(), n_tok, out.indices.as<int32_t>(),
-                                                runs.as<int64_t>());
-  KERNEL_CHECK();
+  int32_t n_large = 0;
+  HIP_CHECK(hipMemcpyAsync(&n_large, n_large_d, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  DevBuf sorted_l, seg, flags, tmp;
+  if (n_large > 0) {  // long documents: hipcub segmented radix sort, then their run counts
+    sorted_l.reserve(sizeof(int32_t) * n_tok);
+    seg.reserve(sizeof(int64_t) * 2 * n_large);
+    flags.reserve(n_docs);
+    HIP_CHECK(hipMemsetAsync(flags.p, 0, n_docs, st));
+    int64_t* beg = seg.as<int64_t>();
+    int64_t* end = beg + n_large;
+    k_large_segments<<<(unsigned)ceil_div(n_large, 256), 256, 0, st>>>(large, n_large, d_doc_off, beg, end,
+                                                                       flags.as<uint8_t>());
+    KERNEL_CHECK();
+    int nbits = 1;  // bucket ids < numFeatures
+    while ((int64_t(1) << nbits) < num_features) ++nbits;
+    size_t tb = 0;
+    HIP_CHECK(hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, tb, keys.as<int32_t>(), sorted_l.as<int32_t>(),
+                                                         (int)n_tok, n_large, beg, end, 0, nbits, st));
+    tmp.reserve(tb);
+    HIP_CHECK(hipcub::DeviceSegmentedRadixSort::SortKeys(tmp.p, tb, keys.as<int32_t>(), sorted_l.as<int32_t>(),
+                                                         (int)n_tok, n_large, beg, end, 0, nbits, st));
+    k_doc_runs<false, float><<<(unsigned)std::min(n_large, 1 << 16), 64, 0, st>>>(
+        sorted.as<int32_t>(), sorted_l.as<int32_t>(), flags.as<uint8_t>(), large, n_large, d_doc_off, n_docs,
+        nullptr, binary, nullptr, nullptr, nnz.as<int64_t>() + 1);
+    KERNEL_CHECK();
+  }
+  // indptr = [0, inclusive scan of nnz]
+  HIP_CHECK(hipMemsetAsync(out.indptr.p, 0, sizeof(int64_t), st));
+  size_t sb = 0;
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, sb, nnz.as<int64_t>() + 1, out.indptr.as<int64_t>() + 1,
+                                             (int)n_docs, st));
+  DevBuf stmp;
+  stmp.reserve(sb);
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(stmp.p, sb, nnz.as<int64_t>() + 1, out.indptr.as<int64_t>() + 1,
+                                             (int)n_docs, st));
+  int64_t total = 0;
+  HIP_CHECK(hipMemcpyAsync(&total, out.indptr.as<int64_t>() + n_docs, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  out.nnz = total;
+  out.indices.reserve(sizeof(int32_t) * std::max<int64_t>(total, 1));
+  out.values.reserve((value_dtype == STC_F32 ? 4 : 8) * std::max<int64_t>(total, 1));
+  const uint8_t* fl = n_large > 0 ? flags.as<uint8_t>() : nullptr;
   if (value_dtype == STC_F32)
-    k_counts<float><<<grid_for(nnz), 256, 0, c.stream>>>(runs.as<int64_t>(), nnz, n_tok, binary,
-                                                         out.values.as<float>());
+    k_doc_runs<true, float><<<g, 64, 0, st>>>(sorted.as<int32_t>(), sorted_l.as<int32_t>(), fl, large, n_large,
+                                              d_doc_off, n_docs, out.indptr.as<int64_t>(), binary,
+                                              out.indices.as<int32_t>(), out.values.as<float>(), nullptr);
   else
-    k_counts<double><<<grid_for(nnz), 256, 0, c.stream>>>(runs.as<int64_t>(), nnz, n_tok, binary,
-                                                          out.values.as<double>());
+    k_doc_runs<true, double><<<g, 64, 0, st>>>(sorted.as<int32_t>(), sorted_l.as<int32_t>(), fl, large, n_large,
+                                               d_doc_off, n_docs, out.indptr.as<int64_t>(), binary,
+                                               out.indices.as<int32_t>(), out.values.as<double>(), nullptr);
   KERNEL_CHECK();
-  k_indptr<<<grid_for(n_docs + 1), 256, 0, c.stream>>>(d_doc_off, n_docs, incl.as<int32_t>(),
-                                                       out.indptr.as<int64_t>());
-  KERNEL_CHECK();
-  HIP_CHECK(hipStreamSynchronize(c.stream));  // scratch buffers die at scope exit
+  if (n_large > 0) HIP_CHECK(hipStreamSynchronize(st));  // the long-document buffers die at scope exit
 }
 
 }  // namespace hashing

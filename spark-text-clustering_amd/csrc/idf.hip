@@ -5,11 +5,8 @@
 // :180-192 (tf × idf with the idf==0 → 1e-4 floor).
 //
 // df is a column histogram of a Zipf-skewed CSR: the hottest term sits in nearly every row, so
-// per-entry atomics would serialise on a handful of addresses.  Instead the (value > 0) column
-// ids are radix-sorted (contention-free, deterministic) and each run's [lo, hi) is recorded:
-// df[j] = hi[j] − lo[j].  Bytes: 4·nnz read + ~3 radix passes; the result is exact int64.
-#include <hipcub/hipcub.hpp>
-
+// per-entry global atomics would serialise on a handful of addresses.  k_df_hist pre-aggregates
+// each workgroup's slice in LDS (see there); bytes: the CSR's indices + values read once.
 #include "stc_internal.h"
 
 namespace stc {
@@ -22,65 +19,61 @@ static int grid_for(int64_t n) {
   return (int)g;
 }
 
+// df[j] += 1 for every entry with value > 0 (DocumentFrequencyAggregator.add: rows hold each id
+// once).  Each workgroup counts a contiguous slice of entries in an LDS hash table (open addressing,
+// ≤ 8 probes, claimed by CAS) and flushes it with one global atomic per distinct id: a Zipf corpus's
+// hot ids — present in almost every row — cost one global atomic per workgroup instead of one per
+// row.  Ids that find no slot add to the global count directly.  Integer adds: exact and
+// order-independent, so df is identical run to run.
+constexpr int kDfSlots = 8192;
+constexpr int kDfThreads = 1024;
+
 template <typename V>
-__global__ __launch_bounds__(256) void k_keys(const int32_t* __restrict__ idx,
-                                              const V* __restrict__ val, int64_t nnz,
-                                              uint32_t sentinel, uint32_t* __restrict__ keys) {
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < nnz; e += (int64_t)gridDim.x * 256)
-    keys[e] = val[e] > V(0) ? (uint32_t)idx[e] : sentinel;  // DocumentFrequencyAggregator: values > 0
-}
-
-__global__ __launch_bounds__(256) void k_runs(const uint32_t* __restrict__ k, int64_t n,
-                                              uint32_t sentinel, int64_t* __restrict__ lo,
-                                              int64_t* __restrict__ hi) {
-  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < n; p += (int64_t)gridDim.x * 256) {
-    const uint32_t v = k[p];
-    if (v == sentinel) continue;
-    if (p == 0 || k[p - 1] != v) lo[v] = p;
-    if (p == n - 1 || k[p + 1] != v) hi[v] = p + 1;
+__global__ __launch_bounds__(kDfThreads) void k_df_hist(const int32_t* __restrict__ idx, const V* __restrict__ val,
+                                                        int64_t nnz, int64_t per_block,
+                                                        unsigned long long* __restrict__ df) {
+  __shared__ int32_t key[kDfSlots];
+  __shared__ uint32_t cnt[kDfSlots];
+  for (int i = threadIdx.x; i < kDfSlots; i += kDfThreads) {
+    key[i] = -1;
+    cnt[i] = 0;
   }
-}
-
-__global__ __launch_bounds__(256) void k_df(const int64_t* __restrict__ lo,
-                                            const int64_t* __restrict__ hi, int64_t cols,
-                                            int64_t* __restrict__ df) {
-  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < cols; j += (int64_t)gridDim.x * 256)
-    df[j] = hi[j] - lo[j];
+  __syncthreads();
+  const int64_t e0 = (int64_t)blockIdx.x * per_block;
+  const int64_t e1 = e0 + per_block < nnz ? e0 + per_block : nnz;
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += kDfThreads) {
+    if (!(val[e] > V(0))) continue;
+    const int32_t id = idx[e];
+    uint32_t h = ((uint32_t)id * 2654435761u) >> 19;  // 13 bits
+    bool done = false;
+    for (int probe = 0; probe < 8 && !done; ++probe, h = (h + 1) & (kDfSlots - 1)) {
+      const int32_t k = atomicCAS(&key[h], -1, id);
+      if (k == -1 || k == id) {
+        atomicAdd(&cnt[h], 1u);
+        done = true;
+      }
+    }
+    if (!done) atomicAdd(&df[id], 1ull);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kDfSlots; i += kDfThreads)
+    if (key[i] >= 0) atomicAdd(&df[key[i]], (unsigned long long)cnt[i]);
 }
 
 void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df) {
   HIP_CHECK(hipMemsetAsync(d_df, 0, sizeof(int64_t) * m.cols, c.stream));
   if (m.nnz == 0) return;
-  STC_REQUIRE(m.nnz < (int64_t(1) << 31), "idf: at most 2^31-1 entries per call");
-  const uint32_t sentinel = (uint32_t)m.cols;
-  int nbits = 1;
-  while ((int64_t(1) << nbits) <= (int64_t)sentinel) ++nbits;
-  DevBuf keys, sorted, lo, hi, tmp;
-  keys.reserve(4 * m.nnz);
-  sorted.reserve(4 * m.nnz);
-  lo.reserve(8 * m.cols);
-  hi.reserve(8 * m.cols);
+  // ≈ 2 workgroups per CU, each a contiguous slice (hot ids repeat within it)
+  const int64_t blocks = std::min<int64_t>(512, ceil_div(m.nnz, (int64_t)kDfThreads));
+  const int64_t per = ceil_div(m.nnz, blocks);
+  auto* df = reinterpret_cast<unsigned long long*>(d_df);
   if (m.dtype == STC_F32)
-    k_keys<float><<<grid_for(m.nnz), 256, 0, c.stream>>>(m.indices.as<int32_t>(), m.values.as<float>(),
-                                                         m.nnz, sentinel, keys.as<uint32_t>());
+    k_df_hist<float><<<(unsigned)blocks, kDfThreads, 0, c.stream>>>(m.indices.as<int32_t>(), m.values.as<float>(),
+                                                                     m.nnz, per, df);
   else
-    k_keys<double><<<grid_for(m.nnz), 256, 0, c.stream>>>(m.indices.as<int32_t>(), m.values.as<double>(),
-                                                          m.nnz, sentinel, keys.as<uint32_t>());
+    k_df_hist<double><<<(unsigned)blocks, kDfThreads, 0, c.stream>>>(m.indices.as<int32_t>(), m.values.as<double>(),
+                                                                      m.nnz, per, df);
   KERNEL_CHECK();
-  size_t tb = 0;
-  HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, keys.as<uint32_t>(), sorted.as<uint32_t>(),
-                                              (int)m.nnz, 0, nbits, c.stream));
-  tmp.reserve(tb);
-  HIP_CHECK(hipcub::DeviceRadixSort::SortKeys(tmp.p, tb, keys.as<uint32_t>(), sorted.as<uint32_t>(),
-                                              (int)m.nnz, 0, nbits, c.stream));
-  HIP_CHECK(hipMemsetAsync(lo.p, 0, 8 * m.cols, c.stream));
-  HIP_CHECK(hipMemsetAsync(hi.p, 0, 8 * m.cols, c.stream));
-  k_runs<<<grid_for(m.nnz), 256, 0, c.stream>>>(sorted.as<uint32_t>(), m.nnz, sentinel,
-                                                lo.as<int64_t>(), hi.as<int64_t>());
-  KERNEL_CHECK();
-  k_df<<<grid_for(m.cols), 256, 0, c.stream>>>(lo.as<int64_t>(), hi.as<int64_t>(), m.cols, d_df);
-  KERNEL_CHECK();
-  HIP_CHECK(hipStreamSynchronize(c.stream));
 }
 
 // DocumentFrequencyAggregator.idf(): df >= minDocFreq ? ln((m + 1) / (df + 1)) : 0

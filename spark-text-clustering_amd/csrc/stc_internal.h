@@ -103,6 +103,7 @@ struct Ctx {
   ncclComm_t comm = nullptr;
   int n_ranks = 1;
   int rank = 0;
+  DevBuf scratch[4];  // grow-only scratch of the featurisation kernels (hashing_tf.hip)
   void use() const { HIP_CHECK(hipSetDevice(device)); }
 };
 

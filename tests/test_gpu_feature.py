@@ -136,3 +136,40 @@ def test_device_resident_tokens_synthetic_dictionary(ctx, oracle):
     docs = [[raw[tok_off[t]:tok_off[t + 1]] for t in range(doc_off[i], doc_off[i + 1])] for i in range(300)]
     ip, ix, vv = oracle.hashing_tf(docs, 1 << 18, False, oracle.HASH_SPARK24)
     assert np.array_equal(got.indptr, ip) and np.array_equal(got.indices, ix) and np.array_equal(got.values, vv)
+
+
+@pytest.mark.parametrize("nf", [1 << 18, 97])
+def test_hashing_tf_document_lengths(ctx, oracle, nf):
+    """Every per-document sort path of K2 (hashing_tf.hip): register bitonic sorts of 1/2/4/8/16 keys
+    per lane at both sides of each size boundary, the segmented radix sort past 1024 tokens, a long
+    document of one repeated token, and runs that cross 64-key emit chunks."""
+    import stc
+
+    rng = np.random.default_rng(21)
+    lens = [0, 1, 2, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 1023, 1024, 1025, 3000, 20000]
+    vocab = [f"w{i}" for i in range(5000)]
+    docs = [[vocab[j] for j in rng.zipf(1.3, n) % len(vocab)] for n in lens]
+    docs.append(["same"] * 2000)
+    docs.append(["a", "b"] * 700)
+    rng.shuffle(docs)
+    out = stc.HashingTF(numFeatures=nf, ctx=ctx).transform(docs)
+    ip, ix, vv = oracle.hashing_tf(docs, nf, False, oracle.HASH_SPARK24)
+    assert np.array_equal(out.indptr, ip)
+    assert np.array_equal(out.indices, ix)
+    assert np.array_equal(out.values, vv)
+
+
+def test_idf_doc_freq_zipf_hot_ids(ctx):
+    """k_df_hist: LDS-aggregated document frequencies on a Zipf corpus (hot ids in every row, more
+    distinct ids per workgroup slice than LDS slots) equal the exact column counts of positive values."""
+    import stc
+    from stc import synth
+
+    corpus = synth.zipf_corpus(40000, 200, 1 << 18, seed=3)
+    vals = corpus.values.copy()
+    vals[::7] = 0.0  # explicit zeros do not count
+    tf = stc.CsrMatrix(corpus.indptr, corpus.indices, vals, corpus.num_cols)
+    m = stc.IDF(minDocFreq=0, ctx=ctx).fit(tf)
+    df = np.bincount(tf.indices[vals > 0], minlength=tf.num_cols)
+    assert np.array_equal(m.docFreq, df)
+    assert m.numDocs == 40000
