@@ -894,7 +894,7 @@ void upload_tokens(Ctx& c, TokenUpload& u, const uint8_t* utf8, int64_t n_bytes,
     STC_REQUIRE(doc_off[0] == 0 && doc_off[n_docs] == n_tok, "doc_off must span [0, n_tok]");
     for (int64_t d = 0; d < n_docs; ++d) STC_REQUIRE(doc_off[d + 1] >= doc_off[d], "doc_off must be non-decreasing");
   }
-  u.utf8.reserve(std::max<int64_t>(n_bytes, 1));
+  u.utf8.reserve(n_bytes + 16);  // k_hash reads whole aligned dwords up to 8 bytes past a token
   u.tok_off.reserve(8 * (n_tok + 1));
   if (n_bytes) HIP_CHECK(hipMemcpyAsync(u.utf8.p, utf8, n_bytes, hipMemcpyHostToDevice, c.stream));
   HIP_CHECK(hipMemcpyAsync(u.tok_off.p, tok_off, 8 * (n_tok + 1), hipMemcpyHostToDevice, c.stream));

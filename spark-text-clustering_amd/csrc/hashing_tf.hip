@@ -38,42 +38,61 @@ __device__ __forceinline__ uint32_t fmix(uint32_t h1, uint32_t len) {
   return h1;
 }
 
-// MurmurHash3_x86_32(seed 42).  SPARK24 = Spark 2.4 hashUnsafeBytes (each tail byte
-// sign-extended and mixed as a block); otherwise the standard tail (Spark 3 hashUnsafeBytes2).
+// MurmurHash3_x86_32(seed 42) of n bytes at p.  SPARK24 = Spark 2.4 hashUnsafeBytes (each tail
+// byte sign-extended and mixed as a block); otherwise the standard tail (Spark 3 hashUnsafeBytes2).
+// The bytes are read as whole aligned dwords (the buffers carry ≥ 8 bytes of padding) and realigned
+// with v_alignbyte: a byte load per character was the kernel's issue bottleneck.
 template <bool SPARK24>
 __device__ __forceinline__ int32_t murmur3(const uint8_t* p, uint32_t n) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  const uint32_t sh = (uint32_t)(a & 3);
   uint32_t h1 = 42u;
+  uint32_t cur = w[0];
   const uint32_t nb = n & ~3u;
   for (uint32_t i = 0; i < nb; i += 4) {
-    const uint32_t k1 = (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8) | ((uint32_t)p[i + 2] << 16) |
-                        ((uint32_t)p[i + 3] << 24);
-    h1 = mix_h1(h1, mix_k1(k1));
+    const uint32_t nxt = w[(i >> 2) + 1];
+    h1 = mix_h1(h1, mix_k1(__builtin_amdgcn_alignbyte(nxt, cur, sh)));
+    cur = nxt;
   }
-  if (SPARK24) {
-    for (uint32_t i = nb; i < n; ++i) h1 = mix_h1(h1, mix_k1((uint32_t)(int32_t)(int8_t)p[i]));
-  } else {
-    const uint32_t tail = n - nb;
-    uint32_t k1 = 0;
-    if (tail >= 3) k1 ^= (uint32_t)p[nb + 2] << 16;
-    if (tail >= 2) k1 ^= (uint32_t)p[nb + 1] << 8;
-    if (tail >= 1) {
-      k1 ^= (uint32_t)p[nb];
-      h1 ^= mix_k1(k1);
+  const uint32_t tail = n - nb;
+  if (tail) {
+    const uint32_t t = __builtin_amdgcn_alignbyte(w[(nb >> 2) + 1], cur, sh);  // bytes nb.. in order
+    if (SPARK24) {
+      for (uint32_t i = 0; i < tail; ++i)
+        h1 = mix_h1(h1, mix_k1((uint32_t)(int32_t)(int8_t)(t >> (8 * i))));
+    } else {
+      h1 ^= mix_k1(t & (0xFFFFFFFFu >> (8 * (4 - tail))));
     }
   }
   return (int32_t)fmix(h1, n);
 }
 
+// four tokens per thread and step, a grid stride apart (neighbouring lanes keep neighbouring tokens,
+// so the byte loads stay coalesced) — four independent offset → bytes → hash chains in flight
 template <bool SPARK24>
 __global__ __launch_bounds__(256) void k_hash(const uint8_t* __restrict__ utf8,
                                               const int64_t* __restrict__ tok_off, int64_t n_tok,
                                               int32_t num_features, int32_t* __restrict__ out) {
-  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < n_tok;
-       t += (int64_t)gridDim.x * 256) {
-    const int64_t b = tok_off[t];
-    const int32_t h = murmur3<SPARK24>(utf8 + b, (uint32_t)(tok_off[t + 1] - b));
-    int32_t raw = h % num_features;  // Utils.nonNegativeMod (Java % truncates toward zero)
-    out[t] = raw + (raw < 0 ? num_features : 0);
+  const int64_t S = (int64_t)gridDim.x * 256;
+  for (int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x; t0 < n_tok; t0 += 4 * S) {
+    int64_t b[4], e[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t t = t0 + q * S < n_tok ? t0 + q * S : n_tok - 1;
+      b[q] = tok_off[t];
+      e[q] = tok_off[t + 1];
+    }
+    int32_t h[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) h[q] = murmur3<SPARK24>(utf8 + b[q], (uint32_t)(e[q] - b[q]));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (t0 + q * S < n_tok) {
+        const int32_t raw = h[q] % num_features;  // Utils.nonNegativeMod (Java % truncates toward zero)
+        out[t0 + q * S] = raw + (raw < 0 ? num_features : 0);
+      }
+    }
   }
 }
 
@@ -87,10 +106,11 @@ static int grid_for(int64_t n, int64_t per_block = 256, int64_t cap = 256 * 16) 
 void hash_tokens(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t n_tok,
                  int32_t num_features, int variant, int32_t* d_idx) {
   if (n_tok == 0) return;
+  const int g = grid_for(ceil_div(n_tok, (int64_t)4), 256, 256 * 32);
   if (variant == STC_HASH_SPARK24)
-    k_hash<true><<<grid_for(n_tok), 256, 0, c.stream>>>(d_utf8, d_tok_off, n_tok, num_features, d_idx);
+    k_hash<true><<<g, 256, 0, c.stream>>>(d_utf8, d_tok_off, n_tok, num_features, d_idx);
   else
-    k_hash<false><<<grid_for(n_tok), 256, 0, c.stream>>>(d_utf8, d_tok_off, n_tok, num_features, d_idx);
+    k_hash<false><<<g, 256, 0, c.stream>>>(d_utf8, d_tok_off, n_tok, num_features, d_idx);
   KERNEL_CHECK();
 }
 
@@ -110,8 +130,11 @@ void hash_tokens(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_
 constexpr int kSortCap = 1024;  // ≤ 16 keys per lane
 
 template <int P>
-__device__ __forceinline__ void bitonic_regs(int32_t (&x)[P], int lane, int m) {
+__device__ __forceinline__ void bitonic_regs(int32_t (&x)[P], int lane) {
+  constexpr int m = 64 * P;  // fully unrolled: every partner distance is a constant
+#pragma unroll
   for (int k = 2; k <= m; k <<= 1) {
+#pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
       if (j >= P) {  // partner in lane ^ (j / P), same register
         const int lx = j / P;
@@ -148,7 +171,7 @@ __device__ __forceinline__ int64_t sort_doc(const int32_t* __restrict__ keys, in
     const int e = lane * P + p;
     x[p] = e < n ? keys[s + e] : INT32_MAX;  // pads sort last (bucket ids < numFeatures ≤ 2^31 − 1)
   }
-  bitonic_regs<P>(x, lane, P * 64);
+  bitonic_regs<P>(x, lane);
   const int32_t prev_last = __shfl_up(x[P - 1], 1, 64);
   int heads = 0;
 #pragma unroll
@@ -164,12 +187,16 @@ __device__ __forceinline__ int64_t sort_doc(const int32_t* __restrict__ keys, in
   return heads;
 }
 
-__global__ __launch_bounds__(64) void k_doc_sort(const int32_t* __restrict__ keys, const int64_t* __restrict__ doc_off,
-                                                 int64_t n_docs, int32_t* __restrict__ sorted,
-                                                 int64_t* __restrict__ nnz, int32_t* __restrict__ large,
-                                                 int32_t* __restrict__ n_large) {
-  const int lane = threadIdx.x;
-  for (int64_t d = blockIdx.x; d < n_docs; d += gridDim.x) {
+constexpr int kDocWaves = 4;  // documents in flight per workgroup (one per wave)
+
+__global__ __launch_bounds__(64 * kDocWaves) void k_doc_sort(const int32_t* __restrict__ keys,
+                                                            const int64_t* __restrict__ doc_off, int64_t n_docs,
+                                                            int32_t* __restrict__ sorted, int64_t* __restrict__ nnz,
+                                                            int32_t* __restrict__ large,
+                                                            int32_t* __restrict__ n_large) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t d = (int64_t)blockIdx.x * kDocWaves + (threadIdx.x >> 6); d < n_docs;
+       d += (int64_t)gridDim.x * kDocWaves) {
     const int64_t s = doc_off[d], n64 = doc_off[d + 1] - s;
     if (n64 > kSortCap) {
       if (lane == 0) large[atomicAdd(n_large, 1)] = (int32_t)d;
@@ -246,7 +273,7 @@ __device__ __forceinline__ void doc_runs(const int32_t* __restrict__ src, int64_
 }
 
 template <bool EMIT, typename V>
-__global__ __launch_bounds__(64) void k_doc_runs(const int32_t* __restrict__ sorted,
+__global__ __launch_bounds__(64 * kDocWaves) void k_doc_runs(const int32_t* __restrict__ sorted,
                                                  const int32_t* __restrict__ sorted_l,
                                                  const uint8_t* __restrict__ is_large,
                                                  const int32_t* __restrict__ large, int32_t n_large,
@@ -254,9 +281,10 @@ __global__ __launch_bounds__(64) void k_doc_runs(const int32_t* __restrict__ sor
                                                  const int64_t* __restrict__ indptr, int binary,
                                                  int32_t* __restrict__ idx, V* __restrict__ vals,
                                                  int64_t* __restrict__ nnz) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const int64_t count = EMIT ? n_docs : n_large;  // COUNT runs over the long documents only
-  for (int64_t w = blockIdx.x; w < count; w += gridDim.x) {
+  for (int64_t w = (int64_t)blockIdx.x * kDocWaves + (threadIdx.x >> 6); w < count;
+       w += (int64_t)gridDim.x * kDocWaves) {
     const int64_t d = EMIT ? w : large[w];
     const int64_t s = doc_off[d], n = doc_off[d + 1] - s;
     const int32_t* src = (is_large && is_large[d]) ? sorted_l : sorted;
@@ -291,8 +319,8 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
   int32_t* large = small.as<int32_t>() + 16;
   hash_tokens(c, d_utf8, d_tok_off, n_tok, num_features, variant, keys.as<int32_t>());
   HIP_CHECK(hipMemsetAsync(n_large_d, 0, sizeof(int32_t), st));
-  const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(n_docs, 1), 1 << 20);
-  k_doc_sort<<<g, 64, 0, st>>>(keys.as<int32_t>(), d_doc_off, n_docs, sorted.as<int32_t>(),
+  const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(ceil_div(n_docs, kDocWaves), 1), 1 << 14);
+  k_doc_sort<<<g, 64 * kDocWaves, 0, st>>>(keys.as<int32_t>(), d_doc_off, n_docs, sorted.as<int32_t>(),
                                nnz.as<int64_t>() + 1, large, n_large_d);
   KERNEL_CHECK();
   int32_t n_large = 0;
@@ -317,7 +345,7 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
     tmp.reserve(tb);
     HIP_CHECK(hipcub::DeviceSegmentedRadixSort::SortKeys(tmp.p, tb, keys.as<int32_t>(), sorted_l.as<int32_t>(),
                                                          (int)n_tok, n_large, beg, end, 0, nbits, st));
-    k_doc_runs<false, float><<<(unsigned)std::min(n_large, 1 << 16), 64, 0, st>>>(
+    k_doc_runs<false, float><<<(unsigned)std::min<int64_t>(ceil_div((int64_t)n_large, (int64_t)kDocWaves), 1 << 14), 64 * kDocWaves, 0, st>>>(
         sorted.as<int32_t>(), sorted_l.as<int32_t>(), flags.as<uint8_t>(), large, n_large, d_doc_off, n_docs,
         nullptr, binary, nullptr, nullptr, nnz.as<int64_t>() + 1);
     KERNEL_CHECK();
@@ -339,11 +367,11 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
   out.values.reserve((value_dtype == STC_F32 ? 4 : 8) * std::max<int64_t>(total, 1));
   const uint8_t* fl = n_large > 0 ? flags.as<uint8_t>() : nullptr;
   if (value_dtype == STC_F32)
-    k_doc_runs<true, float><<<g, 64, 0, st>>>(sorted.as<int32_t>(), sorted_l.as<int32_t>(), fl, large, n_large,
+    k_doc_runs<true, float><<<g, 64 * kDocWaves, 0, st>>>(sorted.as<int32_t>(), sorted_l.as<int32_t>(), fl, large, n_large,
                                               d_doc_off, n_docs, out.indptr.as<int64_t>(), binary,
                                               out.indices.as<int32_t>(), out.values.as<float>(), nullptr);
   else
-    k_doc_runs<true, double><<<g, 64, 0, st>>>(sorted.as<int32_t>(), sorted_l.as<int32_t>(), fl, large, n_large,
+    k_doc_runs<true, double><<<g, 64 * kDocWaves, 0, st>>>(sorted.as<int32_t>(), sorted_l.as<int32_t>(), fl, large, n_large,
                                                d_doc_off, n_docs, out.indptr.as<int64_t>(), binary,
                                                out.indices.as<int32_t>(), out.values.as<double>(), nullptr);
   KERNEL_CHECK();

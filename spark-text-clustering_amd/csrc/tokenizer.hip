@@ -186,7 +186,7 @@ void tokenize(Ctx& c, const uint8_t* d_text, const int64_t* d_text_off, int64_t 
   n_out_bytes = h[1];
   bad_pos = h[2];  // -1 (all ones) when every character is supported
   if (bad_pos >= 0) return;
-  out_utf8.reserve(std::max<int64_t>(n_out_bytes, 1));
+  out_utf8.reserve(n_out_bytes + 16);  // k_hash reads whole aligned dwords past a token
   out_tok_off.reserve(8 * (n_tok + 1));
   if (n_docs > 0) {
     k_emit<<<grid_docs(n_docs), 64 * kWaves, 0, s>>>(d_text, d_text_off, n_docs,

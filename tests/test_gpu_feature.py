@@ -159,17 +159,19 @@ def test_hashing_tf_document_lengths(ctx, oracle, nf):
     assert np.array_equal(out.values, vv)
 
 
-def test_idf_doc_freq_zipf_hot_ids(ctx):
-    """k_df_hist: LDS-aggregated document frequencies on a Zipf corpus (hot ids in every row, more
-    distinct ids per workgroup slice than LDS slots) equal the exact column counts of positive values."""
+@pytest.mark.parametrize("V", [1 << 18, 1 << 20])
+def test_idf_doc_freq_zipf_hot_ids(ctx, V):
+    """doc_freq: heavy-hitter document frequencies on a Zipf corpus (hot ids in every row, more
+    distinct ids per workgroup slice than LDS slots) equal the exact column counts of positive values;
+    2^18 buckets take the LDS vocabulary tiles, 2^20 the radix-sorted runs."""
     import stc
     from stc import synth
 
-    corpus = synth.zipf_corpus(40000, 200, 1 << 18, seed=3)
+    corpus = synth.zipf_corpus(40000 if V <= 1 << 18 else 5000, 200, V, seed=3)
     vals = corpus.values.copy()
     vals[::7] = 0.0  # explicit zeros do not count
     tf = stc.CsrMatrix(corpus.indptr, corpus.indices, vals, corpus.num_cols)
     m = stc.IDF(minDocFreq=0, ctx=ctx).fit(tf)
     df = np.bincount(tf.indices[vals > 0], minlength=tf.num_cols)
     assert np.array_equal(m.docFreq, df)
-    assert m.numDocs == 40000
+    assert m.numDocs == tf.num_rows
