@@ -229,8 +229,8 @@ def featurization(stc, ctx, a, log, tokens, reps=3):
     b_tr = nnz * (4 + 8 + 8) + 8.0 * V
     total = float(t.sum())
     return {
-        "label": "featurisation: HashingTF(2^18, spark24 murmur3) -> IDF(2).fit -> transform(1e-4 floor), "
-                 "tokens resident in HBM",
+        "label": f"featurisation: HashingTF(2^{int(V).bit_length() - 1}, spark24 murmur3) -> IDF(2).fit -> "
+                 "transform(1e-4 floor), tokens resident in HBM",
         "value": n_tok / total, "unit": "tokens/s", "dtype": "f64 (values), int32 (indices)",
         "corpus": f"{n_docs} docs x {n_tok // max(1, n_docs)} tokens, Zipf(1) over a seeded 2^18-word "
                   f"dictionary (1-12 chars, 1-4 byte UTF-8: every murmur3 tail length)",

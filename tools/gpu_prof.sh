@@ -5,7 +5,7 @@
 # Summarise afterwards (here): python tools/pmc_summary.py gpurun_out/prof --tag rNN
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/prof; rm -rf $OUT; mkdir -p $OUT
+OUT=${PROF_OUT:-gpurun_out/prof}; rm -rf $OUT; mkdir -p $OUT
 B="bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-hbm-copy --no-secondary ${BENCH_ARGS:-}"
 PASSES=${PROF_PASSES:-"stats fetch write sq grbm"}
 run() {  # run NAME SECONDS ARGS...
