@@ -265,8 +265,12 @@ def run_state(stc, ctx, dcorp, a, dtype, total, lam0, barrier, log, steps, warmu
             "mean_inner_iters": (cc1["inner_iters"] - cc0["inner_iters"]) / max(1, cc1["docs"] - cc0["docs"]),
             "minibatches": n_cold}
     burn = max(0, a.state_minibatches - n_cold - warmup)
-    for _ in range(burn + warmup):
+    log(f"{burn + warmup} untimed minibatches ({dtype})")
+    for i in range(burn + warmup):
         h.next(stats=False)
+        if i % 4 == 3:  # progress (a profiler pass serialises kernels: keep the log moving)
+            ctx.synchronize()
+            log(f"  minibatch {n_cold + i + 1}")
     ctx.synchronize()
     c0 = h.counters()
     h.enable_timing(True)
