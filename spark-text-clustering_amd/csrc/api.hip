@@ -62,6 +62,7 @@ struct stc_lda {
   // bit-identical to the one-GPU reduction.  virt > 1 runs the same slices on one GPU without
   // collectives (STC_VIRTUAL_SHARDS, for testing the slicing).
   int shards = 1, virt = 1;
+  bool force_coll = false;  // STC_COLLECTIVE_MSTEP=1: the RCCL slice path even on a 1-rank communicator (tests)
   int64_t Vs = 0, vpad = 0;
   bool lam_stale = false;  // rows outside this rank's slice are out of date (sharded M-step)
 
@@ -145,7 +146,7 @@ void claim_event_set(stc_lda& L) {
 // chunks); the padded rows of stat are zero, those of λ / Bp never read.  Called before a step; a
 // change of shard count (comm initialised after the handle) keeps λ and recomputes the rest.
 void ensure_layout(stc_lda& L) {
-  const int want = L.ctx->comm && L.ctx->n_ranks > 1 ? L.ctx->n_ranks : L.virt;
+  const int want = L.ctx->comm && (L.ctx->n_ranks > 1 || L.force_coll) ? L.ctx->n_ranks : L.virt;
   if (want == L.shards && L.Vs > 0) return;
   if (L.lam_stale) throw Error(STC_ERR_STATE, "the shard count changed after sharded steps");
   const int64_t RB = lda::kRowsPerBlock;
@@ -396,7 +397,7 @@ template <typename T>
 void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
   Ctx& c = *L.ctx;
   hipStream_t s = c.stream;
-  const bool ranks = c.comm && c.n_ranks > 1;
+  const bool ranks = c.comm && (c.n_ranks > 1 || L.force_coll);
   if (c.comm) {
     RCCL_CHECK(ncclGroupStart());
     if (ranks) {
@@ -1196,6 +1197,8 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->nblocks_m = ceil_div(L->V, lda::kRowsPerBlock);
     const char* vs = std::getenv("STC_VIRTUAL_SHARDS");
     L->virt = vs ? std::max(1, std::min(64, std::atoi(vs))) : 1;
+    const char* fc = std::getenv("STC_COLLECTIVE_MSTEP");
+    L->force_coll = fc && fc[0] == '1';
     ensure_layout(*L);  // λ, Bp, stat, logscale, colpart for the current shard count
     L->colsum.reserve(8 * L->k);
     L->alpha.reserve(8 * L->k);

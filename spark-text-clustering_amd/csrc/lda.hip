@@ -362,6 +362,9 @@ void launch_estep(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound) 
 // segmented SpMM over the batch's (term, slot) pairs radix-sorted by term.  One wave per chunk of
 // kChunk sorted entries, lanes over topics; runs that cross chunk edges go to head/tail partials
 // that k_fixup adds in chunk order.  Plain stores, no atomics, bitwise reproducible.
+// Topics are processed in slabs of 64·Q columns (blockIdx.y, the slow grid dimension): each wave
+// keeps kU·Q gathered eθ' values in flight without spilling at any k, and the waves running
+// together share one slab of eθ' (≤ 100 MB at 50k docs) in the MALL.
 // ---------------------------------------------------------------------------------------
 template <typename T, int Q>
 __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ skeys,
@@ -370,6 +373,7 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
                                                 const T* __restrict__ eth, int kp, T* __restrict__ stat,
                                                 T* __restrict__ headbuf, T* __restrict__ tailbuf,
                                                 int64_t nchunks) {
+  const int c0 = (int)blockIdx.y * 64 * Q;  // this slab's first topic column
   // kU entries in flight per wave: their (term, r, doc) are read out of the lanes that loaded them
   // (v_readlane: wave-uniform, so the eθ' row address is scalar) and their eθ' rows are all requested
   // before the first is accumulated — the gathers are served by L2 / MALL, and one row at a time
@@ -394,7 +398,7 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
     else dst = stat + (int64_t)v * kp;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      const int col = lane + 64 * q;
+      const int col = c0 + lane + 64 * q;
       if (col < kp) dst[col] = acc[q];
       acc[q] = T(0);
     }
@@ -424,7 +428,7 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
         const T* er = eth + (int64_t)__builtin_amdgcn_readlane(dv, jj) * kp;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-          const int col = lane + 64 * q;
+          const int col = c0 + lane + 64 * q;
           e[u][q] = col < kp ? er[col] : T(0);
         }
       }
@@ -452,7 +456,8 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
   // the run's owner (the chunk where it starts) adds the head partials of the chunks the run covers,
   // in chunk order; kG chunks are fetched at a time (keys and partials), so a run over hundreds of
   // chunks (the most frequent terms) costs hundreds / kG dependent round trips, not hundreds
-  constexpr int kG = 32;
+  constexpr int kG = 32 / Q;
+  const int c0 = (int)blockIdx.y * 64 * Q;  // this slab's first topic column
   const int lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= nchunks) return;
@@ -465,7 +470,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
   T acc[Q];
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
-    const int col = lane + 64 * q;
+    const int col = c0 + lane + 64 * q;
     acc[q] = col < kp ? tailbuf[c * kp + col] : T(0);
   }
   bool more = true;
@@ -480,7 +485,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
       go[g] = skeys[q1 - 1] == last && q1 < E && skeys[q1] == last;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        const int col = lane + 64 * q;
+        const int col = c0 + lane + 64 * q;
         h[g][q] = col < kp ? headbuf[c2 * kp + col] : T(0);
       }
     }
@@ -497,7 +502,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
   }
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
-    const int col = lane + 64 * q;
+    const int col = c0 + lane + 64 * q;
     if (col < kp) stat[(int64_t)last * kp + col] = acc[q];
   }
 }
@@ -506,7 +511,7 @@ template <typename T, int Q>
 static void sstats_q(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, int64_t E,
                      const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf) {
   const int64_t nchunks = ceil_div(E, kChunk);
-  const dim3 grid((unsigned)ceil_div(nchunks, 4));
+  const dim3 grid((unsigned)ceil_div(nchunks, 4), (unsigned)ceil_div(kp, 64 * Q));
   k_sstats<T, Q><<<grid, 256, 0, s>>>(skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, nchunks);
   KERNEL_CHECK();
   k_fixup<T, Q><<<grid, 256, 0, s>>>(skeys, E, kp, stat, headbuf, tailbuf, nchunks);
@@ -517,15 +522,14 @@ template <typename T>
 void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, int64_t E,
                    const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf) {
   if (E == 0) return;
+  if (kp > 4096) throw Error(STC_ERR_INVALID_ARG, "k > 4096 topics is not supported");
+  // slab width: ≤ 4 (fp64) / 8 (fp32) columns per lane — the whole row when it is that narrow
   const int q = (kp + 63) / 64;
+  constexpr int QMAX = sizeof(T) == 8 ? 4 : 8;
   if (q <= 1) sstats_q<T, 1>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
   else if (q <= 2) sstats_q<T, 2>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 4) sstats_q<T, 4>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 8) sstats_q<T, 8>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 16) sstats_q<T, 16>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 32) sstats_q<T, 32>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 64) sstats_q<T, 64>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
-  else throw Error(STC_ERR_INVALID_ARG, "k > 4096 topics is not supported");
+  else if (q <= 4 || QMAX == 4) sstats_q<T, 4>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
+  else sstats_q<T, QMAX>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -50,6 +50,17 @@ struct WTr<float> {
     d += dpp_f<DPP_QP_1032>(d);         // bit 0
     return d;
   }
+  // 8 values → this lane's row (bits 5, 4, 2 reduce-scatter; bits 3, 1, 0 all-reduce)
+  static __device__ __forceinline__ float rs8(const float* x, int lane) {
+    float a[4], b[2];
+    swap_add_n<true, 4>(x, x + 4, a);
+    swap_add_n<false, 2>(a, a + 2, b);
+    float d = rs_dpp<DPP_ROW_HALF_MIRROR>(b[0], b[1], lane & 4);
+    d += dpp_f<DPP_ROW_ROR8>(d);
+    d += dpp_f<DPP_QP_1032>(d);
+    d += dpp_f<DPP_QP_2301>(d);
+    return d;
+  }
 };
 template <>
 struct WTr<double> {
@@ -70,11 +81,38 @@ struct WTr<double> {
     d += dpp_d<DPP_QP_1032>(d);
     return d;
   }
+  static __device__ __forceinline__ double rs8(const double* x, int lane) {
+    double a[4], b[2];
+    swap_add_nd<true, 4>(x, x + 4, a);
+    swap_add_nd<false, 2>(a, a + 2, b);
+    double d = rs_dpp_d<DPP_ROW_HALF_MIRROR>(b[0], b[1], lane & 4);
+    d += dpp_d<DPP_ROW_ROR8>(d);
+    d += dpp_d<DPP_QP_1032>(d);
+    d += dpp_d<DPP_QP_2301>(d);
+    return d;
+  }
 };
 // the chunk row a lane holds after rs16 (levels bit 5, 4, 2, 1 halve the set; bits 3 and 0 all-reduce)
 __device__ __forceinline__ int rs16_row(int lane) {
   return 8 * ((lane >> 5) & 1) + 4 * ((lane >> 4) & 1) + 2 * ((lane >> 2) & 1) + ((lane >> 1) & 1);
 }
+// CH-row chunks (16, or 8 where the register budget is tight): the reduction, the row a lane ends
+// with, and the lanes that publish it (one per row)
+template <typename T, int CH>
+__device__ __forceinline__ T rs_chunk(const T* x, int lane) {
+  if constexpr (CH == 16) return WTr<T>::rs16(x, lane);
+  else return WTr<T>::rs8(x, lane);
+}
+template <int CH>
+__device__ __forceinline__ int rs_row(int lane) {
+  if constexpr (CH == 16) return rs16_row(lane);
+  else return 4 * ((lane >> 5) & 1) + 2 * ((lane >> 4) & 1) + ((lane >> 2) & 1);
+}
+template <int CH>
+__device__ __forceinline__ bool rs_pub(int lane) { return (lane & (CH == 16 ? 9 : 11)) == 0; }
+// rows per Phase A chunk: 8 for fp64 with ≥ 2 topics per lane (room for more register rows)
+template <typename T, int Q>
+constexpr int wide_chunk() { return sizeof(T) == 8 && Q >= 2 ? 8 : kWChunk; }
 
 // Q adjacent topics [t0, t0 + Q) of row `row` (pitch kp), zero past kp
 template <typename T, int Q>
@@ -138,7 +176,8 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
   WLds<T>& sm = *reinterpret_cast<WLds<T>*>(smem);
   T* const sB = reinterpret_cast<T*>(smem + wide_lds_fixed<T>());  // [nl][512·Q]
   using Tr = WTr<T>;
-  constexpr int LB = (int)(64 / (sizeof(T) * Q)) < kWChunk ? (int)(64 / (sizeof(T) * Q)) : kWChunk;  // ≤ 64 B / lane
+  constexpr int CH = wide_chunk<T, Q>();
+  constexpr int LB = (int)(64 / (sizeof(T) * Q)) < CH ? (int)(64 / (sizeof(T) * Q)) : CH;  // ≤ 64 B / lane
   if ((int64_t)blockIdx.x >= a.n) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t slot = a.slot0 + blockIdx.x;
@@ -264,25 +303,25 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
     // Phase A: per-wave row sums of B_n·eθ, 16 rows at a time — register rows (compile-time indices;
     // their zero padding past nnz gives zero sums), then the LDS / streamed rows
 #pragma unroll
-    for (int c = 0; c < NR / kWChunk; ++c) {
-      if (kWChunk * c < nnz) {
-        T x[kWChunk];
+    for (int c = 0; c < NR / CH; ++c) {
+      if (CH * c < nnz) {
+        T x[CH];
 #pragma unroll
-        for (int i = 0; i < kWChunk; ++i) {
+        for (int i = 0; i < CH; ++i) {
           T acc = T(0);
 #pragma unroll
-          for (int q = 0; q < Q; ++q) acc = fma(B[kWChunk * c + i][q], eth[q], acc);
+          for (int q = 0; q < Q; ++q) acc = fma(B[CH * c + i][q], eth[q], acc);
           x[i] = acc;
         }
-        const T v = Tr::rs16(x, lane);
-        const int n = kWChunk * c + rs16_row(lane);
-        if ((lane & 9) == 0 && n < nnz) sm.xs[wave][n] = v;
+        const T v = rs_chunk<T, CH>(x, lane);
+        const int n = CH * c + rs_row<CH>(lane);
+        if (rs_pub<CH>(lane) && n < nnz) sm.xs[wave][n] = v;
       }
     }
-    for (int n0 = NR; n0 < nnz; n0 += kWChunk) {
-      T x[kWChunk];
+    for (int n0 = NR; n0 < nnz; n0 += CH) {
+      T x[CH];
 #pragma unroll
-      for (int b = 0; b < kWChunk; b += LB) {
+      for (int b = 0; b < CH; b += LB) {
         T y[LB][Q];
         rows_q<T, Q, LB>(a.Bp, sm.ids, sB, kp, t0, NR, nres, nnz, n0 + b, y);  // LB rows' loads in flight
 #pragma unroll
@@ -293,9 +332,9 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
           x[b + i] = acc;
         }
       }
-      const T v = Tr::rs16(x, lane);
-      const int n = n0 + rs16_row(lane);
-      if ((lane & 9) == 0 && n < nnz) sm.xs[wave][n] = v;
+      const T v = rs_chunk<T, CH>(x, lane);
+      const int n = n0 + rs_row<CH>(lane);
+      if (rs_pub<CH>(lane) && n < nnz) sm.xs[wave][n] = v;
     }
     const T dsum_w = Tr::wsum(dg);
     if (lane == 0) sm.red[0][wave] = dsum_w;
@@ -442,10 +481,20 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
 // register rows per (T, Q): NR·Q·sizeof(T)/4 ≈ 128 VGPRs, so 512 threads keep two waves per SIMD
 // (fp32 Q = 1 — config 4's k = 500 — takes 176 rows: 227 VGPRs, no spills, the most the register
 // file holds at two waves per SIMD; its streamed tail is what bounds that config)
+#ifndef WIDE_NR64_Q1
+#define WIDE_NR64_Q1 64
+#endif
+#ifndef WIDE_NR64_Q2
+#define WIDE_NR64_Q2 24
+#endif
+#ifndef WIDE_NR64_Q4
+#define WIDE_NR64_Q4 8
+#endif
 template <typename T, int Q>
 constexpr int wide_nr() {
   return (sizeof(T) == 4 && Q == 1) ? 176
-         : sizeof(T) == 8 && Q >= 2 ? (Q == 2 ? 16 : 0)  // fp64 ≥ 1024 topics: LDS + streamed rows only
+         : (sizeof(T) == 8 && Q == 1) ? WIDE_NR64_Q1
+         : sizeof(T) == 8 && Q >= 2 ? (Q == 2 ? WIDE_NR64_Q2 : WIDE_NR64_Q4)  // fp64: 8-row chunks
                                     : (int)(128 * 4 / (sizeof(T) * Q)) / kWChunk * kWChunk;
 }
 

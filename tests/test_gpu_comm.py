@@ -95,3 +95,42 @@ def test_two_ranks_lda_next_idf_bound(tmp_path, oracle):
     rel = np.max(np.abs(a["lam"] - st.lam.T) / st.lam.T)
     assert rel < 1e-9, rel
     np.testing.assert_allclose(a["alpha"], st.alpha, rtol=1e-9)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_one_rank_communicator_collective_paths(ctx, monkeypatch, dtype):
+    """libstc's RCCL calls on a real communicator (one rank: the box has one GPU, and RCCL refuses two
+    ranks on one device): with STC_COLLECTIVE_MSTEP=1 every next() runs the multi-GPU M-step — the
+    grouped reduce-scatter of stat + all-reduce of logphat/count + the next draw's size, the sliced λ
+    update, the colsum-partial all-gather, the expElogβ'/logscale all-gathers — then get_topics
+    gathers the sharded λ and the bound all-reduces its corpus and topics parts; IDF fit reduces
+    df/m.  Everything must be bit-identical to the same run without a communicator."""
+    import stc
+    from helpers import random_corpus
+
+    rng = np.random.default_rng(51)
+    corpus = random_corpus(rng, 400, 3000, 1, 50, empty_every=9)
+    c1 = stc.Context(0)
+    c1.comm_init(stc.Context.unique_id(), 1, 0)
+    dt = stc.STC_F32 if dtype == "f32" else stc.STC_F64
+    runs = []
+    for c, coll in ((ctx, "0"), (c1, "1")):
+        monkeypatch.setenv("STC_COLLECTIVE_MSTEP", coll)
+        h = stc.LdaHandle(c, 9, corpus.num_cols, mini_batch_fraction=0.2, seed=4, dtype=dtype,
+                          optimize_doc_concentration=True)
+        d = stc.DeviceCsr.upload(c, corpus, dt)
+        h.set_corpus(d, corpus.num_rows)
+        h.init_random(6)
+        for _ in range(6):
+            h.next(stats=False)
+        bound = h.bound(d, gamma_seed=2)  # before get_topics: λ still sharded, topics part all-reduced
+        idf = stc.IDF(minDocFreq=2, ctx=c).fit(corpus)
+        runs.append(dict(lam=h.topics(), alpha=h.alpha(), it=h.iteration(), bound=bound, idf=idf.idf,
+                         df=idf.docFreq))
+    a, b = runs
+    assert a["it"] == b["it"] == 6
+    np.testing.assert_array_equal(a["lam"], b["lam"])
+    np.testing.assert_array_equal(a["alpha"], b["alpha"])
+    assert a["bound"] == b["bound"]
+    np.testing.assert_array_equal(a["idf"], b["idf"])
+    np.testing.assert_array_equal(a["df"], b["df"])
