@@ -55,6 +55,12 @@ struct stc_lda {
       nonempty, r, keys, vals, skeys, svals, stat, headbuf, tailbuf, sort_tmp, scan_tmp,
       stats4, cum2, bound, dtmp, lpart;
   DevBuf s_counts, s_weights, s_short, s_cincl, s_wincl, s_sincl;
+  DevBuf o_keys, o_keys2, o_idx, o_idx2, o_batch, o_orig, o_nnz, o_tmp;  // slot ordering (order_slots)
+  bool sort_docs = true;  // STC_SORT_DOCS=0 keeps sampling order
+  // many-topic kernel: per-entry row order, rarest terms first (lda_wide.hip), for `order_for`
+  DevBuf order, order_df;
+  const DCsr* order_for = nullptr;
+  bool hot_order = true;  // STC_HOT_ORDER=0: CSR order
   int64_t wave_cap = 0;  // docs with nnz <= wave_cap run the wave-per-document E-step
 
   // M-step sharding over the vocabulary (multi-GPU): rank r owns λ / expElogβ rows [r·Vs, (r+1)·Vs);
@@ -286,6 +292,50 @@ lda::EStepArgs<T> estep_args(stc_lda& L) {
 // the topics-across-lanes kernel (lda_wide.hip) beyond
 bool use_wide(int k, int dtype) { return dtype == STC_F32 ? lda::wave_row_cap(k) == 0 : lda::grid64_row_cap(k) == 0; }
 
+// the fast kernel's slots [0, n_short) in descending nnz: the longest documents start first, so the
+// launch does not end on a few long documents started late (longest-processing-time-first).  Each
+// slot keeps its member index (orig: γ₀ keys, outputs), so results only change in the summation
+// order of sstats within a term.
+void order_slots(stc_lda& L, int64_t n_short) {
+  if (!L.sort_docs || n_short < 2) return;
+  hipStream_t s = L.ctx->stream;
+  L.o_keys.reserve(8 * n_short);
+  L.o_keys2.reserve(8 * n_short);
+  L.o_idx.reserve(4 * n_short);
+  L.o_idx2.reserve(4 * n_short);
+  L.o_batch.reserve(4 * n_short);
+  L.o_orig.reserve(4 * n_short);
+  L.o_nnz.reserve(8 * n_short);
+  HIP_CHECK(hipMemcpyAsync(L.o_keys.p, L.nnzp.p, 8 * n_short, hipMemcpyDeviceToDevice, s));
+  lda::launch_iota(s, L.o_idx.as<int32_t>(), n_short);
+  size_t tb = 0;
+  HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(nullptr, tb, L.o_keys.as<int64_t>(), L.o_keys2.as<int64_t>(),
+                                                         L.o_idx.as<int32_t>(), L.o_idx2.as<int32_t>(), (int)n_short,
+                                                         0, 16, s));
+  L.o_tmp.reserve(tb);
+  HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(L.o_tmp.p, tb, L.o_keys.as<int64_t>(), L.o_keys2.as<int64_t>(),
+                                                         L.o_idx.as<int32_t>(), L.o_idx2.as<int32_t>(), (int)n_short,
+                                                         0, 16, s));
+  lda::launch_permute_slots(s, L.o_idx2.as<int32_t>(), n_short, L.batch.as<int32_t>(), L.orig.as<int32_t>(),
+                            L.nnzp.as<int64_t>(), L.o_batch.as<int32_t>(), L.o_orig.as<int32_t>(),
+                            L.o_nnz.as<int64_t>());
+  HIP_CHECK(hipMemcpyAsync(L.batch.p, L.o_batch.p, 4 * n_short, hipMemcpyDeviceToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(L.orig.p, L.o_orig.p, 4 * n_short, hipMemcpyDeviceToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(L.nnzp.p, L.o_nnz.p, 8 * n_short, hipMemcpyDeviceToDevice, s));
+}
+
+// the many-topic kernel's row order for the training corpus: the corpus's document frequencies,
+// then each row's entries by ascending df (once per set_corpus)
+void ensure_order(stc_lda& L) {
+  if (!L.hot_order || L.wave_cap <= 0 || !use_wide(L.k, L.dtype) || L.order_for == L.corpus) return;
+  const DCsr& m = *L.corpus;
+  L.order.reserve(4 * std::max<int64_t>(m.nnz, 1));
+  L.order_df.reserve(8 * m.cols);
+  idf::doc_freq(*L.ctx, m, L.order_df.as<int64_t>());
+  hashing::row_order_by_df(*L.ctx, m, L.order_df.as<int64_t>(), L.order.as<int32_t>());
+  L.order_for = L.corpus;
+}
+
 // fast kernel on slots [0, n_short), workgroup kernel on [n_short, n)
 template <typename T>
 void launch_split(stc_lda& L, lda::EStepArgs<T> a, int64_t n, int64_t n_short, bool stats, bool bound) {
@@ -331,6 +381,7 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   a.batch = L.batch.as<int32_t>();
   a.orig = L.orig.as<int32_t>();
   a.bptr = L.bptr.as<int64_t>();
+  a.order = L.order_for == L.corpus ? L.order.as<int32_t>() : nullptr;
   a.gamma0 = g0;
   a.iteration = iteration;
   a.key_mode = 0;
@@ -493,6 +544,7 @@ template <typename T>
 void step_ids(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, stc_step_stats* st) {
   require_ready(L);
   relayout(L);
+  ensure_order(L);
   claim_event_set(L);
   record(L, 0);
   const Part p = upload_members<T>(L, ids, n);
@@ -534,6 +586,7 @@ template <typename T>
 void next_impl(stc_lda& L, stc_step_stats* st) {
   require_ready(L);
   relayout(L);
+  ensure_order(L);
   Ctx& c = *L.ctx;
   hipStream_t s = c.stream;
   const int64_t D = L.corpus->rows;
@@ -575,6 +628,7 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
     lda::launch_fill_batch(s, L.corpus->indptr.as<int64_t>(), D, L.wave_cap, L.s_counts.as<int32_t>(),
                            L.s_cincl.as<int32_t>(), L.s_sincl.as<int32_t>(), ns32, L.batch.as<int32_t>(),
                            L.orig.as<int32_t>(), L.nnzp.as<int64_t>());
+  order_slots(L, ns32);
   slot_offsets(L, n);
   sample_draw(L, draw + 1);  // the next draw, counted with this step's collective
   L.pre_inflight = true;
@@ -588,6 +642,7 @@ void estep_only(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0,
                 double* stat_out, int32_t* iters_out) {
   require_ready(L);
   relayout(L);
+  ensure_order(L);
   hipStream_t s = L.ctx->stream;
   const Part p = upload_members<T>(L, ids, n);
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
@@ -1197,6 +1252,10 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->nblocks_m = ceil_div(L->V, lda::kRowsPerBlock);
     const char* vs = std::getenv("STC_VIRTUAL_SHARDS");
     L->virt = vs ? std::max(1, std::min(64, std::atoi(vs))) : 1;
+    const char* ho = std::getenv("STC_HOT_ORDER");
+    L->hot_order = !(ho && ho[0] == '0');
+    const char* sd = std::getenv("STC_SORT_DOCS");
+    L->sort_docs = !(sd && sd[0] == '0');
     const char* fc = std::getenv("STC_COLLECTIVE_MSTEP");
     L->force_coll = fc && fc[0] == '1';
     ensure_layout(*L);  // λ, Bp, stat, logscale, colpart for the current shard count
@@ -1234,6 +1293,7 @@ int stc_lda_set_corpus(stc_lda* L, const stc_dcsr* corpus, int64_t corpus_size_t
     L->corpus = corpus;
     L->corpus_total = corpus_size_total;
     L->pre_valid = false;  // a prefetched draw sampled the previous corpus
+    L->order_for = nullptr;
   });
 }
 

@@ -292,6 +292,55 @@ __global__ __launch_bounds__(64 * kDocWaves) void k_doc_runs(const int32_t* __re
   }
 }
 
+// order[s + i] = the in-row position of row d's i-th rarest term (df ascending, ties by position):
+// the E-step row order of lda_wide.hip.  Rows past kSortCap keep CSR order.
+template <int P>
+__device__ __forceinline__ void order_row(const int32_t* __restrict__ idx, const int64_t* __restrict__ df,
+                                          int32_t* __restrict__ order, int64_t s, int n, int lane) {
+  int32_t x[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int e = lane * P + p;
+    const int64_t f = e < n ? df[idx[s + e]] : 0;
+    x[p] = e < n ? (int32_t)((f < (1 << 21) - 1 ? f : (1 << 21) - 1) << 10 | e) : INT32_MAX;
+  }
+  bitonic_regs<P>(x, lane);
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int e = lane * P + p;
+    if (e < n) order[s + e] = x[p] & 1023;
+  }
+}
+
+__global__ __launch_bounds__(64 * kDocWaves) void k_row_order(const int64_t* __restrict__ indptr, int64_t rows,
+                                                             const int32_t* __restrict__ idx,
+                                                             const int64_t* __restrict__ df,
+                                                             int32_t* __restrict__ order) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t d = (int64_t)blockIdx.x * kDocWaves + (threadIdx.x >> 6); d < rows;
+       d += (int64_t)gridDim.x * kDocWaves) {
+    const int64_t s = indptr[d], n64 = indptr[d + 1] - s;
+    if (n64 > kSortCap) {
+      for (int64_t e = lane; e < n64; e += 64) order[s + e] = (int32_t)e;
+      continue;
+    }
+    const int n = (int)n64;
+    if (n <= 64) order_row<1>(idx, df, order, s, n, lane);
+    else if (n <= 128) order_row<2>(idx, df, order, s, n, lane);
+    else if (n <= 256) order_row<4>(idx, df, order, s, n, lane);
+    else if (n <= 512) order_row<8>(idx, df, order, s, n, lane);
+    else order_row<16>(idx, df, order, s, n, lane);
+  }
+}
+
+void row_order_by_df(Ctx& c, const DCsr& m, const int64_t* d_df, int32_t* d_order) {
+  if (m.rows == 0 || m.nnz == 0) return;
+  const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(ceil_div(m.rows, kDocWaves), 1), 1 << 14);
+  k_row_order<<<g, 64 * kDocWaves, 0, c.stream>>>(m.indptr.as<int64_t>(), m.rows, m.indices.as<int32_t>(), d_df,
+                                                  d_order);
+  KERNEL_CHECK();
+}
+
 void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t n_tok,
                const int64_t* d_doc_off, int64_t n_docs, int32_t num_features, int binary,
                int variant, int value_dtype, DCsr& out) {

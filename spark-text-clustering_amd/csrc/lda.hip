@@ -1023,6 +1023,35 @@ void launch_fill_batch(hipStream_t s, const int64_t* indptr, int64_t D, int64_t 
   KERNEL_CHECK();
 }
 
+// slots [0, n) reordered by idx: out[i] = in[idx[i]] for the slot arrays
+__global__ __launch_bounds__(256) void k_permute_slots(const int32_t* __restrict__ idx, int64_t n,
+                                                       const int32_t* __restrict__ batch, const int32_t* __restrict__ orig,
+                                                       const int64_t* __restrict__ nnz, int32_t* __restrict__ batch2,
+                                                       int32_t* __restrict__ orig2, int64_t* __restrict__ nnz2) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int32_t j = idx[i];
+    batch2[i] = batch[j];
+    orig2[i] = orig[j];
+    nnz2[i] = nnz[j];
+  }
+}
+__global__ __launch_bounds__(256) void k_iota(int32_t* __restrict__ x, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) x[i] = (int32_t)i;
+}
+void launch_permute_slots(hipStream_t s, const int32_t* idx, int64_t n, const int32_t* batch, const int32_t* orig,
+                          const int64_t* nnz, int32_t* batch2, int32_t* orig2, int64_t* nnz2) {
+  if (n == 0) return;
+  const int64_t g = ceil_div(n, 256);
+  k_permute_slots<<<(unsigned)(g > 4096 ? 4096 : g), 256, 0, s>>>(idx, n, batch, orig, nnz, batch2, orig2, nnz2);
+  KERNEL_CHECK();
+}
+void launch_iota(hipStream_t s, int32_t* x, int64_t n) {
+  if (n == 0) return;
+  const int64_t g = ceil_div(n, 256);
+  k_iota<<<(unsigned)(g > 4096 ? 4096 : g), 256, 0, s>>>(x, n);
+  KERNEL_CHECK();
+}
+
 // host-injected membership: flags + stable partition into [short | long] slots
 __global__ __launch_bounds__(256) void k_part_flags(const int64_t* __restrict__ indptr,
                                                     const int32_t* __restrict__ batch, int64_t n,

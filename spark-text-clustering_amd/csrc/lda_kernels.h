@@ -38,6 +38,10 @@ struct EStepArgs {
   int64_t slot0 = 0;
   int64_t n = 0;                       // slots in this launch
   const int64_t* bptr = nullptr;       // slot → first entry slot (nullptr: the row's CSR offset)
+  // per CSR entry: the in-row position of the row's n-th E-step row (lda_wide.hip: the corpus's
+  // rarest terms first, so the register / LDS rows are the cold ones and the streamed rows the hot
+  // ones the MALL holds for every CU); nullptr: CSR order
+  const int32_t* order = nullptr;
   const T* Bp = nullptr;               // V×kp  row-scaled expElogβ'
   const double* logscale = nullptr;    // V     m_v (BOUND)
   const double* alpha = nullptr;       // k
@@ -129,6 +133,9 @@ void launch_sample(hipStream_t s, const int64_t* indptr, int64_t D, double fract
 // writes partitioned slots: batch_p (row), orig_p (raw member position), nnz_p
 // out[0..2] = {*a, *b, *c} (the inclusive scans' totals for one readback)
 void launch_last3(hipStream_t s, const int32_t* a, const int64_t* b, const int32_t* c, int64_t* out);
+void launch_permute_slots(hipStream_t s, const int32_t* idx, int64_t n, const int32_t* batch, const int32_t* orig,
+                          const int64_t* nnz, int32_t* batch2, int32_t* orig2, int64_t* nnz2);
+void launch_iota(hipStream_t s, int32_t* x, int64_t n);
 void launch_fill_batch(hipStream_t s, const int64_t* indptr, int64_t D, int64_t cap,
                        const int32_t* counts, const int32_t* count_incl,
                        const int32_t* short_incl, int64_t n_short, int32_t* batch_p,

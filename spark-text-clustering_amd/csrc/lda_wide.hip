@@ -197,8 +197,9 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
   for (int j = 0; j < RL; ++j) {
     const int n = tid + kWThreads * j;
     const bool v = n < nnz;
-    const int id = v ? a.indices[s0 + n] : 0;
-    cts[j] = v ? a.values[s0 + n] : T(0);
+    const int64_t pos = s0 + (v && a.order ? a.order[s0 + n] : n);
+    const int id = v ? a.indices[pos] : 0;
+    cts[j] = v ? a.values[pos] : T(0);
     sm.ids[n] = id;  // published by the __syncthreads_or below
     // Spark's 1e-100 in the row-scaled space (lda.hip): ε'_n = 1e-100·e^{−m_v}, kept finite (a row whose
     // e^{−m_v} overflows has an all-zero unscaled expElogβ in Spark and contributes nothing; r ≈ 0 here)
@@ -239,7 +240,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
       if (n < nnz) {
         a.r[e0 + n] = T(0);
         if (STATS) {
-          a.keys[e0 + n] = (uint32_t)a.indices[s0 + n];
+          a.keys[e0 + n] = (uint32_t)sm.ids[n];
           a.vals[e0 + n] = entry_val<T>(slot, e0 + n, T(0));
         }
       }
@@ -279,7 +280,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
   T B[NR > 0 ? NR : 1][Q];
 #pragma unroll
   for (int n = 0; n < NR; ++n) {
-    if (n < nnz) load_q<T, Q>(a.Bp, (int64_t)a.indices[s0 + n], kp, t0, B[n]);
+    if (n < nnz) load_q<T, Q>(a.Bp, (int64_t)sm.ids[n], kp, t0, B[n]);
     else {
 #pragma unroll
       for (int q = 0; q < Q; ++q) B[n][q] = T(0);
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
   }
   for (int n = NR; n < nres && n < nnz; ++n) {
     T x[Q];
-    load_q<T, Q>(a.Bp, (int64_t)a.indices[s0 + n], kp, t0, x);
+    load_q<T, Q>(a.Bp, (int64_t)sm.ids[n], kp, t0, x);
 #pragma unroll
     for (int q = 0; q < Q; ++q) sB[(int64_t)(n - NR) * (kWThreads * Q) + t0 + q] = x[q];  // read back by this lane
   }
@@ -356,7 +357,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
         sm.rr[n] = r;
         rd = fma(r, dot, rd);
         if (BOUND && last && cts[j] != T(0)) {
-          b_tok += (double)cts[j] * (log(fmax((double)dot, 1e-300)) + a.logscale[a.indices[s0 + n]]);
+          b_tok += (double)cts[j] * (log(fmax((double)dot, 1e-300)) + a.logscale[sm.ids[n]]);
           c_tok += (double)cts[j];
         }
       }
@@ -414,7 +415,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
       const T r = sm.rr[n];
       a.r[e0 + n] = r;
       if (STATS) {
-        a.keys[e0 + n] = (uint32_t)a.indices[s0 + n];
+        a.keys[e0 + n] = (uint32_t)sm.ids[n];
         a.vals[e0 + n] = entry_val<T>(slot, e0 + n, r);
       }
     }

@@ -418,6 +418,7 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 namespace hashing {
 void hash_tokens(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t n_tok,
                  int32_t num_features, int variant, int32_t* d_idx);
+void row_order_by_df(Ctx& c, const DCsr& m, const int64_t* d_df, int32_t* d_order);
 void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t n_tok,
                const int64_t* d_doc_off, int64_t n_docs, int32_t num_features, int binary,
                int variant, int value_dtype, DCsr& out);
