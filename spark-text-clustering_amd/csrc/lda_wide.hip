@@ -170,6 +170,18 @@ __host__ __device__ constexpr size_t wide_lds_fixed() {
   return (sizeof(WLds<T>) + 255) / 256 * 256;
 }
 
+#ifndef WIDE_LB_BYTES
+#define WIDE_LB_BYTES 64  // streamed-row loads in flight per lane (bytes)
+#endif
+#ifndef WIDE_NR64_Q1
+#define WIDE_NR64_Q1 64
+#endif
+#ifndef WIDE_NR64_Q2
+#define WIDE_NR64_Q2 24
+#endif
+#ifndef WIDE_NR64_Q4
+#define WIDE_NR64_Q4 8
+#endif
 template <typename T, int Q, int NR, bool STATS, bool BOUND>
 __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -177,7 +189,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
   T* const sB = reinterpret_cast<T*>(smem + wide_lds_fixed<T>());  // [nl][512·Q]
   using Tr = WTr<T>;
   constexpr int CH = wide_chunk<T, Q>();
-  constexpr int LB = (int)(64 / (sizeof(T) * Q)) < CH ? (int)(64 / (sizeof(T) * Q)) : CH;  // ≤ 64 B / lane
+  constexpr int LB = (int)(WIDE_LB_BYTES / (sizeof(T) * Q)) < CH ? (int)(WIDE_LB_BYTES / (sizeof(T) * Q)) : CH;
   if ((int64_t)blockIdx.x >= a.n) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t slot = a.slot0 + blockIdx.x;
@@ -482,15 +494,6 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
 // register rows per (T, Q): NR·Q·sizeof(T)/4 ≈ 128 VGPRs, so 512 threads keep two waves per SIMD
 // (fp32 Q = 1 — config 4's k = 500 — takes 176 rows: 227 VGPRs, no spills, the most the register
 // file holds at two waves per SIMD; its streamed tail is what bounds that config)
-#ifndef WIDE_NR64_Q1
-#define WIDE_NR64_Q1 64
-#endif
-#ifndef WIDE_NR64_Q2
-#define WIDE_NR64_Q2 24
-#endif
-#ifndef WIDE_NR64_Q4
-#define WIDE_NR64_Q4 8
-#endif
 template <typename T, int Q>
 constexpr int wide_nr() {
   return (sizeof(T) == 4 && Q == 1) ? 176
