@@ -24,43 +24,114 @@ static int grid_for(int64_t n) {
 // df[j] = #entries (rows hold each id once) with id j and value > 0 (DocumentFrequencyAggregator.add).
 // A Zipf corpus's hot ids sit in almost every row, and device-scope atomics run at a few G/s, so
 // the histogram is built without per-entry global atomics:
-//  * numFeatures ≤ 2^18 (k_df_tile): vocabulary tiles of 2^15 ids; workgroup (tile t, entry chunk
-//    c) streams the chunk's ids, counts those in its tile in LDS (128 KB of u32), and writes its
-//    partial histogram; k_df_reduce sums the partials over the chunks in chunk order.
+//  * numFeatures ≤ 2^18: vocabulary tiles of 2^15 ids.  k_df_bin splits each entry chunk by tile
+//    (one read of the CSR), k_df_binned counts a tile over a group of chunks in LDS (128 KB of u32)
+//    and writes its partial histogram, k_df_reduce sums the partials in group order.
 //  * larger vocabularies: the (value > 0) ids are radix-sorted and each run's [lo, hi) recorded.
 // Both are exact integer counts, identical run to run.
 constexpr int kTileBits = 15;
 constexpr int kTile = 1 << kTileBits;
 constexpr int kTileThreads = 1024;
 
+// Binned variant (one read of the CSR): k_df_bin splits each chunk of kBinChunk entries by tile —
+// the (value > 0) ids' low 15 bits as u16, tile-major inside the chunk's own region of the bin array
+// (no global scan: a chunk's region is its kBinChunk slots) — and k_df_binned counts one tile over a
+// group of chunks in LDS.  Bytes per entry: 4 + s (id, value) read, 2 written, 2 read.
+constexpr int kBinChunk = 16384;
+constexpr int kBinThreads = 1024;
+constexpr int kBinPer = kBinChunk / kBinThreads;  // entries per thread
+constexpr int kMaxTiles = 8;
+
 template <typename V>
-__global__ __launch_bounds__(kTileThreads) void k_df_tile(const int32_t* __restrict__ idx, const V* __restrict__ val,
-                                                          int64_t nnz, int64_t per, int n_tiles, int64_t cols,
-                                                          uint32_t* __restrict__ part) {
+__global__ __launch_bounds__(kBinThreads) void k_df_bin(const int32_t* __restrict__ idx, const V* __restrict__ val,
+                                                        int64_t nnz, int n_tiles, uint16_t* __restrict__ bins,
+                                                        int32_t* __restrict__ tab /* [chunk][2·kMaxTiles] */) {
+  __shared__ int32_t wtot[kBinThreads / 64][kMaxTiles];
+  __shared__ int32_t tbase[kMaxTiles + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t c = blockIdx.x, e0 = c * kBinChunk;
+  uint32_t ent[kBinPer];  // tile << 16 | low id, or ~0u
+  int cnt[kMaxTiles];
+#pragma unroll
+  for (int t = 0; t < kMaxTiles; ++t) cnt[t] = 0;
+#pragma unroll
+  for (int u = 0; u < kBinPer; ++u) {
+    const int64_t e = e0 + u * kBinThreads + tid;
+    uint32_t x = ~0u;
+    if (e < nnz && val[e] > V(0)) {
+      const uint32_t id = (uint32_t)idx[e];
+      x = ((id >> kTileBits) << 16) | (id & (kTile - 1));
+    }
+    ent[u] = x;
+#pragma unroll
+    for (int t = 0; t < kMaxTiles; ++t) cnt[t] += (x >> 16) == (uint32_t)t ? 1 : 0;
+  }
+  // exclusive prefix of each tile's counts over the block's threads (thread order)
+  int pre[kMaxTiles];
+#pragma unroll
+  for (int t = 0; t < kMaxTiles; ++t) {
+    int v = cnt[t];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(v, o, 64);
+      if (lane >= o) v += y;
+    }
+    pre[t] = v - cnt[t];
+    if (lane == 63) wtot[wave][t] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int run = 0;
+    for (int t = 0; t < kMaxTiles; ++t) {
+      tbase[t] = run;
+      int tot = 0;
+      for (int w = 0; w < kBinThreads / 64; ++w) tot += wtot[w][t];
+      tab[c * 2 * kMaxTiles + t] = run;                 // the tile's offset inside the chunk region
+      tab[c * 2 * kMaxTiles + kMaxTiles + t] = tot;     // and its count
+      run += tot;
+    }
+    tbase[kMaxTiles] = run;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < kMaxTiles; ++t) {
+    int wb = 0;
+    for (int w = 0; w < wave; ++w) wb += wtot[w][t];
+    pre[t] += tbase[t] + wb;
+  }
+  uint16_t* out = bins + e0;
+#pragma unroll
+  for (int u = 0; u < kBinPer; ++u) {
+    const uint32_t x = ent[u];
+    if (x != ~0u) {
+      const int t = (int)(x >> 16);
+      int pos = 0;
+#pragma unroll
+      for (int q = 0; q < kMaxTiles; ++q)
+        if (q == t) pos = pre[q]++;
+      out[pos] = (uint16_t)(x & 0xFFFF);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kTileThreads) void k_df_binned(const uint16_t* __restrict__ bins,
+                                                            const int32_t* __restrict__ tab, int64_t chunks,
+                                                            int64_t per_group, int n_tiles, int64_t cols,
+                                                            uint32_t* __restrict__ part) {
   extern __shared__ uint32_t cnt[];
   const int t = blockIdx.x % n_tiles;
-  const int64_t c = blockIdx.x / n_tiles;
+  const int64_t g = blockIdx.x / n_tiles;
   for (int i = threadIdx.x; i < kTile; i += kTileThreads) cnt[i] = 0;
   __syncthreads();
-  // per is a multiple of 8: each thread streams 8 consecutive ids (two 16-byte loads in flight)
-  const int64_t e0 = c * per, e1 = e0 + per < nnz ? e0 + per : nnz;
-  for (int64_t e = e0 + 8 * threadIdx.x; e < e1; e += 8 * kTileThreads) {
-    int32_t id[8];
-    if (e + 8 <= e1) {
-      const int4 a = *reinterpret_cast<const int4*>(idx + e), b = *reinterpret_cast<const int4*>(idx + e + 4);
-      id[0] = a.x; id[1] = a.y; id[2] = a.z; id[3] = a.w;
-      id[4] = b.x; id[5] = b.y; id[6] = b.z; id[7] = b.w;
-    } else {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) id[q] = e + q < e1 ? idx[e + q] : -1;
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (id[q] >= 0 && (id[q] >> kTileBits) == t && val[e + q] > V(0)) atomicAdd(&cnt[id[q] & (kTile - 1)], 1u);
+  const int64_t c0 = g * per_group, c1 = c0 + per_group < chunks ? c0 + per_group : chunks;
+  for (int64_t c = c0; c < c1; ++c) {
+    const int32_t off = tab[c * 2 * kMaxTiles + t], n = tab[c * 2 * kMaxTiles + kMaxTiles + t];
+    const uint16_t* b = bins + c * kBinChunk + off;
+    for (int i = threadIdx.x; i < n; i += kTileThreads) atomicAdd(&cnt[b[i]], 1u);
   }
   __syncthreads();
   const int64_t j0 = (int64_t)t * kTile;
-  uint32_t* out = part + c * cols + j0;
+  uint32_t* out = part + g * cols + j0;
   for (int i = threadIdx.x; i < kTile && j0 + i < cols; i += kTileThreads) out[i] = cnt[i];
 }
 
@@ -96,24 +167,31 @@ void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df) {
   hipStream_t s = c.stream;
   HIP_CHECK(hipMemsetAsync(d_df, 0, sizeof(int64_t) * m.cols, s));
   if (m.nnz == 0) return;
-  if (m.cols <= (int64_t(8) << kTileBits)) {
+  if (m.cols <= (int64_t(kMaxTiles) << kTileBits)) {
     const int T = (int)ceil_div(m.cols, (int64_t)kTile);
-    const int64_t C = std::max<int64_t>(1, std::min<int64_t>(ceil_div(m.nnz, (int64_t)65536), 1024 / T));
-    const int64_t per = ceil_div(ceil_div(m.nnz, C), (int64_t)8) * 8;
+    const int64_t chunks = ceil_div(m.nnz, (int64_t)kBinChunk);
+    const int64_t G = std::max<int64_t>(1, std::min<int64_t>(chunks, 1024 / T));  // chunk groups
+    const int64_t per_group = ceil_div(chunks, G);
+    const int64_t groups = ceil_div(chunks, per_group);
+    DevBuf& bins = c.scratch[1];
+    DevBuf& tab = c.scratch[2];
     DevBuf& part = c.scratch[0];
-    part.reserve(sizeof(uint32_t) * C * m.cols);
-    const size_t lds = sizeof(uint32_t) * kTile;
-    if (m.dtype == STC_F32) {
-      HIP_CHECK(hipFuncSetAttribute((const void*)k_df_tile<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      k_df_tile<float><<<(unsigned)(T * C), kTileThreads, lds, s>>>(m.indices.as<int32_t>(), m.values.as<float>(),
-                                                                    m.nnz, per, T, m.cols, part.as<uint32_t>());
-    } else {
-      HIP_CHECK(hipFuncSetAttribute((const void*)k_df_tile<double>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      k_df_tile<double><<<(unsigned)(T * C), kTileThreads, lds, s>>>(m.indices.as<int32_t>(), m.values.as<double>(),
-                                                                     m.nnz, per, T, m.cols, part.as<uint32_t>());
-    }
+    bins.reserve(sizeof(uint16_t) * chunks * kBinChunk);
+    tab.reserve(sizeof(int32_t) * chunks * 2 * kMaxTiles);
+    part.reserve(sizeof(uint32_t) * groups * m.cols);
+    if (m.dtype == STC_F32)
+      k_df_bin<float><<<(unsigned)chunks, kBinThreads, 0, s>>>(m.indices.as<int32_t>(), m.values.as<float>(), m.nnz,
+                                                               T, bins.as<uint16_t>(), tab.as<int32_t>());
+    else
+      k_df_bin<double><<<(unsigned)chunks, kBinThreads, 0, s>>>(m.indices.as<int32_t>(), m.values.as<double>(),
+                                                                m.nnz, T, bins.as<uint16_t>(), tab.as<int32_t>());
     KERNEL_CHECK();
-    k_df_reduce<<<grid_for(m.cols), 256, 0, s>>>(part.as<uint32_t>(), C, m.cols, d_df);
+    const size_t lds = sizeof(uint32_t) * kTile;
+    HIP_CHECK(hipFuncSetAttribute((const void*)k_df_binned, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k_df_binned<<<(unsigned)(T * groups), kTileThreads, lds, s>>>(bins.as<uint16_t>(), tab.as<int32_t>(), chunks,
+                                                                  per_group, T, m.cols, part.as<uint32_t>());
+    KERNEL_CHECK();
+    k_df_reduce<<<grid_for(m.cols), 256, 0, s>>>(part.as<uint32_t>(), groups, m.cols, d_df);
     KERNEL_CHECK();
     return;
   }
