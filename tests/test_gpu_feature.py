@@ -159,11 +159,11 @@ def test_hashing_tf_document_lengths(ctx, oracle, nf):
     assert np.array_equal(out.values, vv)
 
 
-@pytest.mark.parametrize("V", [1 << 18, 1 << 20])
+@pytest.mark.parametrize("V", [1 << 18, 1 << 20, 1 << 21])
 def test_idf_doc_freq_zipf_hot_ids(ctx, V):
     """doc_freq: heavy-hitter document frequencies on a Zipf corpus (hot ids in every row, more
     distinct ids per workgroup slice than LDS slots) equal the exact column counts of positive values;
-    2^18 buckets take the LDS vocabulary tiles, 2^20 the radix-sorted runs."""
+    2^18 buckets take the binned LDS vocabulary tiles, 2^20 and 2^21 the radix-sorted runs."""
     import stc
     from stc import synth
 
