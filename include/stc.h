@@ -25,7 +25,8 @@
  *   stc_lda_topic_distribution  toLocal.topicDistribution(tf) — LDALoader.scala:108
  *   stc_lda_bound               [U] LocalLDAModel.logLikelihood / logPerplexity
  *   stc_comm_*                  the role of Spark's broadcast + treeReduce inside lda.run
- *                               (one RCCL all-reduce of k×V sstats per minibatch over xGMI)
+ *                               (per minibatch: RCCL reduce-scatter of the k×V sstats over
+ *                               vocabulary slices, the slice's λ update, all-gather of expElogβ)
  *
  * Conventions
  *   - Every function returns STC_OK (0) or an STC_ERR_* code; the message of the last failure on
@@ -88,7 +89,10 @@ int stc_synchronize(stc_ctx* ctx);
  * Rank 0 calls stc_comm_unique_id and ships the 128 bytes to the other ranks out of band
  * (the Spark driver broadcast, or torch.distributed's store); every rank then calls
  * stc_comm_init.  Once connected, stc_idf_fit, stc_lda_step/next and stc_lda_bound reduce
- * their partial results over all ranks (RCCL all-reduce over xGMI).                        */
+ * their partial results over all ranks (RCCL over xGMI), and the M-step is sharded: each rank
+ * updates λ on its vocabulary slice, so the λ readers stc_lda_get_topics / stc_lda_describe
+ * become collective too (every rank calls them; the first after a step all-gathers λ).
+ * Connect before stc_lda_create (a later connect re-lays the model out before the next step). */
 int stc_comm_unique_id(uint8_t id_out[128]);
 int stc_comm_init(stc_ctx* ctx, const uint8_t id[128], int n_ranks, int rank);
 int stc_comm_allreduce_f64(stc_ctx* ctx, double* host_inout, int64_t n); /* host scalars */
@@ -212,7 +216,9 @@ int stc_lda_get_iteration(stc_lda* lda, int64_t* iteration_out);
 int stc_lda_step(stc_lda* lda, const int64_t* batch_doc_ids, int64_t n, const double* gamma0,
                  stc_step_stats* stats);
 /* One OnlineLDAOptimizer.next(): device-side Poisson/Bernoulli membership sampling with
- * fraction mini_batch_fraction, then the same step.                                        */
+ * fraction mini_batch_fraction, then the same step.  Every call draws a new sample (an empty
+ * GLOBAL sample returns without an iteration, as Spark's `if (batch.isEmpty()) return this`);
+ * the next draw is sampled during this step, so consecutive calls do not drain the stream.  */
 int stc_lda_next(stc_lda* lda, stc_step_stats* stats);
 /* E-step only (no model update), for tests: gamma_out n×k; stat_out (k×V as V×k layout,
  * may be NULL) receives the summed sufficient statistics Σ_d eθ_d ⊗ (cts/φ) scattered to
