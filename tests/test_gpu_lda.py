@@ -362,3 +362,20 @@ def test_empty_draws_advance(ctx):
     nonempty = sum(1 for x in sizes if x > 0)
     assert 5 <= nonempty <= 60, nonempty  # Poisson(0.2) over 200 draws: mean ≈ 36
     assert h.iteration() == nonempty
+
+
+def test_slot_order_longest_first_same_model(ctx, monkeypatch):
+    """next() runs a small minibatch's documents longest-first (order_slots: batch / orig / nnz
+    permuted together, γ₀ keyed by the member index); the model equals the sampling-order run up
+    to sstats' summation order within a term."""
+    rng = np.random.default_rng(46)
+    corpus = random_corpus(rng, 600, 3000, 1, 120, empty_every=23)
+    runs = []
+    for sort in ("0", "1"):
+        monkeypatch.setenv("STC_SORT_DOCS", sort)
+        h, _ = _train(ctx, corpus, 10, "f64", 5)
+        runs.append((h.topics(), h.alpha(), h.iteration()))
+    (l0, a0, i0), (l1, a1, i1) = runs
+    assert i0 == i1 == 5
+    np.testing.assert_allclose(l1, l0, rtol=1e-10, atol=0)
+    np.testing.assert_allclose(a1, a0, rtol=1e-10, atol=0)
