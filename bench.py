@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--k", type=int, default=None)
     p.add_argument("--fraction", type=float, default=0.05)
     p.add_argument("--corpus", default="zipf", choices=["zipf", "zipf-lda"])
+    p.add_argument("--state", default="burn-in", choices=["burn-in", "planted"],
+                   help="model state of the timed steps: after --state-minibatches from λ₀, or (zipf-lda) "
+                        "the planted topicsMatrix that generated the corpus (SURVEY §8(d) state B)")
     p.add_argument("--dtype", default="f64", choices=["f32", "f64"])
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     p.add_argument("--seed", type=int, default=20261015)
@@ -407,7 +410,12 @@ def main():
 
     DT = {"f32": stc.STC_F32, "f64": stc.STC_F64}
     dcorp = {a.dtype: stc.DeviceCsr.upload(ctx, corpus, DT[a.dtype])}
-    h, r = run_state(stc, ctx, dcorp[a.dtype], a, a.dtype, total, None, barrier, log, a.steps, a.warmup)
+    lam_head = None
+    if a.state == "planted":
+        if a.corpus != "zipf-lda":
+            raise SystemExit("--state planted needs --corpus zipf-lda")
+        lam_head = synth.planted_topics(a.vocab, a.k, seed=seed)
+    h, r = run_state(stc, ctx, dcorp[a.dtype], a, a.dtype, total, lam_head, barrier, log, a.steps, a.warmup)
     head = summarize(reduce_run(r), a, a.dtype, world, a.steps, a.corpus, kernel_name(a.dtype, a.k))
 
     lines = []
@@ -464,7 +472,9 @@ def main():
             "docs": a.docs, "tokens_per_doc": a.tokens, "vocab": a.vocab, "k": a.k,
             "subsampling_rate": a.fraction, "corpus": a.corpus, "parallelism": f"dp{world}",
             "mean_nnz_per_doc": head["mean_nnz_per_doc"], "mean_inner_iters": head["mean_inner_iters"],
-            "model_state": f"after {a.state_minibatches} minibatches from lambda0 (Gamma(100,1/100))",
+            "model_state": (f"after {a.state_minibatches} minibatches from lambda0 (Gamma(100,1/100))"
+                            if a.state == "burn-in" else
+                            f"after {a.state_minibatches} minibatches from the planted topicsMatrix"),
             "cold": head["cold"], "phase_ms": head["phase_ms"],
             "estep_only_docs_per_s": head["estep_only_docs_per_s"], "cap_hits": head["cap_hits"],
         },

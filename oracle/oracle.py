@@ -308,6 +308,40 @@ def train_doc_key(iteration: int, rank: int, batch_pos: int) -> int:
     return ((iteration & 0xFFFFFF) << 40) | ((rank & 0xFF) << 32) | (batch_pos & 0xFFFFFFFF)
 
 
+def init_lambda(seed: int, V: int, k: int, shape: float = 100.0) -> np.ndarray:
+    """[U] OnlineLDAOptimizer.initialize: λ₀ ~ Gamma(shape, 1/shape) i.i.d. (Spark: k×V from its
+    MT generator).  The counter-RNG replacement keyed by the k×V element index t·V + v, as
+    stc_lda_init_random draws it.  Returned V×k (topicsMatrix orientation)."""
+    lam = np.empty((V, k), np.float64)
+    for t in range(k):
+        for v in range(V):
+            lam[v, t] = gamma_sample(doc_stream(seed, t * V + v), 0, shape)
+    return lam
+
+
+def sample_members(seed: int, draw: int, rank: int, n_docs: int, fraction: float,
+                   with_replacement: bool) -> list:
+    """[U] OnlineLDAOptimizer.next: ``docs.sample(withReplacement, miniBatchFraction, rng.nextLong())``
+    — per document a Poisson(f) multiplicity (with replacement) or a Bernoulli(f) flag, from the
+    counter RNG keyed (seed ^ 0x5DEECE66D, draw, rank, doc) as stc_lda_next draws it.  Returns the
+    members in document order, a document repeated by its multiplicity (RDD.sample's order)."""
+    out = []
+    for d in range(n_docs):
+        u = _uniform(doc_stream(seed ^ 0x5DEECE66D, train_doc_key(draw, rank, d)), 0)
+        c = 0
+        if with_replacement:  # Poisson by inversion (capped at 64 like the device)
+            p = math.exp(-fraction)
+            F = p
+            while u > F and c < 64:
+                c += 1
+                p *= fraction / c
+                F += p
+        else:
+            c = 1 if u < fraction else 0
+        out.extend([d] * c)
+    return out
+
+
 # ---------------------------------------------------------------------------------------
 # OnlineLDAOptimizer   [U] mllib.clustering.OnlineLDAOptimizer
 # ---------------------------------------------------------------------------------------

@@ -341,7 +341,8 @@ void ensure_order(stc_lda& L) {
 
 // fast kernel on slots [0, n_short), workgroup kernel on [n_short, n)
 template <typename T>
-void launch_split(stc_lda& L, lda::EStepArgs<T> a, int64_t n, int64_t n_short, bool stats, bool bound) {
+void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int64_t n_short, bool stats,
+                  bool bound) {
   hipStream_t s = L.ctx->stream;
   if (n_short > 0) {
     lda::EStepArgs<T> w = a;
@@ -349,7 +350,7 @@ void launch_split(stc_lda& L, lda::EStepArgs<T> a, int64_t n, int64_t n_short, b
     w.n = n_short;
     if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
     else if constexpr (std::is_same<T, float>::value) lda::launch_estep_wave(s, w, stats, bound);
-    else lda::launch_estep_grid64(s, w, stats, bound);
+    else lda::launch_estep_grid64(s, w, stats, bound, m.max_row < 0 || m.max_row > lda::grid64_onchip_rows(L.k));
   }
   if (n > n_short) {
     a.slot0 = n_short;
@@ -397,7 +398,7 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   a.iters = L.iters.as<int32_t>();
   a.nonempty = L.nonempty.as<int32_t>();
   record(L, 1);
-  launch_split<T>(L, a, n, n_short, true, false);
+  launch_split<T>(L, *L.corpus, a, n, n_short, true, false);
   record(L, 2);
   HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.vpad * L.kp, s));  // padded rows stay zero
   if (E > 0) {
@@ -699,7 +700,7 @@ void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const
   a.gamma = gamma_out ? L.gamma.as<T>() : nullptr;
   a.iters = L.iters.as<int32_t>();
   a.bound = bound ? L.bound.as<double>() : nullptr;
-  launch_split<T>(L, a, n, p.n_short, false, bound);
+  launch_split<T>(L, docs, a, n, p.n_short, false, bound);
   if (gamma_out && n > 0) {
     std::vector<T> g((size_t)(n * L.k));
     HIP_CHECK(hipMemcpyAsync(g.data(), L.gamma.p, sizeof(T) * g.size(), hipMemcpyDeviceToHost, s));
@@ -879,6 +880,8 @@ int stc_dcsr_upload(stc_ctx* ctx, int64_t n_rows, int64_t n_cols, const int64_t*
     m->cols = n_cols;
     m->nnz = nnz;
     m->dtype = value_dtype;
+    m->max_row = 0;
+    for (int64_t r = 0; r < n_rows; ++r) m->max_row = std::max(m->max_row, indptr[r + 1] - indptr[r]);
     m->indptr.reserve(8 * (n_rows + 1));
     m->indices.reserve(4 * std::max<int64_t>(nnz, 1));
     m->values.reserve((value_dtype == STC_F32 ? 4 : 8) * std::max<int64_t>(nnz, 1));

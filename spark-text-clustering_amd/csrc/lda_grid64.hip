@@ -5,7 +5,9 @@
 // other five lane bits a row lane rl; wave w, group g own KL = 13 topics [(2w+g)·13, +13), so k ≤ 104
 // takes W = 4 (k = 100: eight slices of 13).  A lane holds rows n = 32·j + rl (j < R, R = ⌈nnz/32⌉
 // chosen per document) of its slice: R·13 doubles = 26·R VGPRs for R ≤ 5; a sixth row set (nnz ≤ 192)
-// is read from LDS, which keeps the loop free of scratch spills at two waves per SIMD.
+// is read from LDS, which keeps the loop free of scratch spills at two waves per SIMD; a seventh and
+// eighth (nnz ≤ 256: long documents, and most of a planted-topic corpus at L = 200) are re-read from
+// expElogβ' in each pass (a few KB per document, L2-resident for the document's lifetime).
 //   φ_n = B_n·eθ : 13 lane-local fp64 FMAs per row, + the other group's partial through a 64-bit DPP
 //     row_ror:8 (lane i ↔ i^8), then the W wave partials meet in LDS behind the loop's one barrier;
 //     every wave adds them in the same order ⇒ bit-identical φ and r = cts/φ in every wave.
@@ -18,6 +20,10 @@
 // Numerics as lda.hip: Bp row-scaled by e^{-m_v}, Spark's 1e-100 carried as ε'_n = 1e-100·e^{-m_v}.
 #include "estep_common.h"
 
+#ifndef G64_LOAD_BATCH
+#define G64_LOAD_BATCH 3  // row sets whose B loads are in flight together in the load phase
+#endif
+
 namespace stc {
 namespace lda {
 
@@ -28,18 +34,19 @@ template <int W_, int KL_, int RMAX_>
 struct DShape {
   static constexpr int W = W_, KL = KL_, RMAX = RMAX_;
   static constexpr int RREG = 5;  // row sets per lane in VGPRs (26·5 = 130); a sixth goes to LDS
+  static constexpr int RLDS = RREG + 1;  // row sets past this one are streamed from expElogβ'
   static constexpr int KLP = (KL + 1) / 2 * 2;  // LDS slice pitch (ds_read_b128 granules)
 };
-using D26 = DShape<1, 13, 6>;   // k <= 26
-using D52 = DShape<2, 13, 6>;   // k <= 52
-using D104 = DShape<4, 13, 6>;  // k <= 104 (k = 100: 8 slices of 13 topics)
+using D26 = DShape<1, 13, 8>;   // k <= 26
+using D52 = DShape<2, 13, 8>;   // k <= 52
+using D104 = DShape<4, 13, 8>;  // k <= 104 (k = 100: 8 slices of 13 topics)
 
 template <class S>
 struct DLds {
   double eth[S::W][2][S::KLP] __attribute__((aligned(16)));
   // the load stage (one 32-row step of the wave's 2·KL columns) is dead once the loop starts
   union {
-    double phi[2][S::W][S::RMAX][64];
+    double phi[2][S::W][S::RMAX][32];  // per row lane (both groups hold the same joined φ)
     double stage[S::W][32 * 2 * S::KL];
   } __attribute__((aligned(16)));
   double red[2][S::W][2];
@@ -54,16 +61,18 @@ struct DLds {
 // cross-wave exchange of nd φ partials per lane + two wave-uniform scalars behind one barrier; every
 // wave combines them in the same order ⇒ bit-identical results in every wave.  Double-buffered by
 // parity: a buffer is reused only after every wave has passed the following barrier.
+// The two lane groups hold the same joined φ (a + b == b + a), so a row's slot is indexed by the row
+// lane: both groups store the same value to it.
 template <class S>
-__device__ __forceinline__ void xchg_d(DLds<S>& sm, int b, int wave, int lane, double* dot, int nd, double& x,
-                                       double& y) {
+__device__ __forceinline__ void xchg_d(DLds<S>& sm, int b, int wave, int lane, int rl, double* dot, int nd,
+                                       double& x, double& y) {
   constexpr int W = S::W;
   if constexpr (W > 1) {
-    double* const base = &sm.phi[0][0][0][0] + lane;
-    constexpr int BS = S::W * S::RMAX * 64, WS = S::RMAX * 64;
+    double* const base = &sm.phi[0][0][0][0] + rl;
+    constexpr int BS = S::W * S::RMAX * 32, WS = S::RMAX * 32;
     double* const mine = base + (b * BS + wave * WS);
 #pragma unroll
-    for (int j = 0; j < nd; ++j) mine[64 * j] = dot[j];
+    for (int j = 0; j < nd; ++j) mine[32 * j] = dot[j];
     if (lane == 0) {
       sm.red[b][wave][0] = x;
       sm.red[b][wave][1] = y;
@@ -73,16 +82,16 @@ __device__ __forceinline__ void xchg_d(DLds<S>& sm, int b, int wave, int lane, d
       const int o = wave ^ 1;
       const double* const other = base + (b * BS + o * WS);
 #pragma unroll
-      for (int j = 0; j < nd; ++j) dot[j] += other[64 * j];  // a + b == b + a: identical in both waves
+      for (int j = 0; j < nd; ++j) dot[j] += other[32 * j];  // a + b == b + a: identical in both waves
       x += sm.red[b][o][0];
       y += sm.red[b][o][1];
     } else {
       const double* const b0 = base + b * BS;
 #pragma unroll
       for (int j = 0; j < nd; ++j) {
-        double d = b0[64 * j];
+        double d = b0[32 * j];
 #pragma unroll
-        for (int w = 1; w < W; ++w) d += b0[w * WS + 64 * j];
+        for (int w = 1; w < W; ++w) d += b0[w * WS + 32 * j];
         dot[j] = d;
       }
       x = sm.red[b][0][0];
@@ -115,7 +124,8 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
 
   // ---- load in two dependent rounds with every address valid: (1) ids and counts; (2) m_v and the
   // B rows.  Rows past nnz read entry 0 / term 0 and are zeroed; columns past kp are clamped + zeroed.
-  constexpr int RG = R < S::RREG ? R : S::RREG;  // row sets held in VGPRs; the rest in sm.ovf
+  constexpr int RG = R < S::RREG ? R : S::RREG;  // row sets held in VGPRs; the next in sm.ovf
+  constexpr int RL = R < S::RLDS ? R : S::RLDS;  // row sets held on chip; [RL, R) are streamed
   double B[RG][KL];
   double* const ovf = sm.ovf[2 * wave + d.g] + rl;
   // B_{32j+rl, p} of this lane's slice, from registers or (j >= RG) from LDS
@@ -145,38 +155,63 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
   constexpr int NP = (32 * C2 + 63) / 64;         // pieces per lane per step
   const int wcol = wave * 2 * KL;                 // the wave's first column (even)
   double* const stg = sm.stage[wave];
+  // the loads of LB row sets are issued together (one memory latency per batch rather than per row
+  // set), then staged one row set at a time through the wave's stage buffer
 #pragma unroll
-  for (int j = 0; j < R; ++j) {
-    double2 pc[NP];
+  for (int j0 = 0; j0 < RL; j0 += G64_LOAD_BATCH) {
+    double2 pc[G64_LOAD_BATCH][NP];
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int c = lane + 64 * i;
-      const int srow = c / C2, q = c - srow * C2;
-      const int src_lane = (srow & 7) | ((srow >> 3) << 4);  // the group-0 lane holding row srow
-      const int id = __builtin_amdgcn_ds_bpermute(src_lane << 2, ids[j]);
-      const int col = wcol + 2 * q;
-      const double2 x = *reinterpret_cast<const double2*>(a.Bp + (int64_t)id * kp + min(col, kp - 2));
-      const bool keep = c < 32 * C2 && 32 * j + srow < nnz && col < kp;
-      pc[i] = keep ? x : make_double2(0.0, 0.0);
+    for (int jj = 0; jj < G64_LOAD_BATCH; ++jj) {
+      const int j = j0 + jj;
+      if (j >= RL) break;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int c = lane + 64 * i;
+        const int srow = c / C2, q = c - srow * C2;
+        const int src_lane = (srow & 7) | ((srow >> 3) << 4);  // the group-0 lane holding row srow
+        const int id = __builtin_amdgcn_ds_bpermute(src_lane << 2, ids[j]);
+        const int col = wcol + 2 * q;
+        const double2 x = *reinterpret_cast<const double2*>(a.Bp + (int64_t)id * kp + min(col, kp - 2));
+        const bool keep = c < 32 * C2 && 32 * j + srow < nnz && col < kp;
+        pc[jj][i] = keep ? x : make_double2(0.0, 0.0);
+      }
     }
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int c = lane + 64 * i;
-      if (c < 32 * C2) *reinterpret_cast<double2*>(stg + 2 * c) = pc[i];  // row c / C2, piece c % C2
-    }
-    __builtin_amdgcn_wave_barrier();  // one wave writes and reads its stage; LDS is in order per wave
-    const double* mine = stg + rl * 2 * KL + d.g * KL;
+    for (int jj = 0; jj < G64_LOAD_BATCH; ++jj) {
+      const int j = j0 + jj;
+      if (j >= RL) break;
 #pragma unroll
-    for (int p = 0; p < KL; ++p) {
-      if (j < RG) B[j < RG ? j : 0][p] = mine[p];
-      else ovf[32 * p] = mine[p];  // read back only by this lane
+      for (int i = 0; i < NP; ++i) {
+        const int c = lane + 64 * i;
+        if (c < 32 * C2) *reinterpret_cast<double2*>(stg + 2 * c) = pc[jj][i];  // row c / C2, piece c % C2
+      }
+      __builtin_amdgcn_wave_barrier();  // one wave writes and reads its stage; LDS is in order per wave
+      const double* mine = stg + rl * 2 * KL + d.g * KL;
+#pragma unroll
+      for (int p = 0; p < KL; ++p) {
+        if (j < RG) B[j < RG ? j : 0][p] = mine[p];
+        else ovf[32 * p] = mine[p];  // read back only by this lane
+      }
+      __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_wave_barrier();
   }
   // ε'_n = 1e-100·e^{-m_v} held as 2^53·ε'_n (the ballot below asks 2^53·ε' ≥ φ directly), capped at
   // 1e300 where e^{-m_v} overflows (Spark's unscaled expElogβ row is then 0 and the row contributes
   // nothing; r ≈ cts·1e-284 reproduces that without an ∞ in the Newton reciprocal).  Padding rows
   // hold −2^53 (φ = −1, r = −0, never live).
+  // streamed row sets: the lane's KL entries of row 32·j + rl, zero past nnz and past kp.  The offset
+  // goes through an empty asm each pass so the loads stay inside the loop (hoisted, they would spill)
+  const int64_t col0 = d.t0;
+  auto stream_row = [&](int j, double* y) {
+    int64_t off = (int64_t)ids[j] * kp;
+    asm volatile("" : "+v"(off));
+    const bool v = 32 * j + rl < nnz;
+#pragma unroll
+    for (int p = 0; p < KL; ++p) {
+      const double x = a.Bp[off + min(col0 + p, (int64_t)kp - 1)];
+      y[p] = (v && col0 + p < kp) ? x : 0.0;
+    }
+  };
   if (wave == 0 && d.g == 0) {
 #pragma unroll
     for (int j = 0; j < R; ++j)
@@ -188,7 +223,7 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
 
   if (nonempty) {
     double gsum = d.gsum, asum = d.asum, dsum = 0.0, dummy = 0.0;
-    xchg_d<S>(sm, 1, wave, lane, nullptr, 0, gsum, asum);
+    xchg_d<S>(sm, 1, wave, lane, rl, nullptr, 0, gsum, asum);
     d.asum = asum;
     // eθ = exp(ψ(γ) − ψ(Σγ)): Spark's unscaled exp(E[log θ]); inside the loop ψ(Σγ') comes from the
     // Σα + Σcts − Σ cts·ε'/φ identity, so without live ε' it is one constant per document
@@ -216,9 +251,20 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
         for (int c = 0; c < KLP / 2; ++c) {
           const double2 e = *reinterpret_cast<const double2*>(my_eth + 2 * c);
 #pragma unroll
-          for (int j = 0; j < R; ++j) {
+          for (int j = 0; j < RL; ++j) {
             acc[j] = fma(BV(j, 2 * c), e.x, acc[j]);
             if (2 * c + 1 < KL) acc[j] = fma(BV(j, 2 * c + 1), e.y, acc[j]);
+          }
+        }
+#pragma unroll
+        for (int j = RL; j < R; ++j) {
+          double y[KL];
+          stream_row(j, y);
+#pragma unroll
+          for (int c = 0; c < KLP / 2; ++c) {
+            const double2 e = *reinterpret_cast<const double2*>(my_eth + 2 * c);
+            acc[j] = fma(y[2 * c], e.x, acc[j]);
+            if (2 * c + 1 < KL) acc[j] = fma(y[2 * c + 1], e.y, acc[j]);
           }
         }
 #pragma unroll
@@ -226,7 +272,7 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
       }
       // Σ|Δγ| of the last update rides along with the φ exchange
       dsum = wave_sum_d(dg);
-      xchg_d<S>(sm, it & 1, wave, lane, dot, R, dsum, dummy);
+      xchg_d<S>(sm, it & 1, wave, lane, rl, dot, R, dsum, dummy);
       // Spark: while (meanGammaChange > 1e-3), meanGammaChange = Σ|Δγ| / k.  Wave-uniform by
       // construction; readfirstlane makes the loop a scalar loop
       const bool last =
@@ -260,8 +306,15 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
       for (int p = 0; p < KL; ++p) {
         double x = 0.0;
 #pragma unroll
-        for (int j = 0; j < R; ++j) x = fma(BV(j, p), rr[j], x);
+        for (int j = 0; j < RL; ++j) x = fma(BV(j, p), rr[j], x);
         flat[p] = x;
+      }
+#pragma unroll
+      for (int j = RL; j < R; ++j) {
+        double y[KL];
+        stream_row(j, y);
+#pragma unroll
+        for (int p = 0; p < KL; ++p) flat[p] = fma(y[p], rr[j], flat[p]);
       }
       double ys1[N1];
 #pragma unroll
@@ -322,7 +375,10 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
   return nonempty;
 }
 
-template <class S, bool STATS, bool BOUND>
+// LONG = false: documents with ≤ RLDS row sets; LONG = true: the streamed ones (nnz > 32·RLDS).  Both
+// kernels run over the same slots and each skips the other's documents, so the streamed variants'
+// register pressure stays out of the common kernel.
+template <class S, bool STATS, bool BOUND, bool LONG>
 __global__ __launch_bounds__(64 * S::W, 2) void k_estep_grid64(EStepArgs<double> a) {
   constexpr int W = S::W, KL = S::KL;
   constexpr int N1 = hup(KL), N2 = hup(N1), N3 = hup(N2), N4 = hup(N3), N5 = hup(N4);
@@ -338,6 +394,8 @@ __global__ __launch_bounds__(64 * S::W, 2) void k_estep_grid64(EStepArgs<double>
   d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
   d.s0 = a.indptr[d.row];
   d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
+  const int rsets = (d.nnz + 31) >> 5;
+  if (LONG ? rsets <= S::RLDS : rsets > S::RLDS) return;  // the other kernel's document
   d.e0 = a.bptr ? a.bptr[d.slot] : d.s0;
   d.k = a.k;
   d.kp = a.kp;
@@ -379,14 +437,20 @@ __global__ __launch_bounds__(64 * S::W, 2) void k_estep_grid64(EStepArgs<double>
 
   // rows per lane for this document (block-uniform); the partition guarantees nnz <= 32·RMAX
   bool nonempty = false;
-  switch ((d.nnz + 31) >> 5) {
-    case 0:
-    case 1: nonempty = grid64_core<S, 1, STATS, BOUND>(a, sm, d); break;
-    case 2: nonempty = grid64_core<S, 2, STATS, BOUND>(a, sm, d); break;
-    case 3: nonempty = grid64_core<S, 3, STATS, BOUND>(a, sm, d); break;
-    case 4: nonempty = grid64_core<S, 4, STATS, BOUND>(a, sm, d); break;
-    case 5: nonempty = grid64_core<S, 5, STATS, BOUND>(a, sm, d); break;
-    default: nonempty = grid64_core<S, 6, STATS, BOUND>(a, sm, d); break;
+  static_assert(S::RLDS == 6 && S::RMAX == 8, "row-set cases below");
+  if constexpr (LONG) {
+    if (rsets == 7) nonempty = grid64_core<S, 7, STATS, BOUND>(a, sm, d);
+    else nonempty = grid64_core<S, 8, STATS, BOUND>(a, sm, d);
+  } else {
+    switch (rsets) {
+      case 0:
+      case 1: nonempty = grid64_core<S, 1, STATS, BOUND>(a, sm, d); break;
+      case 2: nonempty = grid64_core<S, 2, STATS, BOUND>(a, sm, d); break;
+      case 3: nonempty = grid64_core<S, 3, STATS, BOUND>(a, sm, d); break;
+      case 4: nonempty = grid64_core<S, 4, STATS, BOUND>(a, sm, d); break;
+      case 5: nonempty = grid64_core<S, 5, STATS, BOUND>(a, sm, d); break;
+      default: nonempty = grid64_core<S, 6, STATS, BOUND>(a, sm, d); break;
+    }
   }
 
   // ---- topic-level outputs, once per kernel
@@ -406,7 +470,7 @@ __global__ __launch_bounds__(64 * S::W, 2) void k_estep_grid64(EStepArgs<double>
   }
   // exact Σγ of the final γ (outputs and bound); the loop's last barrier used buffer it & 1
   double gsum = wave_sum_d(d.own ? d.gam : 0.0), dummy = 0.0;
-  xchg_d<S>(sm, (d.it + 1) & 1, wave, lane, nullptr, 0, gsum, dummy);
+  xchg_d<S>(sm, (d.it + 1) & 1, wave, lane, d.rl, nullptr, 0, gsum, dummy);
   const double psisum = digamma_t<double>(gsum);
   if (d.own) {
     if (a.gamma) a.gamma[mem * k + t] = d.gam;
@@ -446,14 +510,21 @@ __global__ __launch_bounds__(64 * S::W, 2) void k_estep_grid64(EStepArgs<double>
   }
 }
 
-template <class S>
-void launch_d(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound) {
+template <class S, bool LONG>
+void launch_d1(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound) {
   const dim3 grid((unsigned)a.n);
   const int threads = 64 * S::W;
-  if (stats) k_estep_grid64<S, true, false><<<grid, threads, 0, s>>>(a);
-  else if (bound) k_estep_grid64<S, false, true><<<grid, threads, 0, s>>>(a);
-  else k_estep_grid64<S, false, false><<<grid, threads, 0, s>>>(a);
+  if (stats) k_estep_grid64<S, true, false, LONG><<<grid, threads, 0, s>>>(a);
+  else if (bound) k_estep_grid64<S, false, true, LONG><<<grid, threads, 0, s>>>(a);
+  else k_estep_grid64<S, false, false, LONG><<<grid, threads, 0, s>>>(a);
   KERNEL_CHECK();
+}
+// the streamed-row documents first (longest first), then the rest; `long_docs` = false when the
+// caller knows no document has more than 32·RLDS rows
+template <class S>
+void launch_d(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs) {
+  if (long_docs) launch_d1<S, true>(s, a, stats, bound);
+  launch_d1<S, false>(s, a, stats, bound);
 }
 
 }  // namespace
@@ -462,12 +533,13 @@ int grid64_row_cap(int k) {
   if (k <= 104) return 32 * D104::RMAX;
   return 0;
 }
+int grid64_onchip_rows(int k) { return k <= 104 ? 32 * D104::RLDS : 0; }
 
-void launch_estep_grid64(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound) {
+void launch_estep_grid64(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs) {
   if (a.n == 0) return;
-  if (a.k <= 26) launch_d<D26>(s, a, stats, bound);
-  else if (a.k <= 52) launch_d<D52>(s, a, stats, bound);
-  else if (a.k <= 104) launch_d<D104>(s, a, stats, bound);
+  if (a.k <= 26) launch_d<D26>(s, a, stats, bound, long_docs);
+  else if (a.k <= 52) launch_d<D52>(s, a, stats, bound, long_docs);
+  else if (a.k <= 104) launch_d<D104>(s, a, stats, bound, long_docs);
   else throw Error(STC_ERR_INVALID_ARG, "fp64 grid E-step: k > 104");
 }
 

@@ -82,7 +82,8 @@ int grid_row_cap(int k);
 void launch_estep_grid(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound);
 // fp64 grid E-step (lda_grid64.hip): k <= 104, nnz <= grid64_row_cap(k) (0 if n/a).
 int grid64_row_cap(int k);
-void launch_estep_grid64(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound);
+int grid64_onchip_rows(int k);  // rows past this are streamed (a second launch, `long_docs`)
+void launch_estep_grid64(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs);
 // many-topic E-step (lda_wide.hip): topics across a 512-thread workgroup, k <= 2048, nnz <= wide_row_cap(k)
 int wide_row_cap(int k);
 template <typename T>

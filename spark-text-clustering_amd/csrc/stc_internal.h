@@ -110,6 +110,7 @@ struct Ctx {
 struct DCsr {
   Ctx* ctx = nullptr;
   int64_t rows = 0, cols = 0, nnz = 0;
+  int64_t max_row = -1;  // longest row's nnz when known (host uploads), −1 otherwise
   int dtype = STC_F64;
   DevBuf indptr;   // int64[rows+1]
   DevBuf indices;  // int32[nnz]

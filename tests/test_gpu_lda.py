@@ -379,3 +379,33 @@ def test_slot_order_longest_first_same_model(ctx, monkeypatch):
     assert i0 == i1 == 5
     np.testing.assert_allclose(l1, l0, rtol=1e-10, atol=0)
     np.testing.assert_allclose(a1, a0, rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("with_replacement", [False, True])
+def test_init_random_and_next_match_oracle(ctx, oracle, with_replacement):
+    """A5 + A6 exactly: stc_lda_init_random's λ₀ (oracle.init_lambda), next()'s device-sampled
+    membership (oracle.sample_members: Bernoulli / Poisson per doc, the draw counter advancing per
+    call) and the counter-RNG γ₀ of each member (oracle.gamma_init keyed by train_doc_key), then three
+    next() calls vs three oracle submit_minibatch calls on those members: λ and α to 1e-9 (fp64)."""
+    rng = np.random.default_rng(21)
+    D, V, k, f, seed = 240, 700, 12, 0.1, 77
+    corpus = random_corpus(rng, D, V, 1, 40, empty_every=17)
+    h, _ = _handle(ctx, corpus, k, "f64", None, mini_batch_fraction=f, seed=seed,
+                   sample_with_replacement=with_replacement, optimize_doc_concentration=True)
+    h.init_random(seed)
+    lam0 = oracle.init_lambda(seed, V, k)
+    np.testing.assert_allclose(h.topics(), lam0, rtol=1e-14)
+    assert abs(lam0.mean() - 1.0) < 0.01 and abs(lam0.var() - 0.01) < 0.002  # Gamma(100, 1/100)
+    alpha, eta = oracle.resolve_alpha_eta(k)
+    state = oracle.OnlineLDAState(lam=lam0.T.copy(), alpha=alpha, eta=eta, corpus_size=D,
+                                  mini_batch_fraction=f, optimize_doc_concentration=True)
+    for draw in (1, 2, 3):
+        members = oracle.sample_members(seed, draw, 0, D, f, with_replacement)
+        assert members, draw
+        st = h.next()
+        assert st["batch_docs"] == len(members), (draw, st["batch_docs"], len(members))
+        it = state.iteration + 1
+        g0 = [oracle.gamma_init(seed, oracle.train_doc_key(it, 0, pos), k) for pos in range(len(members))]
+        oracle.submit_minibatch(state, [corpus.row(d) for d in members], g0)
+    np.testing.assert_allclose(h.topics(), state.lam.T, rtol=1e-9)
+    np.testing.assert_allclose(h.alpha(), state.alpha, rtol=1e-9)
