@@ -62,6 +62,11 @@ struct stc_lda {
   const DCsr* order_for = nullptr;
   bool hot_order = true;  // STC_HOT_ORDER=0: CSR order
   int64_t wave_cap = 0;  // docs with nnz <= wave_cap run the wave-per-document E-step
+  // many-topic documents larger than one CU: a team of P CUs per document (lda_wide.hip
+  // k_estep_wide_mc); STC_WIDE_TEAM=n forces P = n (1: the one-CU kernel)
+  int team_force = 0;
+  DevBuf team_words, team_x;
+  unsigned* htmo = nullptr;  // pinned copy of the team kernel's timeout word
 
   // M-step sharding over the vocabulary (multi-GPU): rank r owns λ / expElogβ rows [r·Vs, (r+1)·Vs);
   // Vs is a multiple of the λ-update block so the per-block colsum partials (and hence colsum) are
@@ -98,6 +103,7 @@ struct stc_lda {
         if (e) (void)hipEventDestroy(e);
     if (hcnt) (void)hipHostFree(hcnt);
     if (hpre) (void)hipHostFree(hpre);
+    if (htmo) (void)hipHostFree(htmo);
     if (ev_pre) (void)hipEventDestroy(ev_pre);
   }
 };
@@ -339,16 +345,69 @@ void ensure_order(stc_lda& L) {
   L.order_for = L.corpus;
 }
 
-// fast kernel on slots [0, n_short), workgroup kernel on [n_short, n)
+// team size for the many-topic kernel: enough CUs that a document of `mean_rows` rows is resident
+// (measured, configs 4/5: a team pays for k ≤ 512 — config 4's k = 500, 1.6× in both dtypes — but not
+// at k = 2000, where the 16 KB of partials per member and iteration cost more than the re-streamed rows)
+template <typename T>
+int team_size(const stc_lda& L, double mean_rows) {
+  if (L.team_force > 0) return std::min(L.team_force, 4);
+  if (L.k > 512) return 1;
+  const int res = lda::wide_resident_rows<T>(L.k);
+  const int P = (int)std::ceil(mean_rows * 1.05 / std::max(res, 1));
+  return std::max(1, std::min(P, 4));
+}
+
+// the team kernel's timeout word (copied to pinned memory after each launch; read once the stream has
+// passed it): a team whose partner never arrived gave up instead of hanging
+void check_team_timeout(stc_lda& L) {
+  if (L.htmo && *L.htmo) {
+    *L.htmo = 0;
+    throw Error(STC_ERR_HIP, "many-topic team E-step: a team member did not arrive (timed out)");
+  }
+}
+
+template <typename T>
+void launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, int P) {
+  Ctx& c = *L.ctx;
+  hipStream_t s = c.stream;
+  int cus = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c.device));
+  lda::WideTeam wt;
+  wt.P = P;
+  wt.blocks = 8 * P * (cus / (8 * P));
+  STC_REQUIRE(wt.blocks > 0, "team E-step: too few CUs");
+  const int teams = wt.blocks / P;
+  wt.xstride = L.kp + 1;  // granules per member: the s partials + Σ r·φ
+  const size_t xbytes = 16 * (size_t)teams * 2 * P * (size_t)wt.xstride;
+  L.team_words.reserve(16);
+  L.team_x.reserve(xbytes);
+  if (!L.htmo) {
+    HIP_CHECK(hipHostMalloc((void**)&L.htmo, sizeof(unsigned), hipHostMallocDefault));
+    *L.htmo = 0;
+  }
+  wt.tmo = L.team_words.as<unsigned>();
+  wt.xbuf = L.team_x.p;
+  // every polled word zeroed before every launch: the timeout word, and the granules' epoch tags
+  // (a tag left by an earlier launch could equal an epoch this launch waits for)
+  HIP_CHECK(hipMemsetAsync(L.team_words.p, 0, 16, s));
+  HIP_CHECK(hipMemsetAsync(L.team_x.p, 0, xbytes, s));
+  lda::launch_estep_wide_mc<T>(s, w, stats, wt);
+  HIP_CHECK(hipMemcpyAsync(L.htmo, wt.tmo, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+}
+
+// fast kernel on slots [0, n_short), workgroup kernel on [n_short, n); mean_rows = the launch's mean
+// entries per document (the many-topic kernel's team size)
 template <typename T>
 void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int64_t n_short, bool stats,
-                  bool bound) {
+                  bool bound, double mean_rows) {
   hipStream_t s = L.ctx->stream;
   if (n_short > 0) {
     lda::EStepArgs<T> w = a;
     w.slot0 = 0;
     w.n = n_short;
-    if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
+    const int P = use_wide(L.k, L.dtype) && !bound ? team_size<T>(L, mean_rows) : 1;
+    if (P > 1) launch_wide_team<T>(L, w, stats, P);
+    else if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
     else if constexpr (std::is_same<T, float>::value) lda::launch_estep_wave(s, w, stats, bound);
     else lda::launch_estep_grid64(s, w, stats, bound, m.max_row < 0 || m.max_row > lda::grid64_onchip_rows(L.k));
   }
@@ -398,7 +457,8 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   a.iters = L.iters.as<int32_t>();
   a.nonempty = L.nonempty.as<int32_t>();
   record(L, 1);
-  launch_split<T>(L, *L.corpus, a, n, n_short, true, false);
+  check_team_timeout(L);
+  launch_split<T>(L, *L.corpus, a, n, n_short, true, false, n > 0 ? (double)E / (double)n : 0.0);
   record(L, 2);
   HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.vpad * L.kp, s));  // padded rows stay zero
   if (E > 0) {
@@ -700,7 +760,8 @@ void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const
   a.gamma = gamma_out ? L.gamma.as<T>() : nullptr;
   a.iters = L.iters.as<int32_t>();
   a.bound = bound ? L.bound.as<double>() : nullptr;
-  launch_split<T>(L, docs, a, n, p.n_short, false, bound);
+  check_team_timeout(L);
+  launch_split<T>(L, docs, a, n, p.n_short, false, bound, n > 0 ? (double)docs.nnz / (double)n : 0.0);
   if (gamma_out && n > 0) {
     std::vector<T> g((size_t)(n * L.k));
     HIP_CHECK(hipMemcpyAsync(g.data(), L.gamma.p, sizeof(T) * g.size(), hipMemcpyDeviceToHost, s));
@@ -1262,6 +1323,8 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->hot_order = !(ho && ho[0] == '0');
     const char* sd = std::getenv("STC_SORT_DOCS");
     L->sort_docs = !(sd && sd[0] == '0');
+    const char* wt = std::getenv("STC_WIDE_TEAM");
+    L->team_force = wt ? std::max(0, std::min(4, std::atoi(wt))) : 0;
     const char* fc = std::getenv("STC_COLLECTIVE_MSTEP");
     L->force_coll = fc && fc[0] == '1';
     ensure_layout(*L);  // λ, Bp, stat, logscale, colpart for the current shard count

@@ -86,6 +86,18 @@ int grid64_onchip_rows(int k);  // rows past this are streamed (a second launch,
 void launch_estep_grid64(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs);
 // many-topic E-step (lda_wide.hip): topics across a 512-thread workgroup, k <= 2048, nnz <= wide_row_cap(k)
 int wide_row_cap(int k);
+// a team of P CUs per document for the many-topic E-step (lda_wide.hip k_estep_wide_mc)
+struct WideTeam {
+  int P = 1;                 // workgroups (CUs) per document
+  int blocks = 0;            // persistent grid: a multiple of 8·P, ≤ the CU count
+  unsigned* tmo = nullptr;   // timeout word (zeroed before each launch)
+  void* xbuf = nullptr;      // [teams][2][P][xstride] 16-byte {epoch, value} granules (zeroed before each launch)
+  int64_t xstride = 0;       // granules per member: kp + 1 (s partials, Σ r·φ)
+};
+template <typename T>
+int wide_resident_rows(int k);
+template <typename T>
+void launch_estep_wide_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt);
 template <typename T>
 void launch_estep_wide(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound);
 

@@ -491,6 +491,378 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_estep_wide_mc — the same fixed point with one document's ROWS split over a team of P workgroups
+// (P CUs), so a block larger than one CU's registers + LDS (fp64 config 4: 371 × 500 × 8 B = 1.5 MB;
+// fp64 config 5: 44 × 2000 × 8 B = 0.7 MB) stays resident instead of being re-streamed from the MALL
+// twice per iteration.  Member m holds rows [m·nnz/P, (m+1)·nnz/P) for all topics:
+//   φ_n, r_n  : local (a member has every topic of its rows);
+//   s = Bᵀr   : a partial per member, exchanged once per iteration with Σ_n r_n·φ_n (the ψ(Σγ')
+//               identity); every member sums the P partials in member order, so γ, eθ and the stop
+//               rule are bit-identical in every member and the team leaves the loop together.
+// Persistent: G = 8·P·⌊CUs/(8P)⌋ blocks (one per CU: the kernel takes all 160 KB of LDS), launched
+// cooperatively (the runtime checks the grid is resident); team members share blockIdx % 8 (one XCD,
+// for L2 locality only).  Exchange (cdna_hip_programming.md Guideline 16, R2: the data is the flag):
+// every value travels in a 16-byte granule {epoch, value} written by ONE 16-B sc1 buffer store and
+// read by 16-B sc1 buffer loads (untorn on gfx950); each consumer wave re-reads its granules until
+// every tag equals the epoch — no flag, no fence, no block barrier.  Granules double-buffered by epoch
+// parity (a member can run at most one exchange ahead, so a slot never holds a newer epoch than the
+// one awaited).  Every spin is bounded: on timeout the kernel sets the timeout word and every team
+// leaves (the host reports it as an error).
+typedef __attribute__((address_space(1))) unsigned int gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+  if constexpr (sizeof(T) == 8)
+    __hip_atomic_store((gu64*)p, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    __hip_atomic_store((gu32*)p, __builtin_bit_cast(unsigned int, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+  if constexpr (sizeof(T) == 8)
+    return __builtin_bit_cast(T, __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  else
+    return __builtin_bit_cast(T, __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+constexpr unsigned kSpinLimit = 1u << 22;  // a few seconds of polling: far past any legitimate wait
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSc1 = 16;  // buffer aux bit: sc1 (write-through store / L1-bypassing load)
+
+template <typename T>
+__device__ __forceinline__ void put_granule(__amdgpu_buffer_rsrc_t rs, int idx, unsigned epoch, T v) {
+  unsigned long long bits;
+  if constexpr (sizeof(T) == 8) bits = __builtin_bit_cast(unsigned long long, v);
+  else bits = __builtin_bit_cast(unsigned int, v);
+  const u32x4 g = {epoch, 0u, (unsigned)bits, (unsigned)(bits >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(g, rs, idx * 16, 0, kSc1);
+}
+template <typename T>
+__device__ __forceinline__ bool get_granule(__amdgpu_buffer_rsrc_t rs, int idx, unsigned epoch, T& v) {
+  const u32x4 g = __builtin_amdgcn_raw_buffer_load_b128(rs, idx * 16, 0, kSc1);
+  const unsigned long long bits = ((unsigned long long)g.w << 32) | g.z;
+  if constexpr (sizeof(T) == 8) v = __builtin_bit_cast(T, bits);
+  else v = __builtin_bit_cast(T, (unsigned)bits);
+  return g.x == epoch;
+}
+__device__ __forceinline__ bool spin_give_up(unsigned spins, unsigned* tmo) {
+  if (spins < kSpinLimit &&
+      __hip_atomic_load((gu32*)tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    return false;
+  __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+template <typename T, int Q, int NR, bool STATS>
+__global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int nl, WideTeam wt) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  WLds<T>& sm = *reinterpret_cast<WLds<T>*>(smem);
+  T* const sB = reinterpret_cast<T*>(smem + wide_lds_fixed<T>());  // [nl][512·Q]
+  __shared__ int s_abort;
+  using Tr = WTr<T>;
+  constexpr int CH = wide_chunk<T, Q>();
+  constexpr int LB = (int)(WIDE_LB_BYTES / (sizeof(T) * Q)) < CH ? (int)(WIDE_LB_BYTES / (sizeof(T) * Q)) : CH;
+  const int P = wt.P;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = (int)blockIdx.x, il = b / 8;
+  const int member = il % P, team = (il / P) * 8 + (b % 8), nteams = (int)gridDim.x / P;
+  // this team's granules [parity][member][xstride], 16 B each
+  const int team_granules = 2 * P * (int)wt.xstride;
+  unsigned char* const xb = reinterpret_cast<unsigned char*>(wt.xbuf) + (int64_t)team * team_granules * 16;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(xb, 0, team_granules * 16, 0x00020000);
+  const int k = a.k, kp = a.kp, t0 = Q * tid;
+  unsigned epoch = 0;
+  if (tid == 0) s_abort = 0;
+
+  for (int64_t j = team; j < a.n; j += nteams) {
+    const int64_t slot = a.slot0 + j;
+    const int64_t row = a.batch ? (int64_t)a.batch[slot] : slot;
+    const int64_t mem = a.orig ? (int64_t)a.orig[slot] : slot;
+    const int64_t s0 = a.indptr[row];
+    const int nnz = (int)(a.indptr[row + 1] - s0);
+    const int64_t e0 = a.bptr ? a.bptr[slot] : s0;
+    const int lo = (int)((int64_t)member * nnz / P), hi = (int)((int64_t)(member + 1) * nnz / P);
+    const int nloc = hi - lo;  // this member's rows (≤ 512 / P ... ≤ 512)
+    const int nres = NR + nl;
+
+    // ---- every row's count (the document's emptiness is a team-wide decision); this member's rows
+    T cts = T(0), eps = T(0);
+    int any = 0;
+    if (tid < nnz) {
+      const int64_t pos = s0 + (a.order ? a.order[s0 + tid] : tid);
+      any = a.values[pos] != T(0);
+    }
+    if (tid < nloc) {
+      const int n = lo + tid;
+      const int64_t pos = s0 + (a.order ? a.order[s0 + n] : n);
+      const int id = a.indices[pos];
+      cts = a.values[pos];
+      sm.ids[tid] = id;
+      eps = fmin(fmax((T)fmin(exp(kLogEps - a.logscale[id]), 1e300), Tr::eps_floor()), Tr::eps_cap());
+    }
+    const bool nonempty = __syncthreads_or(any) != 0;
+
+    uint64_t stream = 0;
+    if (!a.gamma0) {
+      const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, mem) : (uint64_t)(a.doc_id_base + row);
+      stream = doc_stream(a.seed, key);
+    }
+    T gam[Q], alp[Q], eth[Q];
+    T gs = T(0), as = T(0);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int t = t0 + q;
+      gam[q] = t < k ? (a.gamma0 ? a.gamma0[mem * k + t] : (T)gamma_sample(stream, t, a.gamma_shape)) : T(0);
+      alp[q] = t < k ? (T)a.alpha[t] : T(0);
+      gs += gam[q];
+      as += alp[q];
+    }
+    if (!nonempty) {
+      if (member == 0) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const int t = t0 + q;
+          if (t < k) {
+            if (a.gamma) a.gamma[mem * k + t] = T(0);
+            if (STATS) a.elogth[slot * k + t] = T(0);
+          }
+          if (STATS && t < kp) a.eth[slot * kp + t] = T(0);
+        }
+        if (tid == 0) {
+          if (a.iters) a.iters[mem] = 0;
+          if (a.nonempty) a.nonempty[mem] = 0;
+        }
+      }
+      if (tid < nloc) {
+        const int n = lo + tid;
+        a.r[e0 + n] = T(0);
+        if (STATS) {
+          a.keys[e0 + n] = (uint32_t)sm.ids[tid];
+          a.vals[e0 + n] = entry_val<T>(slot, e0 + n, T(0));
+        }
+      }
+      __syncthreads();  // sm.ids is rewritten by the next document
+      continue;
+    }
+    // Σγ₀, Σα over the block (identical in every member)
+    gs = Tr::wsum(gs);
+    as = Tr::wsum(as);
+    if (lane == 0) {
+      sm.xs[wave][0] = gs;
+      sm.xs[wave][1] = as;
+    }
+    __syncthreads();
+    gs = sm.xs[0][0];
+    as = sm.xs[0][1];
+#pragma unroll
+    for (int w = 1; w < kWWaves; ++w) {
+      gs += sm.xs[w][0];
+      as += sm.xs[w][1];
+    }
+    __syncthreads();
+
+    // ---- this member's block: local rows < NR in VGPRs, < NR + nl in LDS, the rest streamed
+    T B[NR > 0 ? NR : 1][Q];
+#pragma unroll
+    for (int n = 0; n < NR; ++n) {
+      if (n < nloc) load_q<T, Q>(a.Bp, (int64_t)sm.ids[n], kp, t0, B[n]);
+      else {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) B[n][q] = T(0);
+      }
+    }
+    for (int n = NR; n < nres && n < nloc; ++n) {
+      T x[Q];
+      load_q<T, Q>(a.Bp, (int64_t)sm.ids[n], kp, t0, x);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) sB[(int64_t)(n - NR) * (kWThreads * Q) + t0 + q] = x[q];
+    }
+
+    T cs = Tr::psi(gs);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) eth[q] = (t0 + q < k) ? Tr::eth(gam[q], cs) : T(0);
+    T dg = T(0);
+    int it = 0;
+    const T kd = (T)k;
+    T rfin = T(0);
+    while (true) {
+      // Phase A over the local rows (as k_estep_wide)
+#pragma unroll
+      for (int c = 0; c < NR / CH; ++c) {
+        if (CH * c < nloc) {
+          T x[CH];
+#pragma unroll
+          for (int i = 0; i < CH; ++i) {
+            T acc = T(0);
+#pragma unroll
+            for (int q = 0; q < Q; ++q) acc = fma(B[CH * c + i][q], eth[q], acc);
+            x[i] = acc;
+          }
+          const T v = rs_chunk<T, CH>(x, lane);
+          const int n = CH * c + rs_row<CH>(lane);
+          if (rs_pub<CH>(lane) && n < nloc) sm.xs[wave][n] = v;
+        }
+      }
+      for (int n0 = NR; n0 < nloc; n0 += CH) {
+        T x[CH];
+#pragma unroll
+        for (int bb = 0; bb < CH; bb += LB) {
+          T y[LB][Q];
+          rows_q<T, Q, LB>(a.Bp, sm.ids, sB, kp, t0, NR, nres, nloc, n0 + bb, y);
+#pragma unroll
+          for (int i = 0; i < LB; ++i) {
+            T acc = T(0);
+#pragma unroll
+            for (int q = 0; q < Q; ++q) acc = fma(y[i][q], eth[q], acc);
+            x[bb + i] = acc;
+          }
+        }
+        const T v = rs_chunk<T, CH>(x, lane);
+        const int n = n0 + rs_row<CH>(lane);
+        if (rs_pub<CH>(lane) && n < nloc) sm.xs[wave][n] = v;
+      }
+      const T dsum_w = Tr::wsum(dg);
+      if (lane == 0) sm.red[0][wave] = dsum_w;
+      __syncthreads();  // (1) row sums and Σ|Δγ| published (and any wave's give-up in s_abort)
+      if (s_abort) break;
+      T dsum = sm.red[0][0];
+#pragma unroll
+      for (int w = 1; w < kWWaves; ++w) dsum += sm.red[0][w];
+      const bool last = (it > 0 && dsum / kd <= T(1e-3)) || it >= a.max_iter;  // team-uniform
+      T rd = T(0);
+      if (tid < nloc) {
+        T dot = sm.xs[0][tid];
+#pragma unroll
+        for (int w = 1; w < kWWaves; ++w) dot += sm.xs[w][tid];
+        const T r = cts * Tr::rcp(dot + eps);
+        sm.rr[tid] = r;
+        rfin = r;
+        rd = fma(r, dot, rd);
+      }
+      rd = Tr::wsum(rd);
+      if (lane == 0) sm.red[1][wave] = rd;
+      __syncthreads();  // (2) r and Σ r·dot published
+      if (last) break;
+      T sgl = sm.red[1][0];
+#pragma unroll
+      for (int w = 1; w < kWWaves; ++w) sgl += sm.red[1][w];
+
+      // Phase B: this member's partial s over its rows
+      T s[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) s[q] = T(0);
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        if (n < nloc) {
+          const T r = sm.rr[n];
+#pragma unroll
+          for (int q = 0; q < Q; ++q) s[q] = fma(B[n][q], r, s[q]);
+        }
+      }
+      for (int n0 = NR; n0 < nloc; n0 += LB) {
+        T y[LB][Q];
+        rows_q<T, Q, LB>(a.Bp, sm.ids, sB, kp, t0, NR, nres, nloc, n0, y);
+#pragma unroll
+        for (int i = 0; i < LB; ++i) {
+          const T r = n0 + i < nloc ? sm.rr[n0 + i] : T(0);
+#pragma unroll
+          for (int q = 0; q < Q; ++q) s[q] = fma(y[i][q], r, s[q]);
+        }
+      }
+      // ---- exchange: publish (s partial, Σ r·dot partial) as epoch granules, then every wave
+      // collects the other members' granules for its lanes' topics; sums in member order
+      ++epoch;
+      const int base = (int)(epoch & 1) * P * (int)wt.xstride;
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (t0 + q < kp) put_granule<T>(rs, base + member * (int)wt.xstride + t0 + q, epoch, s[q]);
+      if (tid == 0) put_granule<T>(rs, base + member * (int)wt.xstride + kp, epoch, sgl);
+      T st[Q];
+      T sg = T(0);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) st[q] = T(0);
+      for (int m = 0; m < P; ++m) {
+        if (m == member) {
+#pragma unroll
+          for (int q = 0; q < Q; ++q) st[q] += s[q];
+          sg += sgl;
+          continue;
+        }
+        const int g0 = base + m * (int)wt.xstride;
+        T v[Q], vs = T(0);
+        for (unsigned spins = 0;; ++spins) {
+          bool ok = get_granule<T>(rs, g0 + kp, epoch, vs);
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            v[q] = T(0);
+            if (t0 + q < kp) ok &= get_granule<T>(rs, g0 + t0 + q, epoch, v[q]);
+          }
+          if (__all(ok)) break;
+          if (spin_give_up(spins, wt.tmo)) {
+            if (lane == 0) s_abort = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) st[q] += v[q];
+        sg += vs;
+      }
+      cs = Tr::psi(as + sg);
+      dg = T(0);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        if (t0 + q < k) {
+          const T gn = fma(eth[q], st[q], alp[q]);
+          dg += fabs(gn - gam[q]);
+          gam[q] = gn;
+          eth[q] = Tr::eth(gn, cs);
+        }
+      }
+      ++it;
+    }
+    if (s_abort) return;  // a team timed out: every block leaves (the host raises)
+
+    // ---- outputs: this member's rows; the topic-level ones from member 0
+    if (tid < nloc) {
+      const int n = lo + tid;
+      a.r[e0 + n] = rfin;
+      if (STATS) {
+        a.keys[e0 + n] = (uint32_t)sm.ids[tid];
+        a.vals[e0 + n] = entry_val<T>(slot, e0 + n, rfin);
+      }
+    }
+    if (member == 0) {
+      double gsd = 0.0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) gsd += (double)gam[q];
+      gsd = wave_sum(gsd);
+      if (lane == 0) sm.bd[wave][0] = gsd;
+      __syncthreads();
+      double gsum = 0.0;
+      for (int w = 0; w < kWWaves; ++w) gsum += sm.bd[w][0];
+      const double psisum = digamma_t<double>(gsum);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int t = t0 + q;
+        if (t < k) {
+          if (a.gamma) a.gamma[mem * k + t] = gam[q];
+          if (STATS) a.elogth[slot * k + t] = (T)(digamma_t<double>((double)gam[q]) - psisum);
+        }
+        if (STATS && t < kp) a.eth[slot * kp + t] = t < k ? eth[q] : T(0);
+      }
+      if (tid == 0) {
+        if (a.iters) a.iters[mem] = it;
+        if (a.nonempty) a.nonempty[mem] = 1;
+      }
+    }
+    __syncthreads();  // LDS (ids, xs, rr, bd, sB) is rewritten by the next document
+  }
+}
+
 // register rows per (T, Q): NR·Q·sizeof(T)/4 ≈ 128 VGPRs, so 512 threads keep two waves per SIMD
 // (fp32 Q = 1 — config 4's k = 500 — takes 176 rows: 227 VGPRs, no spills, the most the register
 // file holds at two waves per SIMD; its streamed tail is what bounds that config)
@@ -522,6 +894,51 @@ void launch_q(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound) {
 }  // namespace
 
 int wide_row_cap(int k) { return k <= kWThreads * 4 ? kWRows : 0; }
+
+// rows one CU keeps resident (VGPRs + LDS) for this (T, k): the team size for a document of nnz rows
+template <typename T>
+int wide_resident_rows(int k) {
+  auto rows = [](auto q) {
+    constexpr int Q = decltype(q)::value;
+    const size_t row_bytes = sizeof(T) * kWThreads * Q;
+    return wide_nr<T, Q>() + (int)((kWLds - wide_lds_fixed<T>()) / row_bytes);
+  };
+  if (k <= kWThreads) return rows(std::integral_constant<int, 1>{});
+  if (k <= 2 * kWThreads) return rows(std::integral_constant<int, 2>{});
+  return rows(std::integral_constant<int, 4>{});
+}
+
+template <typename T, int Q>
+void launch_q_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
+  constexpr int NR = wide_nr<T, Q>();
+  const size_t fixed = wide_lds_fixed<T>();
+  const size_t row_bytes = sizeof(T) * kWThreads * Q;
+  int nl = (int)((kWLds - fixed - 256) / row_bytes);  // 256 B for the kernel's own static word
+  const size_t lds = fixed + (size_t)nl * row_bytes;
+  auto go = [&](auto kern) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    EStepArgs<T> aa = a;
+    WideTeam ww = wt;
+    void* args[] = {&aa, &nl, &ww};
+    HIP_CHECK(hipLaunchCooperativeKernel((const void*)kern, dim3((unsigned)wt.blocks), dim3(kWThreads), args, lds, s));
+  };
+  if (stats) go(k_estep_wide_mc<T, Q, NR, true>);
+  else go(k_estep_wide_mc<T, Q, NR, false>);
+}
+
+template <typename T>
+void launch_estep_wide_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
+  if (a.n == 0) return;
+  if (a.k <= kWThreads) launch_q_mc<T, 1>(s, a, stats, wt);
+  else if (a.k <= 2 * kWThreads) launch_q_mc<T, 2>(s, a, stats, wt);
+  else if (a.k <= 4 * kWThreads) launch_q_mc<T, 4>(s, a, stats, wt);
+  else throw Error(STC_ERR_INVALID_ARG, "wide E-step: k > 2048");
+}
+
+template int wide_resident_rows<float>(int);
+template int wide_resident_rows<double>(int);
+template void launch_estep_wide_mc<float>(hipStream_t, const EStepArgs<float>&, bool, const WideTeam&);
+template void launch_estep_wide_mc<double>(hipStream_t, const EStepArgs<double>&, bool, const WideTeam&);
 
 template <typename T>
 void launch_estep_wide(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound) {

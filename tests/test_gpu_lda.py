@@ -31,14 +31,20 @@ def _handle(ctx, corpus, k, dtype, lam=None, **kw):
                                              ("f32", 77, "wave"), ("f64", 100, "wave"), ("f64", 100, "wg"),
                                              ("f64", 40, "wave"), ("f64", 20, "wave"), ("f64", 104, "wave"),
                                              ("f32", 300, "wave"), ("f64", 300, "wave"), ("f32", 700, "wave"),
-                                             ("f64", 700, "wave"), ("f32", 1500, "wave"), ("f64", 1500, "wave")])
+                                             ("f64", 700, "wave"), ("f32", 1500, "wave"), ("f64", 1500, "wave"),
+                                             ("f64", 300, "team1"), ("f64", 300, "team2"), ("f64", 700, "team3"),
+                                             ("f32", 700, "team2"), ("f64", 1500, "team4")])
 def test_estep_gamma_and_stat(ctx, oracle, dtype, k, kernel, monkeypatch):
     """Every E-step kernel vs the oracle: the register-resident grid kernels (fp32 k <= 128, fp64
     k <= 104 with R = 1..6 row sets, the sixth from LDS), the many-topic kernel (k > 128 / 104: Q = 1, 2,
     4 topics per lane; rows in VGPRs, then LDS, then streamed from global memory — docs up to 600 terms
-    reach all three) and the workgroup-per-doc kernel (docs past the fast kernels' row capacity)."""
+    reach all three), the same with each document's rows split over a team of P = 1..4 CUs
+    (k_estep_wide_mc, "teamP") and the workgroup-per-doc kernel (docs past the fast kernels' row
+    capacity)."""
     if kernel == "wg":
         monkeypatch.setenv("STC_DISABLE_WAVE", "1")
+    if kernel.startswith("team"):  # many-topic kernel with a forced team of P CUs per document
+        monkeypatch.setenv("STC_WIDE_TEAM", kernel[4:])
     rng = np.random.default_rng(10 + k)
     D, V = 48, 2048
     corpus = random_corpus(rng, D, V, 1, 600 if k > 128 else 300, empty_every=13)
@@ -409,3 +415,36 @@ def test_init_random_and_next_match_oracle(ctx, oracle, with_replacement):
         oracle.submit_minibatch(state, [corpus.row(d) for d in members], g0)
     np.testing.assert_allclose(h.topics(), state.lam.T, rtol=1e-9)
     np.testing.assert_allclose(h.alpha(), state.alpha, rtol=1e-9)
+
+
+@pytest.mark.parametrize("dtype,k", [("f64", 300), ("f32", 1500)])
+def test_team_estep_many_documents(ctx, dtype, k, monkeypatch):
+    """The team kernel over many documents of uneven length (teams finish documents at different
+    times, so the epoch flags and the parity-buffered partials are exercised across hundreds of
+    exchanges per team) vs the one-CU many-topic kernel on the same inputs: γ agrees to summation-order
+    rounding and the iteration counts match (a doc on the stop rule's boundary may differ by one)."""
+    rng = np.random.default_rng(23 + k)
+    D, V = 1200, 4096
+    corpus = random_corpus(rng, D, V, 100, 500, empty_every=97)
+    lam = rng.gamma(100.0, 0.01, size=(V, k))
+    g0 = rng.gamma(100.0, 0.01, size=(D, k))
+    out = {}
+    for P in ("1", "2", "3", "4"):
+        monkeypatch.setenv("STC_WIDE_TEAM", P)
+        h, _ = _handle(ctx, corpus, k, dtype, lam)
+        out[P] = h.estep(np.arange(D), g0, want_stat=True)
+    g1, s1, i1 = out["1"]
+    for P in ("2", "3", "4"):
+        g, st, it = out[P]
+        same = it == i1
+        if dtype == "f64":
+            assert (~same).sum() <= 3, (P, np.flatnonzero(~same))
+        else:  # fp32 rounding moves the stop crossing of a few percent of the documents
+            assert np.abs(it.astype(int) - i1).max() <= 3 and (~same).mean() < 0.05, (P, np.flatnonzero(~same))
+        if dtype == "f64":
+            big = g1[same] >= 1.0
+            np.testing.assert_allclose(g[same][big], g1[same][big], rtol=1e-9)
+        else:  # fp32: the oracle test's per-document bound (summation order moves small topics)
+            l1 = np.abs(g[same] - g1[same]).sum(axis=1)
+            assert np.all(l1 <= 1e-3 * k + 1e-4 * g1[same].sum(axis=1)), (P, l1.max())
+        np.testing.assert_allclose(st.sum(), s1.sum(), rtol=1e-6)
