@@ -332,9 +332,11 @@ def kernel_name(dtype, k):
     """The training E-step kernel libstc dispatches (api.hip use_wide: grid kernels up to their topic
     capacity, fp32 k <= 128 / fp64 k <= 104, the many-topic kernel past it)."""
     if k > (128 if dtype == "f32" else 104):
-        return "k_estep_wide (lda_wide.hip): the many-topic training E-step, one launch per minibatch"
+        return ("k_estep_wide / k_estep_wide_mc (lda_wide.hip): the many-topic training E-step (k <= 512: a "
+                "team of CUs per document), one launch per minibatch")
     if dtype == "f64":
-        return "k_estep_grid64 (lda_grid64.hip): the fp64 training E-step, one launch per minibatch"
+        return ("k_estep_grid64 (lda_grid64.hip): the fp64 training E-step, one launch per minibatch (plus "
+                "the streamed-row launch when a document has > 192 rows)")
     return "k_estep_grid (lda_grid.hip): the fp32 training E-step, one launch per minibatch"
 
 
