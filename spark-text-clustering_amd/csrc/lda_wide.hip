@@ -156,6 +156,33 @@ __device__ __forceinline__ void rows_q(const T* __restrict__ Bp, const int* ids,
   }
 }
 
+// the document block's resident rows: rows < NR into registers, rows < nres into LDS (sB), every
+// row of a batch loaded before any is stored (rows past `nrows` read term 0 and are zeroed), so the
+// loads of a batch are in flight together rather than one memory round trip per row
+template <typename T, int Q, int NR>
+__device__ __forceinline__ void load_block(const T* __restrict__ Bp, const int* ids, int nrows, int nres, T* sB,
+                                           int kp, int t0, T (*B)[Q]) {
+#pragma unroll
+  for (int n = 0; n < NR; ++n) {
+    T x[Q];
+    load_q<T, Q>(Bp, n < nrows ? (int64_t)ids[n] : 0, kp, t0, x);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) B[n][q] = n < nrows ? x[q] : T(0);
+  }
+  const int lend = nres < nrows ? nres : nrows;
+  for (int n0 = NR; n0 < lend; n0 += 8) {
+    T x[8][Q];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) load_q<T, Q>(Bp, n0 + i < lend ? (int64_t)ids[n0 + i] : 0, kp, t0, x[i]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (n0 + i < lend) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) sB[(int64_t)(n0 + i - NR) * (kWThreads * Q) + t0 + q] = x[i][q];  // read back by this lane
+      }
+  }
+}
+
 template <typename T>
 struct WLds {
   T xs[kWWaves][kWRows];  // per-wave row sums of φ (Phase A)
@@ -189,6 +216,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
   T* const sB = reinterpret_cast<T*>(smem + wide_lds_fixed<T>());  // [nl][512·Q]
   using Tr = WTr<T>;
   constexpr int CH = wide_chunk<T, Q>();
+  static_assert(NR % 8 == 0 && NR % CH == 0, "Phase A takes register rows CH, Phase B 8 at a time");
   constexpr int LB = (int)(WIDE_LB_BYTES / (sizeof(T) * Q)) < CH ? (int)(WIDE_LB_BYTES / (sizeof(T) * Q)) : CH;
   if ((int64_t)blockIdx.x >= a.n) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -290,21 +318,9 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
 
   // ---- the document block: rows < NR in VGPRs, rows < NR + nl in LDS (coalesced Q-wide loads)
   T B[NR > 0 ? NR : 1][Q];
-#pragma unroll
-  for (int n = 0; n < NR; ++n) {
-    if (n < nnz) load_q<T, Q>(a.Bp, (int64_t)sm.ids[n], kp, t0, B[n]);
-    else {
-#pragma unroll
-      for (int q = 0; q < Q; ++q) B[n][q] = T(0);
-    }
-  }
-  for (int n = NR; n < nres && n < nnz; ++n) {
-    T x[Q];
-    load_q<T, Q>(a.Bp, (int64_t)sm.ids[n], kp, t0, x);
-#pragma unroll
-    for (int q = 0; q < Q; ++q) sB[(int64_t)(n - NR) * (kWThreads * Q) + t0 + q] = x[q];  // read back by this lane
-  }
+  load_block<T, Q, NR>(a.Bp, sm.ids, nnz, nres, sB, kp, t0, B);
 
+  for (int n = nnz + tid; n < kWRows; n += kWThreads) sm.rr[n] = T(0);  // Phase B reads rows in 8s
   T cs = Tr::psi(gs);  // ψ(Σγ) of the current γ
 #pragma unroll
   for (int q = 0; q < Q; ++q) eth[q] = (t0 + q < k) ? Tr::eth(gam[q], cs) : T(0);
@@ -387,13 +403,13 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
     T s[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) s[q] = T(0);
+    // register rows without per-row branches (rows past nnz: B = 0, r = 0), so the r loads of
+    // consecutive rows are in flight together instead of one LDS round trip per row
 #pragma unroll
     for (int n = 0; n < NR; ++n) {
-      if (n < nnz) {
-        const T r = sm.rr[n];
+      const T r = sm.rr[n];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) s[q] = fma(B[n][q], r, s[q]);
-      }
+      for (int q = 0; q < Q; ++q) s[q] = fma(B[n][q], r, s[q]);
     }
     for (int n0 = NR; n0 < nnz; n0 += LB) {
       T y[LB][Q];
@@ -564,6 +580,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
   __shared__ int s_abort;
   using Tr = WTr<T>;
   constexpr int CH = wide_chunk<T, Q>();
+  static_assert(NR % 8 == 0 && NR % CH == 0, "Phase A takes register rows CH, Phase B 8 at a time");
   constexpr int LB = (int)(WIDE_LB_BYTES / (sizeof(T) * Q)) < CH ? (int)(WIDE_LB_BYTES / (sizeof(T) * Q)) : CH;
   const int P = wt.P;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -576,6 +593,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
   const int k = a.k, kp = a.kp, t0 = Q * tid;
   unsigned epoch = 0;
   if (tid == 0) s_abort = 0;
+  STAMP_DECL
 
   for (int64_t j = team; j < a.n; j += nteams) {
     const int64_t slot = a.slot0 + j;
@@ -666,21 +684,9 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
 
     // ---- this member's block: local rows < NR in VGPRs, < NR + nl in LDS, the rest streamed
     T B[NR > 0 ? NR : 1][Q];
-#pragma unroll
-    for (int n = 0; n < NR; ++n) {
-      if (n < nloc) load_q<T, Q>(a.Bp, (int64_t)sm.ids[n], kp, t0, B[n]);
-      else {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) B[n][q] = T(0);
-      }
-    }
-    for (int n = NR; n < nres && n < nloc; ++n) {
-      T x[Q];
-      load_q<T, Q>(a.Bp, (int64_t)sm.ids[n], kp, t0, x);
-#pragma unroll
-      for (int q = 0; q < Q; ++q) sB[(int64_t)(n - NR) * (kWThreads * Q) + t0 + q] = x[q];
-    }
+    load_block<T, Q, NR>(a.Bp, sm.ids, nloc, nres, sB, kp, t0, B);
 
+    if (tid >= nloc) sm.rr[tid] = T(0);  // Phase B reads rows in 8s (published by barrier (1))
     T cs = Tr::psi(gs);
 #pragma unroll
     for (int q = 0; q < Q; ++q) eth[q] = (t0 + q < k) ? Tr::eth(gam[q], cs) : T(0);
@@ -688,6 +694,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
     int it = 0;
     const T kd = (T)k;
     T rfin = T(0);
+    STAMP(0);  // per-document preamble: counts, γ₀, the block's loads
     while (true) {
       // Phase A over the local rows (as k_estep_wide)
 #pragma unroll
@@ -726,6 +733,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
       }
       const T dsum_w = Tr::wsum(dg);
       if (lane == 0) sm.red[0][wave] = dsum_w;
+      STAMP(1);  // Phase A
       __syncthreads();  // (1) row sums and Σ|Δγ| published (and any wave's give-up in s_abort)
       if (s_abort) break;
       T dsum = sm.red[0][0];
@@ -745,6 +753,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
       rd = Tr::wsum(rd);
       if (lane == 0) sm.red[1][wave] = rd;
       __syncthreads();  // (2) r and Σ r·dot published
+      STAMP(2);  // barriers, r, Σ r·φ
       if (last) break;
       T sgl = sm.red[1][0];
 #pragma unroll
@@ -755,12 +764,10 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
 #pragma unroll
       for (int q = 0; q < Q; ++q) s[q] = T(0);
 #pragma unroll
-      for (int n = 0; n < NR; ++n) {
-        if (n < nloc) {
-          const T r = sm.rr[n];
+      for (int n = 0; n < NR; ++n) {  // no per-row branches (rows past nloc: B = 0, r = 0)
+        const T r = sm.rr[n];
 #pragma unroll
-          for (int q = 0; q < Q; ++q) s[q] = fma(B[n][q], r, s[q]);
-        }
+        for (int q = 0; q < Q; ++q) s[q] = fma(B[n][q], r, s[q]);
       }
       for (int n0 = NR; n0 < nloc; n0 += LB) {
         T y[LB][Q];
@@ -772,6 +779,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
           for (int q = 0; q < Q; ++q) s[q] = fma(y[i][q], r, s[q]);
         }
       }
+      STAMP(3);  // Phase B
       // ---- exchange: publish (s partial, Σ r·dot partial) as epoch granules, then every wave
       // collects the other members' granules for its lanes' topics; sums in member order
       ++epoch;
@@ -793,6 +801,19 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
         }
         const int g0 = base + m * (int)wt.xstride;
         T v[Q], vs = T(0);
+#ifdef STC_TEAM_NOWAIT  // timing-only diagnostic build: read whatever is there (wrong results)
+        if (true) {
+          get_granule<T>(rs, g0 + kp, epoch, vs);
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            v[q] = T(0);
+            if (t0 + q < kp) get_granule<T>(rs, g0 + t0 + q, epoch, v[q]);
+          }
+          vs = T(0);
+#pragma unroll
+          for (int q = 0; q < Q; ++q) v[q] = T(0);
+        } else
+#endif
         for (unsigned spins = 0;; ++spins) {
           bool ok = get_granule<T>(rs, g0 + kp, epoch, vs);
 #pragma unroll
@@ -811,6 +832,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
         for (int q = 0; q < Q; ++q) st[q] += v[q];
         sg += vs;
       }
+      STAMP(4);  // exchange (publish + wait + member-order sums)
       cs = Tr::psi(as + sg);
       dg = T(0);
 #pragma unroll
@@ -823,6 +845,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
         }
       }
       ++it;
+      STAMP(5);  // γ, ψ/exp
     }
     if (s_abort) return;  // a team timed out: every block leaves (the host raises)
 
@@ -860,7 +883,9 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
       }
     }
     __syncthreads();  // LDS (ids, xs, rr, bd, sB) is rewritten by the next document
+    STAMP(6);  // outputs
   }
+  STAMP_FLUSH
 }
 
 // register rows per (T, Q): NR·Q·sizeof(T)/4 ≈ 128 VGPRs, so 512 threads keep two waves per SIMD
@@ -872,6 +897,17 @@ constexpr int wide_nr() {
          : (sizeof(T) == 8 && Q == 1) ? WIDE_NR64_Q1
          : sizeof(T) == 8 && Q >= 2 ? (Q == 2 ? WIDE_NR64_Q2 : WIDE_NR64_Q4)  // fp64: 8-row chunks
                                     : (int)(128 * 4 / (sizeof(T) * Q)) / kWChunk * kWChunk;
+}
+
+// the team kernel's register rows: WIDE_MC_NR_CUT Phase-A chunks fewer than the one-CU kernel (its
+// persistent loop holds more live state; measured: the spills of the uncut form sit outside the inner
+// loop, so the default cuts nothing)
+#ifndef WIDE_MC_NR_CUT
+#define WIDE_MC_NR_CUT 0
+#endif
+template <typename T, int Q>
+constexpr int wide_nr_mc() {
+  return wide_nr<T, Q>() - WIDE_MC_NR_CUT * wide_chunk<T, Q>();
 }
 
 template <typename T, int Q>
@@ -901,7 +937,7 @@ int wide_resident_rows(int k) {
   auto rows = [](auto q) {
     constexpr int Q = decltype(q)::value;
     const size_t row_bytes = sizeof(T) * kWThreads * Q;
-    return wide_nr<T, Q>() + (int)((kWLds - wide_lds_fixed<T>()) / row_bytes);
+    return wide_nr_mc<T, Q>() + (int)((kWLds - wide_lds_fixed<T>() - 256) / row_bytes);
   };
   if (k <= kWThreads) return rows(std::integral_constant<int, 1>{});
   if (k <= 2 * kWThreads) return rows(std::integral_constant<int, 2>{});
@@ -910,7 +946,7 @@ int wide_resident_rows(int k) {
 
 template <typename T, int Q>
 void launch_q_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
-  constexpr int NR = wide_nr<T, Q>();
+  constexpr int NR = wide_nr_mc<T, Q>();
   const size_t fixed = wide_lds_fixed<T>();
   const size_t row_bytes = sizeof(T) * kWThreads * Q;
   int nl = (int)((kWLds - fixed - 256) / row_bytes);  // 256 B for the kernel's own static word
@@ -952,5 +988,11 @@ void launch_estep_wide(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bo
 template void launch_estep_wide<float>(hipStream_t, const EStepArgs<float>&, bool, bool);
 template void launch_estep_wide<double>(hipStream_t, const EStepArgs<double>&, bool, bool);
 
+}  // namespace lda
+}  // namespace stc
+
+namespace stc {
+namespace lda {
+STC_STAMP_READER(stc_debug_stamps_wide)
 }  // namespace lda
 }  // namespace stc

@@ -1,0 +1,81 @@
+"""Where the team E-step (lda_wide.hip k_estep_wide_mc) spends its cycles: per-phase s_memtime stamps.
+
+    make -C spark-text-clustering_amd/csrc stamp
+    STC_LIB=spark-text-clustering_amd/stc/libstc_stamp.so python tools/stamp_team.py [--dtype f64 ...]
+
+A config-4-shaped workload (k = 500, V = 2^20, 500 tokens per doc) on a smaller corpus; prints each
+phase's share of the summed wave cycles and cycles per wave per inner iteration (8 waves per block,
+P blocks per document).  The stamps fence the schedule: read SHARES, not absolute time.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "spark-text-clustering_amd"))
+
+PHASES = ["per-doc preamble + block loads", "A: phi rows + reduce", "barriers, r, sum r*phi", "B: s partial",
+          "exchange: publish + wait + sums", "gamma, psi/exp", "outputs"]
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--docs", type=int, default=100_000)
+    p.add_argument("--tokens", type=int, default=500)
+    p.add_argument("--vocab", type=int, default=1 << 20)
+    p.add_argument("--k", type=int, default=500)
+    p.add_argument("--fraction", type=float, default=0.05)
+    p.add_argument("--dtype", default="f64")
+    p.add_argument("--burn", type=int, default=5)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--seed", type=int, default=20261015)
+    a = p.parse_args()
+    assert "stamp" in os.environ.get("STC_LIB", ""), "set STC_LIB to the stamp build"
+    import stc
+    from stc import synth
+
+    corpus = synth.make_corpus("zipf", a.docs, a.tokens, a.vocab, a.k, a.seed, workers=8)
+    print("corpus generated", file=sys.stderr, flush=True)
+    ctx = stc.Context(0)
+    lib = stc._lib.load()
+    reader = lib.stc_debug_stamps_wide
+    reader.restype = C.c_int
+    reader.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
+    buf = (C.c_ulonglong * 12)()
+    dc = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F32 if a.dtype == "f32" else stc.STC_F64)
+    h = stc.LdaHandle(ctx, a.k, a.vocab, mini_batch_fraction=a.fraction, optimize_doc_concentration=True,
+                      seed=a.seed, dtype=a.dtype)
+    h.set_corpus(dc, a.docs)
+    h.init_random(a.seed)
+    for i in range(a.burn):
+        h.next(stats=False)
+        ctx.synchronize()
+        print(f"burn-in minibatch {i + 1}", file=sys.stderr, flush=True)
+    assert reader(buf, 12, 1) == 0
+    c0 = h.counters()
+    for _ in range(a.steps):
+        h.next(stats=False)
+    ctx.synchronize()
+    assert reader(buf, 12, 1) == 0
+    c1 = h.counters()
+    cyc = np.array(buf[:], dtype=np.float64)
+    docs = c1["docs"] - c0["docs"]
+    iters = c1["inner_iters"] - c0["inner_iters"]
+    tot = cyc[:len(PHASES)].sum()
+    P = int(os.environ.get("STC_WIDE_TEAM", "0")) or None
+    out = {"k": a.k, "dtype": a.dtype, "team": P or "auto", "docs": int(docs),
+           "mean_inner_iters": iters / max(1, docs), "share": {}, "cycles_per_block_wave_iter": {}}
+    waves = 8 * (P or 1)
+    for i, name in enumerate(PHASES):
+        out["share"][name] = round(cyc[i] / tot, 4)
+        out["cycles_per_block_wave_iter"][name] = round(cyc[i] / (waves * max(1, iters)), 1)
+    out["note"] = "per-iteration cycles assume `team` blocks per document (set STC_WIDE_TEAM)"
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
