@@ -346,15 +346,29 @@ void ensure_order(stc_lda& L) {
 }
 
 // team size for the many-topic kernel: enough CUs that a document of `mean_rows` rows is resident
-// (measured, configs 4/5: a team pays for k ≤ 512 — config 4's k = 500, 1.6× in both dtypes — but not
-// at k = 2000, where the 16 KB of partials per member and iteration cost more than the re-streamed rows)
+// team for the many-topic kernel: enough CUs that a document of `mean_rows` rows stays resident.
+// k ≤ 512: rows split (k_estep_wide_mc), P = ⌈1.05·rows / resident rows⌉ ≤ 4 (config 4, k = 500:
+// fp64 P = 4, fp32 P = 2).  k > 512: topics split (k_estep_wide_tc), members of up to 1024 topics, when
+// the one-CU kernel cannot keep the rows resident (config 5, k = 2000: fp64 P = 2; fp32 stays one CU).
+// P = 1: the one-CU kernel.  STC_WIDE_TEAM=n forces P = n.
+struct TeamChoice {
+  int P = 1;
+  bool topics = false;
+};
 template <typename T>
-int team_size(const stc_lda& L, double mean_rows) {
-  if (L.team_force > 0) return std::min(L.team_force, 4);
-  if (L.k > 512) return 1;
-  const int res = lda::wide_resident_rows<T>(L.k);
-  const int P = (int)std::ceil(mean_rows * 1.05 / std::max(res, 1));
-  return std::max(1, std::min(P, 4));
+TeamChoice team_choice(const stc_lda& L, double mean_rows) {
+  const double need = 1.05 * mean_rows;
+  if (L.team_force == 1) return {1, false};
+  if (L.k <= 512) {
+    int P = L.team_force > 1 ? L.team_force : (int)std::ceil(need / std::max(lda::wide_resident_rows<T>(L.k), 1));
+    return {std::max(1, std::min(P, 4)), false};
+  }
+  if (L.team_force > 1) return {std::max(L.team_force, (L.k + 2047) / 2048), true};
+  if (lda::wide_resident_rows<T>(L.k) >= need) return {1, false};
+  // two members of up to 1024 topics: measured at config 5 (k = 2000, fp64, E-step per minibatch) P = 2
+  // 44.0 ms, one CU 53.7, P = 3 (a member without topics) 71.2, P = 4 61.9 — a member's exchange
+  // latency is fixed, so the fewest members that hold the block win
+  return {std::max(2, std::min(4, (L.k + 1023) / 1024)), true};
 }
 
 // the team kernel's timeout word (copied to pinned memory after each launch; read once the stream has
@@ -367,7 +381,8 @@ void check_team_timeout(stc_lda& L) {
 }
 
 template <typename T>
-void launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, int P) {
+void launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamChoice tc) {
+  const int P = tc.P;
   Ctx& c = *L.ctx;
   hipStream_t s = c.stream;
   int cus = 0;
@@ -377,7 +392,8 @@ void launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, int P)
   wt.blocks = 8 * P * (cus / (8 * P));
   STC_REQUIRE(wt.blocks > 0, "team E-step: too few CUs");
   const int teams = wt.blocks / P;
-  wt.xstride = L.kp + 1;  // granules per member: the s partials + Σ r·φ
+  // granules per member: rows split, the s partials + Σ r·φ; topics split, the φ partials + Σ|Δγ| + Σγ
+  wt.xstride = std::max<int64_t>(L.kp + 1, 512 + 2);
   const size_t xbytes = 16 * (size_t)teams * 2 * P * (size_t)wt.xstride;
   L.team_words.reserve(16);
   L.team_x.reserve(xbytes);
@@ -391,7 +407,8 @@ void launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, int P)
   // (a tag left by an earlier launch could equal an epoch this launch waits for)
   HIP_CHECK(hipMemsetAsync(L.team_words.p, 0, 16, s));
   HIP_CHECK(hipMemsetAsync(L.team_x.p, 0, xbytes, s));
-  lda::launch_estep_wide_mc<T>(s, w, stats, wt);
+  if (tc.topics) lda::launch_estep_wide_tc<T>(s, w, stats, wt);
+  else lda::launch_estep_wide_mc<T>(s, w, stats, wt);
   HIP_CHECK(hipMemcpyAsync(L.htmo, wt.tmo, sizeof(unsigned), hipMemcpyDeviceToHost, s));
 }
 
@@ -405,8 +422,8 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
     lda::EStepArgs<T> w = a;
     w.slot0 = 0;
     w.n = n_short;
-    const int P = use_wide(L.k, L.dtype) && !bound ? team_size<T>(L, mean_rows) : 1;
-    if (P > 1) launch_wide_team<T>(L, w, stats, P);
+    const TeamChoice tc = use_wide(L.k, L.dtype) && !bound ? team_choice<T>(L, mean_rows) : TeamChoice{};
+    if (tc.P > 1) launch_wide_team<T>(L, w, stats, tc);
     else if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
     else if constexpr (std::is_same<T, float>::value) lda::launch_estep_wave(s, w, stats, bound);
     else lda::launch_estep_grid64(s, w, stats, bound, m.max_row < 0 || m.max_row > lda::grid64_onchip_rows(L.k));

@@ -92,12 +92,16 @@ struct WideTeam {
   int blocks = 0;            // persistent grid: a multiple of 8·P, ≤ the CU count
   unsigned* tmo = nullptr;   // timeout word (zeroed before each launch)
   void* xbuf = nullptr;      // [teams][2][P][xstride] 16-byte {epoch, value} granules (zeroed before each launch)
-  int64_t xstride = 0;       // granules per member: kp + 1 (s partials, Σ r·φ)
+  int64_t xstride = 0;       // granules per member: rows split kp + 1 (s partials, Σ r·φ); topics split
+                             // 512 + 2 (φ partials, Σ|Δγ|, Σγ)
 };
 template <typename T>
 int wide_resident_rows(int k);
 template <typename T>
 void launch_estep_wide_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt);
+// the same with the TOPICS split over the team (k > 512; lda_wide.hip k_estep_wide_tc)
+template <typename T>
+void launch_estep_wide_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt);
 template <typename T>
 void launch_estep_wide(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound);
 

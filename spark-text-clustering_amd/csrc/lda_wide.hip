@@ -136,15 +136,17 @@ __device__ __forceinline__ void load_q(const T* __restrict__ Bp, int64_t row, in
 }
 
 // the lane's Q entries of rows n0 .. n0+15 past the register rows: from LDS (n < nres), streamed from
-// global memory (n < nnz; every load issued before any is used), zero past nnz
+// global memory (n < nnz; every load issued before any is used), zero past nnz.  t0: the lane's first
+// topic (global column); its LDS column is Q·lane-in-block (the topic-split team's t0 is offset)
 template <typename T, int Q, int LB>
 __device__ __forceinline__ void rows_q(const T* __restrict__ Bp, const int* ids, const T* sB, int kp, int t0, int nr,
                                        int nres, int nnz, int n0, T (*y)[Q]) {
+  const int lc = Q * (int)threadIdx.x;
 #pragma unroll
   for (int i = 0; i < LB; ++i) {
     const int n = n0 + i;
     if (n < nres && n < nnz) {
-      const T* p = sB + (int64_t)(n - nr) * (kWThreads * Q) + t0;
+      const T* p = sB + (int64_t)(n - nr) * (kWThreads * Q) + lc;
 #pragma unroll
       for (int q = 0; q < Q; ++q) y[i][q] = p[q];
     } else if (n < nnz) {
@@ -170,6 +172,7 @@ __device__ __forceinline__ void load_block(const T* __restrict__ Bp, const int* 
     for (int q = 0; q < Q; ++q) B[n][q] = n < nrows ? x[q] : T(0);
   }
   const int lend = nres < nrows ? nres : nrows;
+  const int lc = Q * (int)threadIdx.x;  // LDS column (t0 is the global one)
   for (int n0 = NR; n0 < lend; n0 += 8) {
     T x[8][Q];
 #pragma unroll
@@ -178,7 +181,7 @@ __device__ __forceinline__ void load_block(const T* __restrict__ Bp, const int* 
     for (int i = 0; i < 8; ++i)
       if (n0 + i < lend) {
 #pragma unroll
-        for (int q = 0; q < Q; ++q) sB[(int64_t)(n0 + i - NR) * (kWThreads * Q) + t0 + q] = x[i][q];  // read back by this lane
+        for (int q = 0; q < Q; ++q) sB[(int64_t)(n0 + i - NR) * (kWThreads * Q) + lc + q] = x[i][q];  // read back by this lane
       }
   }
 }
@@ -888,6 +891,331 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
   STAMP_FLUSH
 }
 
+// ---------------------------------------------------------------------------------------------
+// k_estep_wide_tc — a team of P workgroups per document with the TOPICS split (k > 512: config 5's
+// k = 2000 in fp64, whose 44 × 2000 × 8 B block is 4.5× what one CU keeps resident at 4 topics per
+// lane).  Member m owns topics [m·512Q, (m+1)·512Q) and every row of the document, so s = Bᵀr and the
+// γ / eθ update are local and the team exchanges only each member's φ partials (nnz values) plus its
+// Σ|Δγ| (the stop rule) once per iteration — 44 values at config 5 instead of the row split's 2000.
+// Every member adds the P partials in member order, so φ, r, Σ r·φ and the stop rule are identical in
+// every member.  ψ(Σγ₀) and Σα come from all k topics in every member (γ₀ is counter-RNG keyed); the
+// final Σγ (E[log θ] for logphat) is one more exchange.  Grid, granules, bounds: as k_estep_wide_mc.
+template <typename T, int Q, int NR, bool STATS>
+__global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int nl, WideTeam wt) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  WLds<T>& sm = *reinterpret_cast<WLds<T>*>(smem);
+  T* const sB = reinterpret_cast<T*>(smem + wide_lds_fixed<T>());  // [nl][512·Q]
+  __shared__ int s_abort;
+  using Tr = WTr<T>;
+  constexpr int CH = wide_chunk<T, Q>();
+  static_assert(NR % 8 == 0 && NR % CH == 0, "Phase A takes register rows CH, Phase B 8 at a time");
+  constexpr int LB = (int)(WIDE_LB_BYTES / (sizeof(T) * Q)) < CH ? (int)(WIDE_LB_BYTES / (sizeof(T) * Q)) : CH;
+  constexpr int GD = kWRows, GS = kWRows + 1;  // granule slots: row partials [0, nnz), Σ|Δγ|, Σγ
+  const int P = wt.P;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = (int)blockIdx.x, il = b / 8;
+  const int member = il % P, team = (il / P) * 8 + (b % 8), nteams = (int)gridDim.x / P;
+  const int team_granules = 2 * P * (int)wt.xstride;
+  unsigned char* const xb = reinterpret_cast<unsigned char*>(wt.xbuf) + (int64_t)team * team_granules * 16;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(xb, 0, team_granules * 16, 0x00020000);
+  const int k = a.k, kp = a.kp, kP = kWThreads * Q;
+  const int t0 = member * kP + Q * tid;  // this lane's first topic
+  unsigned epoch = 0;
+  if (tid == 0) s_abort = 0;
+
+  // one exchange: publish `mine` at slot `idx` (if `pub`), then the member-order sum of slot `idx`
+  // over the team (every lane of a wave takes part in the poll; `need` = this lane reads the slot)
+  auto exchange = [&](int idx, T mine, bool pub, bool need) -> T {
+    const int base = (int)(epoch & 1) * P * (int)wt.xstride;
+    if (pub) put_granule<T>(rs, base + member * (int)wt.xstride + idx, epoch, mine);
+    T sum = T(0);
+    for (int m = 0; m < P; ++m) {
+      T v = T(0);
+      if (m == member) {
+        v = mine;
+      } else {
+        for (unsigned spins = 0;; ++spins) {
+          const bool ok = !need || get_granule<T>(rs, base + m * (int)wt.xstride + idx, epoch, v);
+          if (__all(ok)) break;
+          if (spin_give_up(spins, wt.tmo)) {
+            if (lane == 0) s_abort = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      sum += v;
+    }
+    return sum;
+  };
+
+  for (int64_t j = team; j < a.n; j += nteams) {
+    const int64_t slot = a.slot0 + j;
+    const int64_t row = a.batch ? (int64_t)a.batch[slot] : slot;
+    const int64_t mem = a.orig ? (int64_t)a.orig[slot] : slot;
+    const int64_t s0 = a.indptr[row];
+    const int nnz = (int)(a.indptr[row + 1] - s0);
+    const int64_t e0 = a.bptr ? a.bptr[slot] : s0;
+    const int nres = NR + nl;
+
+    T cts = T(0), eps = T(0);
+    int any = 0;
+    if (tid < nnz) {
+      const int64_t pos = s0 + (a.order ? a.order[s0 + tid] : tid);
+      const int id = a.indices[pos];
+      cts = a.values[pos];
+      sm.ids[tid] = id;
+      eps = fmin(fmax((T)fmin(exp(kLogEps - a.logscale[id]), 1e300), Tr::eps_floor()), Tr::eps_cap());
+      any = cts != T(0);
+    }
+    const bool nonempty = __syncthreads_or(any) != 0;
+
+    uint64_t stream = 0;
+    if (!a.gamma0) {
+      const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, mem) : (uint64_t)(a.doc_id_base + row);
+      stream = doc_stream(a.seed, key);
+    }
+    T gam[Q], alp[Q], eth[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int t = t0 + q;
+      gam[q] = t < k ? (a.gamma0 ? a.gamma0[mem * k + t] : (T)gamma_sample(stream, t, a.gamma_shape)) : T(0);
+      alp[q] = t < k ? (T)a.alpha[t] : T(0);
+    }
+    if (!nonempty) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int t = t0 + q;
+        if (t < k) {
+          if (a.gamma) a.gamma[mem * k + t] = T(0);
+          if (STATS) a.elogth[slot * k + t] = T(0);
+        }
+        if (STATS && t < kp && q + Q * tid < kP) a.eth[slot * kp + t] = T(0);
+      }
+      if (member == 0) {
+        if (tid < nnz) {
+          a.r[e0 + tid] = T(0);
+          if (STATS) {
+            a.keys[e0 + tid] = (uint32_t)sm.ids[tid];
+            a.vals[e0 + tid] = entry_val<T>(slot, e0 + tid, T(0));
+          }
+        }
+        if (tid == 0) {
+          if (a.iters) a.iters[mem] = 0;
+          if (a.nonempty) a.nonempty[mem] = 0;
+        }
+      }
+      __syncthreads();
+      continue;
+    }
+    // Σγ₀ and Σα over all k topics, in the same order in every member (lane l: topics l·Q + q of every
+    // member's range)
+    T gs = T(0), as = T(0);
+    for (int m = 0; m < P; ++m) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int t = m * kP + Q * tid + q;
+        if (t < k) {
+          gs += m == member ? gam[q] : (a.gamma0 ? a.gamma0[mem * k + t] : (T)gamma_sample(stream, t, a.gamma_shape));
+          as += (T)a.alpha[t];
+        }
+      }
+    }
+    gs = Tr::wsum(gs);
+    as = Tr::wsum(as);
+    if (lane == 0) {
+      sm.xs[wave][0] = gs;
+      sm.xs[wave][1] = as;
+    }
+    __syncthreads();
+    gs = sm.xs[0][0];
+    as = sm.xs[0][1];
+#pragma unroll
+    for (int w = 1; w < kWWaves; ++w) {
+      gs += sm.xs[w][0];
+      as += sm.xs[w][1];
+    }
+    __syncthreads();
+
+    // the block of this member's topics: rows < NR in VGPRs, < NR + nl in LDS, the rest streamed
+    T B[NR > 0 ? NR : 1][Q];
+    load_block<T, Q, NR>(a.Bp, sm.ids, nnz, nres, sB, kp, t0, B);
+    if (tid >= nnz) sm.rr[tid] = T(0);
+
+    T cs = Tr::psi(gs);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) eth[q] = (t0 + q < k) ? Tr::eth(gam[q], cs) : T(0);
+    T dg = T(0);
+    int it = 0;
+    const T kd = (T)k;
+    T rfin = T(0);
+    while (true) {
+      // Phase A: this member's φ partials, as k_estep_wide
+#pragma unroll
+      for (int c = 0; c < NR / CH; ++c) {
+        if (CH * c < nnz) {
+          T x[CH];
+#pragma unroll
+          for (int i = 0; i < CH; ++i) {
+            T acc = T(0);
+#pragma unroll
+            for (int q = 0; q < Q; ++q) acc = fma(B[CH * c + i][q], eth[q], acc);
+            x[i] = acc;
+          }
+          const T v = rs_chunk<T, CH>(x, lane);
+          const int n = CH * c + rs_row<CH>(lane);
+          if (rs_pub<CH>(lane) && n < nnz) sm.xs[wave][n] = v;
+        }
+      }
+      for (int n0 = NR; n0 < nnz; n0 += CH) {
+        T x[CH];
+#pragma unroll
+        for (int bb = 0; bb < CH; bb += LB) {
+          T y[LB][Q];
+          rows_q<T, Q, LB>(a.Bp, sm.ids, sB, kp, t0, NR, nres, nnz, n0 + bb, y);
+#pragma unroll
+          for (int i = 0; i < LB; ++i) {
+            T acc = T(0);
+#pragma unroll
+            for (int q = 0; q < Q; ++q) acc = fma(y[i][q], eth[q], acc);
+            x[bb + i] = acc;
+          }
+        }
+        const T v = rs_chunk<T, CH>(x, lane);
+        const int n = n0 + rs_row<CH>(lane);
+        if (rs_pub<CH>(lane) && n < nnz) sm.xs[wave][n] = v;
+      }
+      const T dsum_w = Tr::wsum(dg);
+      if (lane == 0) sm.red[0][wave] = dsum_w;
+      __syncthreads();  // (1) row sums and Σ|Δγ| published (and any wave's give-up in s_abort)
+      if (s_abort) break;
+      ++epoch;
+      T dotp = T(0);
+      if (tid < nnz) {
+        dotp = sm.xs[0][tid];
+#pragma unroll
+        for (int w = 1; w < kWWaves; ++w) dotp += sm.xs[w][tid];
+      }
+      T dsp = sm.red[0][0];
+#pragma unroll
+      for (int w = 1; w < kWWaves; ++w) dsp += sm.red[0][w];
+      // one exchange round for both: each lane's row partial and every member's Σ|Δγ| partial
+      T dot = T(0), dsum = T(0);
+      {
+        const int base = (int)(epoch & 1) * P * (int)wt.xstride;
+        const bool row = tid < nnz;
+        if (row) put_granule<T>(rs, base + member * (int)wt.xstride + tid, epoch, dotp);
+        if (tid == 0) put_granule<T>(rs, base + member * (int)wt.xstride + GD, epoch, dsp);
+        for (int m = 0; m < P; ++m) {
+          T v = T(0), w = T(0);
+          if (m == member) {
+            v = dotp;
+            w = dsp;
+          } else {
+            for (unsigned spins = 0;; ++spins) {
+              bool ok = get_granule<T>(rs, base + m * (int)wt.xstride + GD, epoch, w);
+              if (row) ok &= get_granule<T>(rs, base + m * (int)wt.xstride + tid, epoch, v);
+              if (__all(ok)) break;
+              if (spin_give_up(spins, wt.tmo)) {
+                if (lane == 0) s_abort = 1;
+                break;
+              }
+              __builtin_amdgcn_s_sleep(1);
+            }
+          }
+          dot += row ? v : T(0);
+          dsum += w;
+        }
+      }
+      const bool last = (it > 0 && dsum / kd <= T(1e-3)) || it >= a.max_iter;  // team-uniform
+      T rd = T(0);
+      if (tid < nnz) {
+        const T r = cts * Tr::rcp(dot + eps);
+        sm.rr[tid] = r;
+        rfin = r;
+        rd = fma(r, dot, rd);
+      }
+      rd = Tr::wsum(rd);
+      if (lane == 0) sm.red[1][wave] = rd;
+      __syncthreads();  // (2) r and Σ r·dot published
+      if (last || s_abort) break;
+      T sg = sm.red[1][0];
+#pragma unroll
+      for (int w = 1; w < kWWaves; ++w) sg += sm.red[1][w];
+      cs = Tr::psi(as + sg);
+
+      // Phase B: s over every row for this member's topics (local)
+      T s[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) s[q] = T(0);
+#pragma unroll
+      for (int n = 0; n < NR; ++n) {
+        const T r = sm.rr[n];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) s[q] = fma(B[n][q], r, s[q]);
+      }
+      for (int n0 = NR; n0 < nnz; n0 += LB) {
+        T y[LB][Q];
+        rows_q<T, Q, LB>(a.Bp, sm.ids, sB, kp, t0, NR, nres, nnz, n0, y);
+#pragma unroll
+        for (int i = 0; i < LB; ++i) {
+          const T r = n0 + i < nnz ? sm.rr[n0 + i] : T(0);
+#pragma unroll
+          for (int q = 0; q < Q; ++q) s[q] = fma(y[i][q], r, s[q]);
+        }
+      }
+      dg = T(0);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        if (t0 + q < k) {
+          const T gn = fma(eth[q], s[q], alp[q]);
+          dg += fabs(gn - gam[q]);
+          gam[q] = gn;
+          eth[q] = Tr::eth(gn, cs);
+        }
+      }
+      ++it;
+    }
+    if (s_abort) return;  // a team timed out: every block leaves (the host raises)
+
+    // ---- outputs: rows from member 0 (identical in every member); this member's topics
+    if (member == 0 && tid < nnz) {
+      a.r[e0 + tid] = rfin;
+      if (STATS) {
+        a.keys[e0 + tid] = (uint32_t)sm.ids[tid];
+        a.vals[e0 + tid] = entry_val<T>(slot, e0 + tid, rfin);
+      }
+    }
+    // exact Σγ of the final γ over the team (E[log θ] = ψ(γ) − ψ(Σγ))
+    double gsd = 0.0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) gsd += (double)gam[q];
+    gsd = wave_sum(gsd);
+    if (lane == 0) sm.bd[wave][0] = gsd;
+    __syncthreads();
+    double gpart = 0.0;
+    for (int w = 0; w < kWWaves; ++w) gpart += sm.bd[w][0];
+    ++epoch;
+    const double gsum = (double)exchange(GS, (T)gpart, tid == 0, true);
+    if (s_abort) return;
+    const double psisum = digamma_t<double>(gsum);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int t = t0 + q;
+      if (t < k) {
+        if (a.gamma) a.gamma[mem * k + t] = gam[q];
+        if (STATS) a.elogth[slot * k + t] = (T)(digamma_t<double>((double)gam[q]) - psisum);
+      }
+      if (STATS && t < kp && q + Q * tid < kP) a.eth[slot * kp + t] = t < k ? eth[q] : T(0);
+    }
+    if (member == 0 && tid == 0) {
+      if (a.iters) a.iters[mem] = it;
+      if (a.nonempty) a.nonempty[mem] = 1;
+    }
+    __syncthreads();  // LDS (ids, xs, rr, bd, sB) is rewritten by the next document
+  }
+}
+
 // register rows per (T, Q): NR·Q·sizeof(T)/4 ≈ 128 VGPRs, so 512 threads keep two waves per SIMD
 // (fp32 Q = 1 — config 4's k = 500 — takes 176 rows: 227 VGPRs, no spills, the most the register
 // file holds at two waves per SIMD; its streamed tail is what bounds that config)
@@ -961,6 +1289,37 @@ void launch_q_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTea
   if (stats) go(k_estep_wide_mc<T, Q, NR, true>);
   else go(k_estep_wide_mc<T, Q, NR, false>);
 }
+
+template <typename T, int Q>
+void launch_q_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
+  constexpr int NR = wide_nr_mc<T, Q>();
+  const size_t fixed = wide_lds_fixed<T>();
+  const size_t row_bytes = sizeof(T) * kWThreads * Q;
+  int nl = (int)((kWLds - fixed - 256) / row_bytes);
+  const size_t lds = fixed + (size_t)nl * row_bytes;
+  auto go = [&](auto kern) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    EStepArgs<T> aa = a;
+    WideTeam ww = wt;
+    void* args[] = {&aa, &nl, &ww};
+    HIP_CHECK(hipLaunchCooperativeKernel((const void*)kern, dim3((unsigned)wt.blocks), dim3(kWThreads), args, lds, s));
+  };
+  if (stats) go(k_estep_wide_tc<T, Q, NR, true>);
+  else go(k_estep_wide_tc<T, Q, NR, false>);
+}
+
+// topic split: member topics 512·Q with Q = ⌈k / (512·P)⌉ ≤ 4
+template <typename T>
+void launch_estep_wide_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
+  if (a.n == 0) return;
+  const int q = (a.k + kWThreads * wt.P - 1) / (kWThreads * wt.P);
+  if (q <= 1) launch_q_tc<T, 1>(s, a, stats, wt);
+  else if (q <= 2) launch_q_tc<T, 2>(s, a, stats, wt);
+  else if (q <= 4) launch_q_tc<T, 4>(s, a, stats, wt);
+  else throw Error(STC_ERR_INVALID_ARG, "topic-split team E-step: k > 2048·P");
+}
+template void launch_estep_wide_tc<float>(hipStream_t, const EStepArgs<float>&, bool, const WideTeam&);
+template void launch_estep_wide_tc<double>(hipStream_t, const EStepArgs<double>&, bool, const WideTeam&);
 
 template <typename T>
 void launch_estep_wide_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
