@@ -364,7 +364,10 @@ TeamChoice team_choice(const stc_lda& L, double mean_rows) {
     return {std::max(1, std::min(P, 4)), false};
   }
   if (L.team_force > 1) return {std::max(L.team_force, (L.k + 2047) / 2048), true};
-  if (lda::wide_resident_rows<T>(L.k) >= need) return {1, false};
+  // only when a quarter or more of the rows would be re-streamed: a few streamed rows cost the one-CU
+  // kernel less than a member's exchange (config 5 planted state, fp32: 47 resident of ≈ 47 rows, one
+  // CU 2.2× faster than P = 2 at 3 inner iterations)
+  if (lda::wide_resident_rows<T>(L.k) >= 0.75 * mean_rows) return {1, false};
   // two members of up to 1024 topics: measured at config 5 (k = 2000, fp64, E-step per minibatch) P = 2
   // 44.0 ms, one CU 53.7, P = 3 (a member without topics) 71.2, P = 4 61.9 — a member's exchange
   // latency is fixed, so the fewest members that hold the block win
