@@ -29,17 +29,25 @@ namespace lda {
 
 namespace {
 
-// (waves per document, topics per lane group, max rows per lane)
-template <int W_, int KL_, int RMAX_>
+// (waves per document, topics per lane group, max rows per lane, row sets in VGPRs)
+template <int W_, int KL_, int RMAX_, int RREG_ = 5>
 struct DShape {
   static constexpr int W = W_, KL = KL_, RMAX = RMAX_;
-  static constexpr int RREG = 5;  // row sets per lane in VGPRs (26·5 = 130); a sixth goes to LDS
+  static constexpr int RREG = RREG_;  // row sets per lane in VGPRs (26·5 = 130); the next goes to LDS
   static constexpr int RLDS = RREG + 1;  // row sets past this one are streamed from expElogβ'
   static constexpr int KLP = (KL + 1) / 2 * 2;  // LDS slice pitch (ds_read_b128 granules)
 };
 using D26 = DShape<1, 13, 8>;   // k <= 26
 using D52 = DShape<2, 13, 8>;   // k <= 52
 using D104 = DShape<4, 13, 8>;  // k <= 104 (k = 100: 8 slices of 13 topics)
+constexpr int kOnChipSets = 6;   // row sets the common kernel holds on chip (5 in VGPRs + 1 in LDS)
+// the long-document kernel's shape: G64_LONG_RREG row sets in VGPRs (4 was tried: no fewer scratch
+// spills in the seven- and eight-set variants, one more streamed set)
+#ifndef G64_LONG_RREG
+#define G64_LONG_RREG 5
+#endif
+template <class S>
+using DLong = DShape<S::W, S::KL, S::RMAX, G64_LONG_RREG>;
 
 template <class S>
 struct DLds {
@@ -395,7 +403,7 @@ __global__ __launch_bounds__(64 * S::W, 2) void k_estep_grid64(EStepArgs<double>
   d.s0 = a.indptr[d.row];
   d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
   const int rsets = (d.nnz + 31) >> 5;
-  if (LONG ? rsets <= S::RLDS : rsets > S::RLDS) return;  // the other kernel's document
+  if (LONG ? rsets <= kOnChipSets : rsets > kOnChipSets) return;  // the other kernel's document
   d.e0 = a.bptr ? a.bptr[d.slot] : d.s0;
   d.k = a.k;
   d.kp = a.kp;
@@ -437,7 +445,7 @@ __global__ __launch_bounds__(64 * S::W, 2) void k_estep_grid64(EStepArgs<double>
 
   // rows per lane for this document (block-uniform); the partition guarantees nnz <= 32·RMAX
   bool nonempty = false;
-  static_assert(S::RLDS == 6 && S::RMAX == 8, "row-set cases below");
+  static_assert(kOnChipSets == 6 && S::RMAX == 8 && (LONG || S::RLDS == kOnChipSets), "row-set cases below");
   if constexpr (LONG) {
     if (rsets == 7) nonempty = grid64_core<S, 7, STATS, BOUND>(a, sm, d);
     else nonempty = grid64_core<S, 8, STATS, BOUND>(a, sm, d);
@@ -523,7 +531,7 @@ void launch_d1(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound
 // caller knows no document has more than 32·RLDS rows
 template <class S>
 void launch_d(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs) {
-  if (long_docs) launch_d1<S, true>(s, a, stats, bound);
+  if (long_docs) launch_d1<DLong<S>, true>(s, a, stats, bound);
   launch_d1<S, false>(s, a, stats, bound);
 }
 
@@ -533,7 +541,7 @@ int grid64_row_cap(int k) {
   if (k <= 104) return 32 * D104::RMAX;
   return 0;
 }
-int grid64_onchip_rows(int k) { return k <= 104 ? 32 * D104::RLDS : 0; }
+int grid64_onchip_rows(int k) { return k <= 104 ? 32 * kOnChipSets : 0; }
 
 void launch_estep_grid64(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs) {
   if (a.n == 0) return;
