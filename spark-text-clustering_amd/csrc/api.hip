@@ -384,7 +384,7 @@ void check_team_timeout(stc_lda& L) {
 }
 
 template <typename T>
-void launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamChoice tc) {
+bool launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamChoice tc) {
   const int P = tc.P;
   Ctx& c = *L.ctx;
   hipStream_t s = c.stream;
@@ -393,7 +393,7 @@ void launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamCh
   lda::WideTeam wt;
   wt.P = P;
   wt.blocks = 8 * P * (cus / (8 * P));
-  STC_REQUIRE(wt.blocks > 0, "team E-step: too few CUs");
+  if (wt.blocks <= 0) return false;  // fewer CUs than one team per XCD group: the one-CU kernel
   const int teams = wt.blocks / P;
   // granules per member: rows split, the s partials + Σ r·φ; topics split, the φ partials + Σ|Δγ| + Σγ
   wt.xstride = std::max<int64_t>(L.kp + 1, 512 + 2);
@@ -410,9 +410,9 @@ void launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamCh
   // (a tag left by an earlier launch could equal an epoch this launch waits for)
   HIP_CHECK(hipMemsetAsync(L.team_words.p, 0, 16, s));
   HIP_CHECK(hipMemsetAsync(L.team_x.p, 0, xbytes, s));
-  if (tc.topics) lda::launch_estep_wide_tc<T>(s, w, stats, wt);
-  else lda::launch_estep_wide_mc<T>(s, w, stats, wt);
-  HIP_CHECK(hipMemcpyAsync(L.htmo, wt.tmo, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  const bool ok = tc.topics ? lda::launch_estep_wide_tc<T>(s, w, stats, wt) : lda::launch_estep_wide_mc<T>(s, w, stats, wt);
+  if (ok) HIP_CHECK(hipMemcpyAsync(L.htmo, wt.tmo, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  return ok;
 }
 
 // fast kernel on slots [0, n_short), workgroup kernel on [n_short, n); mean_rows = the launch's mean
@@ -426,8 +426,10 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
     w.slot0 = 0;
     w.n = n_short;
     const TeamChoice tc = use_wide(L.k, L.dtype) && !bound ? team_choice<T>(L, mean_rows) : TeamChoice{};
-    if (tc.P > 1) launch_wide_team<T>(L, w, stats, tc);
-    else if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
+    const bool team = tc.P > 1 && launch_wide_team<T>(L, w, stats, tc);
+    if (team) {
+      // launched (a refused cooperative grid falls through to the one-CU kernel)
+    } else if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
     else if constexpr (std::is_same<T, float>::value) lda::launch_estep_wave(s, w, stats, bound);
     else lda::launch_estep_grid64(s, w, stats, bound, m.max_row < 0 || m.max_row > lda::grid64_onchip_rows(L.k));
   }

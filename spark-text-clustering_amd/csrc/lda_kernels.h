@@ -97,11 +97,12 @@ struct WideTeam {
 };
 template <typename T>
 int wide_resident_rows(int k);
+// false: the runtime refused the cooperative grid (nothing launched; the caller runs the one-CU kernel)
 template <typename T>
-void launch_estep_wide_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt);
+bool launch_estep_wide_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt);
 // the same with the TOPICS split over the team (k > 512; lda_wide.hip k_estep_wide_tc)
 template <typename T>
-void launch_estep_wide_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt);
+bool launch_estep_wide_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt);
 template <typename T>
 void launch_estep_wide(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound);
 

@@ -1273,7 +1273,8 @@ int wide_resident_rows(int k) {
 }
 
 template <typename T, int Q>
-void launch_q_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
+bool launch_q_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
+  bool ok = true;
   constexpr int NR = wide_nr_mc<T, Q>();
   const size_t fixed = wide_lds_fixed<T>();
   const size_t row_bytes = sizeof(T) * kWThreads * Q;
@@ -1284,14 +1285,22 @@ void launch_q_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTea
     EStepArgs<T> aa = a;
     WideTeam ww = wt;
     void* args[] = {&aa, &nl, &ww};
-    HIP_CHECK(hipLaunchCooperativeKernel((const void*)kern, dim3((unsigned)wt.blocks), dim3(kWThreads), args, lds, s));
+    // the runtime rejects a grid that could not be resident (hipErrorCooperativeLaunchTooLarge):
+    // reported to the caller, which runs the one-CU kernel instead
+    const hipError_t e = hipLaunchCooperativeKernel((const void*)kern, dim3((unsigned)wt.blocks), dim3(kWThreads), args, lds, s);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      ok = false;
+    }
   };
   if (stats) go(k_estep_wide_mc<T, Q, NR, true>);
   else go(k_estep_wide_mc<T, Q, NR, false>);
+  return ok;
 }
 
 template <typename T, int Q>
-void launch_q_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
+bool launch_q_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
+  bool ok = true;
   constexpr int NR = wide_nr_mc<T, Q>();
   const size_t fixed = wide_lds_fixed<T>();
   const size_t row_bytes = sizeof(T) * kWThreads * Q;
@@ -1302,38 +1311,45 @@ void launch_q_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTea
     EStepArgs<T> aa = a;
     WideTeam ww = wt;
     void* args[] = {&aa, &nl, &ww};
-    HIP_CHECK(hipLaunchCooperativeKernel((const void*)kern, dim3((unsigned)wt.blocks), dim3(kWThreads), args, lds, s));
+    // the runtime rejects a grid that could not be resident (hipErrorCooperativeLaunchTooLarge):
+    // reported to the caller, which runs the one-CU kernel instead
+    const hipError_t e = hipLaunchCooperativeKernel((const void*)kern, dim3((unsigned)wt.blocks), dim3(kWThreads), args, lds, s);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      ok = false;
+    }
   };
   if (stats) go(k_estep_wide_tc<T, Q, NR, true>);
   else go(k_estep_wide_tc<T, Q, NR, false>);
+  return ok;
 }
 
 // topic split: member topics 512·Q with Q = ⌈k / (512·P)⌉ ≤ 4
 template <typename T>
-void launch_estep_wide_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
-  if (a.n == 0) return;
+bool launch_estep_wide_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
+  if (a.n == 0) return true;
   const int q = (a.k + kWThreads * wt.P - 1) / (kWThreads * wt.P);
-  if (q <= 1) launch_q_tc<T, 1>(s, a, stats, wt);
-  else if (q <= 2) launch_q_tc<T, 2>(s, a, stats, wt);
-  else if (q <= 4) launch_q_tc<T, 4>(s, a, stats, wt);
-  else throw Error(STC_ERR_INVALID_ARG, "topic-split team E-step: k > 2048·P");
+  if (q <= 1) return launch_q_tc<T, 1>(s, a, stats, wt);
+  if (q <= 2) return launch_q_tc<T, 2>(s, a, stats, wt);
+  if (q <= 4) return launch_q_tc<T, 4>(s, a, stats, wt);
+  throw Error(STC_ERR_INVALID_ARG, "topic-split team E-step: k > 2048·P");
 }
-template void launch_estep_wide_tc<float>(hipStream_t, const EStepArgs<float>&, bool, const WideTeam&);
-template void launch_estep_wide_tc<double>(hipStream_t, const EStepArgs<double>&, bool, const WideTeam&);
+template bool launch_estep_wide_tc<float>(hipStream_t, const EStepArgs<float>&, bool, const WideTeam&);
+template bool launch_estep_wide_tc<double>(hipStream_t, const EStepArgs<double>&, bool, const WideTeam&);
 
 template <typename T>
-void launch_estep_wide_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
-  if (a.n == 0) return;
-  if (a.k <= kWThreads) launch_q_mc<T, 1>(s, a, stats, wt);
-  else if (a.k <= 2 * kWThreads) launch_q_mc<T, 2>(s, a, stats, wt);
-  else if (a.k <= 4 * kWThreads) launch_q_mc<T, 4>(s, a, stats, wt);
-  else throw Error(STC_ERR_INVALID_ARG, "wide E-step: k > 2048");
+bool launch_estep_wide_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
+  if (a.n == 0) return true;
+  if (a.k <= kWThreads) return launch_q_mc<T, 1>(s, a, stats, wt);
+  if (a.k <= 2 * kWThreads) return launch_q_mc<T, 2>(s, a, stats, wt);
+  if (a.k <= 4 * kWThreads) return launch_q_mc<T, 4>(s, a, stats, wt);
+  throw Error(STC_ERR_INVALID_ARG, "wide E-step: k > 2048");
 }
 
 template int wide_resident_rows<float>(int);
 template int wide_resident_rows<double>(int);
-template void launch_estep_wide_mc<float>(hipStream_t, const EStepArgs<float>&, bool, const WideTeam&);
-template void launch_estep_wide_mc<double>(hipStream_t, const EStepArgs<double>&, bool, const WideTeam&);
+template bool launch_estep_wide_mc<float>(hipStream_t, const EStepArgs<float>&, bool, const WideTeam&);
+template bool launch_estep_wide_mc<double>(hipStream_t, const EStepArgs<double>&, bool, const WideTeam&);
 
 template <typename T>
 void launch_estep_wide(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound) {
