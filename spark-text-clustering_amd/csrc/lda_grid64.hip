@@ -9,8 +9,11 @@
 // eighth (nnz ≤ 256: long documents, and most of a planted-topic corpus at L = 200) are re-read from
 // expElogβ' in each pass (a few KB per document, L2-resident for the document's lifetime).
 //   φ_n = B_n·eθ : 13 lane-local fp64 FMAs per row, + the other group's partial through a 64-bit DPP
-//     row_ror:8 (lane i ↔ i^8), then the W wave partials meet in LDS behind the loop's one barrier;
-//     every wave adds them in the same order ⇒ bit-identical φ and r = cts/φ in every wave.
+//     row_ror:8 (lane i ↔ i^8), then the W wave partials meet in LDS.  W = 4: row set j's total and
+//     r = cts/φ are computed ONCE, by the (wave, group) pair 2·wave + group = j, and published behind
+//     a second barrier (one rcp chain per row instead of eight; 459 → 408 VALU instructions per
+//     iteration at R = 5).  W < 4: every wave adds the partials in the same order behind one barrier.
+//     Either way every wave sees bit-identical φ and r.
 //   s = Bᵀr : lane-local FMAs into 13 partials, reduce-scattered over the 32 row lanes (permlane32 /
 //     permlane16 swaps of both dwords, then row_half_mirror / quad_perm DPP pairs, all keeping bit 3)
 //     — each lane ends owning at most one topic of its group.
@@ -59,6 +62,9 @@ struct DLds {
   } __attribute__((aligned(16)));
   double red[2][S::W][2];
   double bd[S::W][2];
+  // W = 4: each row set's total φ and r, computed once by the (wave, group) that owns the set
+  double rtot[S::RMAX][32], dtot[S::RMAX][32];
+  int epsf[S::W];
   // per-row counts and 2^53·ε' (read each iteration from here rather than held in VGPRs)
   double rowc[32 * S::RMAX], rowe[32 * S::RMAX];
   // rows past RREG·32 (the sixth row set): their (wave, group) slice lives here, [p][row lane] with
@@ -280,21 +286,70 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
       }
       // Σ|Δγ| of the last update rides along with the φ exchange
       dsum = wave_sum_d(dg);
-      xchg_d<S>(sm, it & 1, wave, lane, rl, dot, R, dsum, dummy);
-      // Spark: while (meanGammaChange > 1e-3), meanGammaChange = Σ|Δγ| / k.  Wave-uniform by
-      // construction; readfirstlane makes the loop a scalar loop
-      const bool last =
-          __builtin_amdgcn_readfirstlane((int)((it > 0 && dsum / kd <= 1e-3) || it >= a.max_iter)) != 0;
+      bool last;
       uint64_t eps_live = 0;
+      if constexpr (W == 4) {
+        // the partials of the four waves meet in LDS; row set j's total φ and r are then computed ONCE,
+        // by worker (wave, group) = ((j mod 8) / 2, j mod 2) — the same sum order as every wave used
+        // before, so the same bits — and published for every wave behind a second barrier
+        double* const base = &sm.phi[0][0][0][0] + rl;
+        constexpr int BS = S::W * S::RMAX * 32, WS = S::RMAX * 32;
+        const int b = it & 1;
 #pragma unroll
-      for (int j = 0; j < R; ++j) {
-        const double cj = sm.rowc[32 * j + rl], ej = sm.rowe[32 * j + rl];
-        const double ph = fma(ej, 0x1p-53, dot[j]);
-        rr[j] = cj * rcp_nr(ph);
-        eps_live |= __builtin_amdgcn_ballot_w64(ej >= ph);  // ε' visible at fp64 resolution
-        if (BOUND && last && d.g == 0 && cj != 0.0) {
-          d.b_tok += cj * (log(fmax(dot[j], 0x1p-1074)) + a.logscale[a.indices[s0 + 32 * j + rl]]);
-          d.c_tok += cj;
+        for (int j = 0; j < R; ++j) base[b * BS + wave * WS + 32 * j] = dot[j];
+        if (lane == 0) sm.red[b][wave][0] = dsum;
+        __syncthreads();  // (A) partials published
+        dsum = sm.red[b][0][0];
+#pragma unroll
+        for (int w = 1; w < W; ++w) dsum += sm.red[b][w][0];
+        last = __builtin_amdgcn_readfirstlane((int)((it > 0 && dsum / kd <= 1e-3) || it >= a.max_iter)) != 0;
+        const int j = 2 * wave + d.g;  // this worker's row set (R ≤ 8 = workers)
+        bool live = false;
+        if (j < R) {
+          const double* const b0 = base + b * BS + 32 * j;
+          double dt = b0[0];
+#pragma unroll
+          for (int w = 1; w < W; ++w) dt += b0[w * WS];
+          const double cj = sm.rowc[32 * j + rl], ej = sm.rowe[32 * j + rl];
+          const double ph = fma(ej, 0x1p-53, dt);
+          sm.rtot[j][rl] = cj * rcp_nr(ph);
+          sm.dtot[j][rl] = dt;
+          live = ej >= ph;  // ε' visible at fp64 resolution
+        }
+        const uint64_t lv = __builtin_amdgcn_ballot_w64(live);
+        if (lane == 0) sm.epsf[wave] = lv != 0;
+        __syncthreads();  // (B) r and φ totals published
+#pragma unroll
+        for (int jj = 0; jj < R; ++jj) {
+          rr[jj] = sm.rtot[jj][rl];
+          dot[jj] = sm.dtot[jj][rl];
+        }
+        eps_live = (sm.epsf[0] | sm.epsf[1] | sm.epsf[2] | sm.epsf[3]) != 0;
+        if (BOUND && last && d.g == 0) {
+#pragma unroll
+          for (int jj = 0; jj < R; ++jj) {
+            const double cj = sm.rowc[32 * jj + rl];
+            if (cj != 0.0) {
+              d.b_tok += cj * (log(fmax(dot[jj], 0x1p-1074)) + a.logscale[a.indices[s0 + 32 * jj + rl]]);
+              d.c_tok += cj;
+            }
+          }
+        }
+      } else {
+        xchg_d<S>(sm, it & 1, wave, lane, rl, dot, R, dsum, dummy);
+        // Spark: while (meanGammaChange > 1e-3), meanGammaChange = Σ|Δγ| / k.  Wave-uniform by
+        // construction; readfirstlane makes the loop a scalar loop
+        last = __builtin_amdgcn_readfirstlane((int)((it > 0 && dsum / kd <= 1e-3) || it >= a.max_iter)) != 0;
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          const double cj = sm.rowc[32 * j + rl], ej = sm.rowe[32 * j + rl];
+          const double ph = fma(ej, 0x1p-53, dot[j]);
+          rr[j] = cj * rcp_nr(ph);
+          eps_live |= __builtin_amdgcn_ballot_w64(ej >= ph);  // ε' visible at fp64 resolution
+          if (BOUND && last && d.g == 0 && cj != 0.0) {
+            d.b_tok += cj * (log(fmax(dot[j], 0x1p-1074)) + a.logscale[a.indices[s0 + 32 * j + rl]]);
+            d.c_tok += cj;
+          }
         }
       }
       if (last) break;
