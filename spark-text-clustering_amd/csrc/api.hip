@@ -291,6 +291,7 @@ lda::EStepArgs<T> estep_args(stc_lda& L) {
   a.rank = L.ctx->rank;
   a.gamma_shape = L.cfg.gamma_shape;
   a.max_iter = L.cfg.max_inner_iter;
+  a.stop_thr = lda::stop_threshold(L.k);
   return a;
 }
 

@@ -57,7 +57,8 @@ struct DLds {
   double eth[S::W][2][S::KLP] __attribute__((aligned(16)));
   // the load stage (one 32-row step of the wave's 2·KL columns) is dead once the loop starts
   union {
-    double phi[2][S::W][S::RMAX][32];  // per row lane (both groups hold the same joined φ)
+    double phi[2][S::W][S::RMAX][32];   // W < 4: per row lane (both groups hold the same joined φ)
+    double phig[2][S::W][2][S::RMAX][32];  // W = 4: per (wave, group) partial, joined by the set's worker
     double stage[S::W][32 * 2 * S::KL];
   } __attribute__((aligned(16)));
   double red[2][S::W][2];
@@ -252,7 +253,6 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
     if (d.own) my_eth[d.tl] = eth;
     __builtin_amdgcn_wave_barrier();  // the slices are read back only by this wave
     int it = 0;
-    const double kd = (double)d.k;
     double dg = 0.0;  // |Δγ| of the owned topic in the last update
     while (true) {
       // Phase A: φ_n = B_n·eθ (+ ε'_n below) ; r_n = cts_n / φ_n
@@ -281,8 +281,13 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
             if (2 * c + 1 < KL) acc[j] = fma(y[2 * c + 1], e.y, acc[j]);
           }
         }
+        if constexpr (W == 4) {  // the groups' partials are joined by the set's worker (LDS)
 #pragma unroll
-        for (int j = 0; j < R; ++j) dot[j] = acc[j] + dpp_d<DPP_ROW_ROR8>(acc[j]);  // + the other group
+          for (int j = 0; j < R; ++j) dot[j] = acc[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < R; ++j) dot[j] = acc[j] + dpp_d<DPP_ROW_ROR8>(acc[j]);  // + the other group
+        }
       }
       // Σ|Δγ| of the last update rides along with the φ exchange
       dsum = wave_sum_d(dg);
@@ -292,24 +297,24 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
         // the partials of the four waves meet in LDS; row set j's total φ and r are then computed ONCE,
         // by worker (wave, group) = ((j mod 8) / 2, j mod 2) — the same sum order as every wave used
         // before, so the same bits — and published for every wave behind a second barrier
-        double* const base = &sm.phi[0][0][0][0] + rl;
-        constexpr int BS = S::W * S::RMAX * 32, WS = S::RMAX * 32;
+        double* const base = &sm.phig[0][0][0][0][0] + rl;
+        constexpr int GS = S::RMAX * 32, WS = 2 * GS, BS = S::W * WS;
         const int b = it & 1;
 #pragma unroll
-        for (int j = 0; j < R; ++j) base[b * BS + wave * WS + 32 * j] = dot[j];
+        for (int j = 0; j < R; ++j) base[b * BS + wave * WS + d.g * GS + 32 * j] = dot[j];
         if (lane == 0) sm.red[b][wave][0] = dsum;
         __syncthreads();  // (A) partials published
         dsum = sm.red[b][0][0];
 #pragma unroll
         for (int w = 1; w < W; ++w) dsum += sm.red[b][w][0];
-        last = __builtin_amdgcn_readfirstlane((int)((it > 0 && dsum / kd <= 1e-3) || it >= a.max_iter)) != 0;
+        last = __builtin_amdgcn_readfirstlane((int)((it > 0 && dsum <= a.stop_thr) || it >= a.max_iter)) != 0;
         const int j = 2 * wave + d.g;  // this worker's row set (R ≤ 8 = workers)
         bool live = false;
         if (j < R) {
           const double* const b0 = base + b * BS + 32 * j;
-          double dt = b0[0];
+          double dt = b0[0] + b0[GS];  // (wave 0, group 0) + (wave 0, group 1), then waves 1..3 alike
 #pragma unroll
-          for (int w = 1; w < W; ++w) dt += b0[w * WS];
+          for (int w = 1; w < W; ++w) dt += b0[w * WS] + b0[w * WS + GS];
           const double cj = sm.rowc[32 * j + rl], ej = sm.rowe[32 * j + rl];
           const double ph = fma(ej, 0x1p-53, dt);
           sm.rtot[j][rl] = cj * rcp_nr(ph);
@@ -339,7 +344,7 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
         xchg_d<S>(sm, it & 1, wave, lane, rl, dot, R, dsum, dummy);
         // Spark: while (meanGammaChange > 1e-3), meanGammaChange = Σ|Δγ| / k.  Wave-uniform by
         // construction; readfirstlane makes the loop a scalar loop
-        last = __builtin_amdgcn_readfirstlane((int)((it > 0 && dsum / kd <= 1e-3) || it >= a.max_iter)) != 0;
+        last = __builtin_amdgcn_readfirstlane((int)((it > 0 && dsum <= a.stop_thr) || it >= a.max_iter)) != 0;
 #pragma unroll
         for (int j = 0; j < R; ++j) {
           const double cj = sm.rowc[32 * j + rl], ej = sm.rowe[32 * j + rl];

@@ -1,6 +1,8 @@
 // lda_kernels.h — host-side launch API of the online-LDA kernels (lda.hip).
 #pragma once
 
+#include <cmath>
+
 #include "stc_internal.h"
 
 namespace stc {
@@ -53,6 +55,9 @@ struct EStepArgs {
   int64_t doc_id_base = 0;
   double gamma_shape = 100.0;
   int max_iter = 100000;
+  // Spark's stop rule Σ|Δγ|/k ≤ 1e-3 as one comparison: the largest double T with fl(T / k) ≤ 1e-3
+  // (fl(x / k) is monotone in x, so x ≤ T ⇔ fl(x / k) ≤ 1e-3 exactly; stop_threshold() below)
+  double stop_thr = 0.0;
   // outputs
   T* gamma = nullptr;                  // n×k (optional)
   T* eth = nullptr;                    // n×kp scaled exp(E[log θ]) (STATS)
@@ -64,6 +69,15 @@ struct EStepArgs {
   int32_t* nonempty = nullptr;         // n (optional)
   double* bound = nullptr;             // n (BOUND)
 };
+
+// the largest double x with fl(x / k) ≤ 1e-3 (host; see EStepArgs::stop_thr)
+inline double stop_threshold(int k) {
+  const double kd = (double)k;
+  double x = 1e-3 * kd;
+  while (x / kd > 1e-3) x = std::nextafter(x, 0.0);
+  while (std::nextafter(x, INFINITY) / kd <= 1e-3) x = std::nextafter(x, INFINITY);
+  return x;
+}
 
 template <typename T>
 size_t estep_lds_bytes(int kp, int lds_rows, int P);
