@@ -6,7 +6,9 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=${PROF_OUT:-gpurun_out/prof}; rm -rf $OUT; mkdir -p $OUT
-B="bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-hbm-copy --no-secondary ${BENCH_ARGS:-}"
+# --workers 1: no corpus-generation worker processes (forked after the profiler initialised the GPU,
+# they hung a --pmc pass twice)
+B="bench.py --steps 5 --warmup 3 --no-cpu-baseline --no-hbm-copy --no-secondary --workers 1 ${BENCH_ARGS:-}"
 PASSES=${PROF_PASSES:-"stats fetch write sq grbm"}
 run() {  # run NAME SECONDS ARGS...
   local name=$1 secs=$2; shift 2
