@@ -5,9 +5,10 @@
 // other five lane bits a row lane rl; wave w, group g own KL = 13 topics [(2w+g)·13, +13), so k ≤ 104
 // takes W = 4 (k = 100: eight slices of 13).  A lane holds rows n = 32·j + rl (j < R, R = ⌈nnz/32⌉
 // chosen per document) of its slice: R·13 doubles = 26·R VGPRs for R ≤ 5; a sixth row set (nnz ≤ 192)
-// is read from LDS, which keeps the loop free of scratch spills at two waves per SIMD; a seventh and
-// eighth (nnz ≤ 256: long documents, and most of a planted-topic corpus at L = 200) are re-read from
-// expElogβ' in each pass (a few KB per document, L2-resident for the document's lifetime).
+// is read from LDS, which keeps the loop free of scratch spills at two waves per SIMD.  Documents with
+// a seventh and eighth set (nnz ≤ 256: long documents, and 13 % of a planted-topic corpus at L = 200)
+// run in a second launch with all eight sets in VGPRs at one wave per SIMD (the row-streaming path,
+// expElogβ' re-read each pass, remains for a shape with fewer register sets than row sets).
 //   φ_n = B_n·eθ : 13 lane-local fp64 FMAs per row, + the other group's partial through a 64-bit DPP
 //     row_ror:8 (lane i ↔ i^8), then the W wave partials meet in LDS.  W = 4: row set j's total and
 //     r = cts/φ are computed ONCE, by the (wave, group) pair 2·wave + group = j, and published behind
@@ -44,10 +45,16 @@ using D26 = DShape<1, 13, 8>;   // k <= 26
 using D52 = DShape<2, 13, 8>;   // k <= 52
 using D104 = DShape<4, 13, 8>;  // k <= 104 (k = 100: 8 slices of 13 topics)
 constexpr int kOnChipSets = 6;   // row sets the common kernel holds on chip (5 in VGPRs + 1 in LDS)
-// the long-document kernel's shape: G64_LONG_RREG row sets in VGPRs (4 was tried: no fewer scratch
-// spills in the seven- and eight-set variants, one more streamed set)
+// the long-document kernel's shape: all G64_LONG_RREG = 8 row sets in VGPRs at one workgroup per CU
+// (G64_LONG_OCC; 346 VGPRs of the 512 a lone wave gets, no scratch, nothing streamed).  Measured on the
+// planted-topic state (13 % of its documents have 193–256 rows): E-step 6.79 → 6.31 ms against five
+// register sets at two workgroups per CU, which spilled and re-read two sets from expElogβ' per pass
+// (four register sets: no fewer spills).
 #ifndef G64_LONG_RREG
-#define G64_LONG_RREG 5
+#define G64_LONG_RREG 8
+#endif
+#ifndef G64_LONG_OCC
+#define G64_LONG_OCC 1  // long-document kernel workgroups per CU the register budget is cut for
 #endif
 template <class S>
 using DLong = DShape<S::W, S::KL, S::RMAX, G64_LONG_RREG>;
@@ -447,7 +454,7 @@ __device__ __forceinline__ bool grid64_core(const EStepArgs<double>& a, DLds<S>&
 // kernels run over the same slots and each skips the other's documents, so the streamed variants'
 // register pressure stays out of the common kernel.
 template <class S, bool STATS, bool BOUND, bool LONG>
-__global__ __launch_bounds__(64 * S::W, 2) void k_estep_grid64(EStepArgs<double> a) {
+__global__ __launch_bounds__(64 * S::W, LONG ? G64_LONG_OCC : 2) void k_estep_grid64(EStepArgs<double> a) {
   constexpr int W = S::W, KL = S::KL;
   constexpr int N1 = hup(KL), N2 = hup(N1), N3 = hup(N2), N4 = hup(N3), N5 = hup(N4);
   __shared__ DLds<S> sm;
