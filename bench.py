@@ -19,7 +19,7 @@ Rank 0 prints ONE JSON line.  value = Σ_ranks minibatch docs in the K timed ste
 max-over-ranks wall time.  Model state: timing starts after exactly
 --state-minibatches (20) minibatches from λ₀ (burn-in + warmup), so the inner-iteration count does
 not depend on --warmup; the first 3 minibatches from λ₀ are timed separately as the "cold" figure.
-roofline: the dominant kernel (the training E-step: k_estep_grid64 for fp64, k_estep_grid for
+roofline: the dominant kernel (the training E-step: k_estep_rows64 for fp64, k_estep_grid for
 fp32; one launch per minibatch): SURVEY.md §8(d) algorithmic bytes per doc
 (nnz·(4 + s) + 2·nnz·k·s + s·k, s = 8 for fp64, 4 for fp32) × the launch's docs ÷ its HIP-event time
 on the library stream; traffic: the PMC FETCH_SIZE(×2, gfx950) + WRITE_SIZE per launch of that
@@ -335,8 +335,8 @@ def kernel_name(dtype, k):
         return ("k_estep_wide / k_estep_wide_mc (lda_wide.hip): the many-topic training E-step (k <= 512: a "
                 "team of CUs per document), one launch per minibatch")
     if dtype == "f64":
-        return ("k_estep_grid64 (lda_grid64.hip): the fp64 training E-step, one launch per minibatch (plus "
-                "the streamed-row launch when a document has > 192 rows)")
+        return ("k_estep_rows64 (lda_rows64.hip): the fp64 training E-step, one launch per minibatch (plus "
+                "the 7-8-row-set launch when a document has > 192 rows)")
     return "k_estep_grid (lda_grid.hip): the fp32 training E-step, one launch per minibatch"
 
 

@@ -208,6 +208,8 @@ int stc_lda_set_alpha(stc_lda* lda, const double* alpha /* k */);
 int stc_lda_get_alpha(stc_lda* lda, double* alpha_out /* k */);
 int stc_lda_get_eta(stc_lda* lda, double* eta_out);
 int stc_lda_get_iteration(stc_lda* lda, int64_t* iteration_out);
+/* k and V of the handle (the JNI shim sizes and checks its Java arrays with them) */
+int stc_lda_shape(const stc_lda* lda, int32_t* k_out, int64_t* vocab_out);
 
 /* One submitMiniBatch over an injected membership: batch_doc_ids are row indices of this
  * rank's corpus (duplicates allowed = sampling with replacement).  gamma0 (n×k, may be NULL)

@@ -15,9 +15,13 @@
  *   - host arrays are pinned with Get<Type>ArrayElements for the duration of the call (the library
  *     copies inputs before it returns and writes outputs before it returns); outputs are released
  *     with mode 0 (copy back), inputs with JNI_ABORT; a null Java array is passed as NULL.
+ *   - every array's length is checked against the elements the C ABI will read or write (sizes from
+ *     the handles: stc_lda_shape, stc_dcsr_shape) BEFORE anything is pinned: a short array throws
+ *     IllegalArgumentException instead of letting the library overrun the pinned copy.
  */
 #include <jni.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -44,6 +48,35 @@ static int check(JNIEnv* env, int st) {
     if (arr) (*env)->Release##JT##ArrayElements(env, (arr), (void*)(p), (mode)); \
   } while (0)
 #define LEN(arr) ((arr) ? (int64_t)(*env)->GetArrayLength(env, (arr)) : (int64_t)0)
+
+static void throw_iae(JNIEnv* env, const char* msg) {
+  jclass ex = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+  if (ex) (*env)->ThrowNew(env, ex, msg);
+}
+/* 1 (with IllegalArgumentException pending) when a non-null array holds fewer than `need` elements;
+ * a null array passes (the C ABI takes NULL as "not given" and rejects it where it is required) */
+static int short_array(JNIEnv* env, jarray arr, int64_t need, const char* what) {
+  if (!arr) return 0;
+  const int64_t n = (int64_t)(*env)->GetArrayLength(env, arr);
+  if (n >= need) return 0;
+  char msg[192];
+  snprintf(msg, sizeof msg, "%s: the Java array has %lld elements, the call needs %lld", what, (long long)n,
+           (long long)need);
+  throw_iae(env, msg);
+  return 1;
+}
+#define NEED(arr, n, what) short_array(env, (jarray)(arr), (int64_t)(n), (what))
+static int lda_shape(JNIEnv* env, jlong lda, int64_t* k, int64_t* vocab) {
+  int32_t kk = 0;
+  int64_t vv = 0;
+  if (check(env, stc_lda_shape(LDA(lda), &kk, &vv))) return 1;
+  *k = kk;
+  *vocab = vv;
+  return 0;
+}
+static int csr_shape(JNIEnv* env, jlong m, int64_t* rows, int64_t* cols, int64_t* nnz) {
+  return check(env, stc_dcsr_shape(CSR(m), rows, cols, nnz));
+}
 
 /* ---- library / device ------------------------------------------------------------------ */
 JNIEXPORT jstring JNICALL FN(lastError)(JNIEnv* env, jclass c) {
@@ -101,6 +134,13 @@ JNIEXPORT void JNICALL FN(commAllreduceF64)(JNIEnv* env, jclass c, jlong ctx, jd
 JNIEXPORT jlong JNICALL FN(dcsrUpload)(JNIEnv* env, jclass c, jlong ctx, jlong rows, jlong cols,
                                        jlongArray indptr, jintArray indices, jdoubleArray values, jint dtype) {
   stc_dcsr* out = NULL;
+  if (rows < 0 || !indptr || NEED(indptr, rows + 1, "dcsrUpload indptr")) {
+    if (!(*env)->ExceptionCheck(env)) throw_iae(env, "dcsrUpload: indptr[rows + 1] is required");
+    return 0;
+  }
+  jlong last = 0;
+  (*env)->GetLongArrayRegion(env, indptr, (jsize)rows, 1, &last);
+  if (NEED(indices, last, "dcsrUpload indices") || NEED(values, last, "dcsrUpload values")) return 0;
   jlong* ip = PIN(jlong, Long, indptr);
   jint* ix = PIN(jint, Int, indices);
   jdouble* vs = PIN(jdouble, Double, values);
@@ -123,6 +163,10 @@ JNIEXPORT jlongArray JNICALL FN(dcsrShape)(JNIEnv* env, jclass c, jlong m) {
 
 JNIEXPORT void JNICALL FN(dcsrDownload)(JNIEnv* env, jclass c, jlong ctx, jlong m, jlongArray indptr,
                                         jintArray indices, jdoubleArray values) {
+  int64_t rows = 0, cols = 0, nnz = 0;
+  if (csr_shape(env, m, &rows, &cols, &nnz) || NEED(indptr, rows + 1, "dcsrDownload indptr") ||
+      NEED(indices, nnz, "dcsrDownload indices") || NEED(values, nnz, "dcsrDownload values"))
+    return;
   jlong* ip = PIN(jlong, Long, indptr);
   jint* ix = PIN(jint, Int, indices);
   jdouble* vs = PIN(jdouble, Double, values);
@@ -155,6 +199,10 @@ JNIEXPORT jlong JNICALL FN(hashingTfDev)(JNIEnv* env, jclass c, jlong ctx, jbyte
 JNIEXPORT void JNICALL FN(hashingTf)(JNIEnv* env, jclass c, jlong ctx, jbyteArray utf8, jlongArray tok_off,
                                      jlongArray doc_off, jint num_features, jboolean binary, jint variant,
                                      jlongArray indptr_out, jintArray indices_out, jdoubleArray values_out) {
+  const int64_t n_tok = LEN(tok_off) - 1, n_docs = LEN(doc_off) - 1;
+  if (NEED(indptr_out, n_docs + 1, "hashingTf indptrOut") || NEED(indices_out, n_tok, "hashingTf indicesOut") ||
+      NEED(values_out, n_tok, "hashingTf valuesOut"))
+    return;
   jbyte* u = PIN(jbyte, Byte, utf8);
   jlong* to = PIN(jlong, Long, tok_off);
   jlong* dof = PIN(jlong, Long, doc_off);
@@ -175,6 +223,7 @@ JNIEXPORT void JNICALL FN(hashingTf)(JNIEnv* env, jclass c, jlong ctx, jbyteArra
 
 JNIEXPORT void JNICALL FN(hashTokens)(JNIEnv* env, jclass c, jlong ctx, jbyteArray utf8, jlongArray tok_off,
                                       jint num_features, jint variant, jintArray idx_out) {
+  if (NEED(idx_out, LEN(tok_off) - 1, "hashTokens idxOut")) return;
   jbyte* u = PIN(jbyte, Byte, utf8);
   jlong* to = PIN(jlong, Long, tok_off);
   jint* ix = PIN(jint, Int, idx_out);
@@ -220,6 +269,10 @@ JNIEXPORT jlong JNICALL FN(hashingTfTokens)(JNIEnv* env, jclass c, jlong ctx, jl
 JNIEXPORT jlongArray JNICALL FN(tokenize)(JNIEnv* env, jclass c, jlong ctx, jbyteArray text, jlongArray text_off,
                                           jbyteArray utf8_out, jlongArray tok_off_out, jlongArray doc_off_out) {
   int64_t nb = 0, nt = 0;
+  const int64_t n_bytes = LEN(text), n_docs = LEN(text_off) - 1;
+  if (NEED(utf8_out, n_bytes, "tokenize utf8Out") || NEED(tok_off_out, n_bytes + n_docs + 1, "tokenize tokOffOut") ||
+      NEED(doc_off_out, n_docs + 1, "tokenize docOffOut"))
+    return NULL;
   jbyte* t = PIN(jbyte, Byte, text);
   jlong* off = PIN(jlong, Long, text_off);
   jbyte* u = PIN(jbyte, Byte, utf8_out);
@@ -257,7 +310,10 @@ JNIEXPORT jlong JNICALL FN(tokenizeHashingTfDev)(JNIEnv* env, jclass c, jlong ct
 /* idfOut[numCols], dfOut[numCols] (may be null); returns m */
 JNIEXPORT jlong JNICALL FN(idfFit)(JNIEnv* env, jclass c, jlong ctx, jlong dcsr, jlong min_doc_freq,
                                    jdoubleArray idf_out, jlongArray df_out) {
-  int64_t m = 0;
+  int64_t m = 0, rows = 0, cols = 0, nnz = 0;
+  if (csr_shape(env, dcsr, &rows, &cols, &nnz) || NEED(idf_out, cols, "idfFit idfOut") ||
+      NEED(df_out, cols, "idfFit dfOut"))
+    return 0;
   jdouble* o = PIN(jdouble, Double, idf_out);
   jlong* df = PIN(jlong, Long, df_out);
   int st = stc_idf_fit(CTX(ctx), CSR(dcsr), min_doc_freq, o, (int64_t*)df, &m);
@@ -269,6 +325,8 @@ JNIEXPORT jlong JNICALL FN(idfFit)(JNIEnv* env, jclass c, jlong ctx, jlong dcsr,
 
 JNIEXPORT void JNICALL FN(idfTransform)(JNIEnv* env, jclass c, jlong ctx, jlong dcsr, jdoubleArray idf,
                                         jdouble zero_floor) {
+  int64_t rows = 0, cols = 0, nnz = 0;
+  if (csr_shape(env, dcsr, &rows, &cols, &nnz) || NEED(idf, cols, "idfTransform idf")) return;
   jdouble* p = PIN(jdouble, Double, idf);
   int st = stc_idf_transform(CTX(ctx), CSR(dcsr), p, zero_floor);
   UNPIN(Double, idf, p, JNI_ABORT);
@@ -316,6 +374,8 @@ JNIEXPORT void JNICALL FN(ldaInitRandom)(JNIEnv* env, jclass c, jlong lda, jlong
 }
 
 JNIEXPORT void JNICALL FN(ldaSetTopics)(JNIEnv* env, jclass c, jlong lda, jdoubleArray topics, jint layout) {
+  int64_t k = 0, V = 0;
+  if (lda_shape(env, lda, &k, &V) || NEED(topics, k * V, "ldaSetTopics topics")) return;
   jdouble* p = PIN(jdouble, Double, topics);
   int st = stc_lda_set_topics(LDA(lda), p, layout);
   UNPIN(Double, topics, p, JNI_ABORT);
@@ -323,6 +383,8 @@ JNIEXPORT void JNICALL FN(ldaSetTopics)(JNIEnv* env, jclass c, jlong lda, jdoubl
 }
 
 JNIEXPORT void JNICALL FN(ldaGetTopics)(JNIEnv* env, jclass c, jlong lda, jdoubleArray out, jint layout) {
+  int64_t k = 0, V = 0;
+  if (lda_shape(env, lda, &k, &V) || NEED(out, k * V, "ldaGetTopics out")) return;
   jdouble* p = PIN(jdouble, Double, out);
   int st = stc_lda_get_topics(LDA(lda), p, layout);
   UNPIN(Double, out, p, 0);
@@ -330,6 +392,8 @@ JNIEXPORT void JNICALL FN(ldaGetTopics)(JNIEnv* env, jclass c, jlong lda, jdoubl
 }
 
 JNIEXPORT void JNICALL FN(ldaSetAlpha)(JNIEnv* env, jclass c, jlong lda, jdoubleArray alpha) {
+  int64_t k = 0, V = 0;
+  if (lda_shape(env, lda, &k, &V) || NEED(alpha, k, "ldaSetAlpha alpha")) return;
   jdouble* p = PIN(jdouble, Double, alpha);
   int st = stc_lda_set_alpha(LDA(lda), p);
   UNPIN(Double, alpha, p, JNI_ABORT);
@@ -337,6 +401,8 @@ JNIEXPORT void JNICALL FN(ldaSetAlpha)(JNIEnv* env, jclass c, jlong lda, jdouble
 }
 
 JNIEXPORT void JNICALL FN(ldaGetAlpha)(JNIEnv* env, jclass c, jlong lda, jdoubleArray out) {
+  int64_t k = 0, V = 0;
+  if (lda_shape(env, lda, &k, &V) || NEED(out, k, "ldaGetAlpha out")) return;
   jdouble* p = PIN(jdouble, Double, out);
   int st = stc_lda_get_alpha(LDA(lda), p);
   UNPIN(Double, out, p, 0);
@@ -355,6 +421,15 @@ JNIEXPORT jlong JNICALL FN(ldaGetIteration)(JNIEnv* env, jclass c, jlong lda) {
   return it;
 }
 
+/* {k, vocabSize} */
+JNIEXPORT jlongArray JNICALL FN(ldaShape)(JNIEnv* env, jclass c, jlong lda) {
+  int64_t s[2] = {0, 0};
+  if (lda_shape(env, lda, &s[0], &s[1])) return NULL;
+  jlongArray out = (*env)->NewLongArray(env, 2);
+  if (out) (*env)->SetLongArrayRegion(env, out, 0, 2, (const jlong*)s);
+  return out;
+}
+
 /* step statistics as doubles: {batchDocs, nonemptyDocs, batchEntries, innerIters, innerItersMax,
  * capHits, rho} */
 static void stats_out(JNIEnv* env, jdoubleArray out, const stc_step_stats* s) {
@@ -368,6 +443,8 @@ JNIEXPORT void JNICALL FN(ldaStep)(JNIEnv* env, jclass c, jlong lda, jlongArray 
                                    jdoubleArray stats) {
   stc_step_stats s;
   memset(&s, 0, sizeof s);
+  int64_t k = 0, V = 0;
+  if (lda_shape(env, lda, &k, &V) || NEED(gamma0, LEN(ids) * k, "ldaStep gamma0")) return;
   jlong* p = PIN(jlong, Long, ids);
   jdouble* g = PIN(jdouble, Double, gamma0);
   int st = stc_lda_step(LDA(lda), (const int64_t*)p, LEN(ids), g, stats ? &s : NULL);
@@ -384,6 +461,12 @@ JNIEXPORT void JNICALL FN(ldaNext)(JNIEnv* env, jclass c, jlong lda, jdoubleArra
 
 JNIEXPORT void JNICALL FN(ldaEstep)(JNIEnv* env, jclass c, jlong lda, jlongArray ids, jdoubleArray gamma0,
                                     jdoubleArray gamma_out, jdoubleArray stat_out, jintArray iters_out) {
+  int64_t k = 0, V = 0;
+  const int64_t n = LEN(ids);
+  if (lda_shape(env, lda, &k, &V) || NEED(gamma0, n * k, "ldaEstep gamma0") ||
+      NEED(gamma_out, n * k, "ldaEstep gammaOut") || NEED(stat_out, V * k, "ldaEstep statOut") ||
+      NEED(iters_out, n, "ldaEstep itersOut"))
+    return;
   jlong* p = PIN(jlong, Long, ids);
   jdouble* g0 = PIN(jdouble, Double, gamma0);
   jdouble* g = PIN(jdouble, Double, gamma_out);
@@ -402,6 +485,10 @@ JNIEXPORT void JNICALL FN(ldaEstep)(JNIEnv* env, jclass c, jlong lda, jlongArray
 JNIEXPORT jdoubleArray JNICALL FN(ldaBound)(JNIEnv* env, jclass c, jlong lda, jlong dcsr, jlong gamma_seed,
                                             jlong doc_id_base, jdoubleArray gamma0) {
   double r[4] = {0, 0, 0, 0};
+  int64_t k = 0, V = 0, rows = 0, cols = 0, nnz = 0;
+  if (lda_shape(env, lda, &k, &V) || csr_shape(env, dcsr, &rows, &cols, &nnz) ||
+      NEED(gamma0, rows * k, "ldaBound gamma0"))
+    return NULL;
   jdouble* g = PIN(jdouble, Double, gamma0);
   int st = stc_lda_bound(LDA(lda), CSR(dcsr), (uint64_t)gamma_seed, doc_id_base, g, &r[0], &r[1], &r[2], &r[3]);
   UNPIN(Double, gamma0, g, JNI_ABORT);
@@ -413,6 +500,10 @@ JNIEXPORT jdoubleArray JNICALL FN(ldaBound)(JNIEnv* env, jclass c, jlong lda, jl
 
 JNIEXPORT void JNICALL FN(ldaTopicDistribution)(JNIEnv* env, jclass c, jlong lda, jlong dcsr, jlong gamma_seed,
                                                 jlong doc_id_base, jdoubleArray gamma0, jdoubleArray out) {
+  int64_t k = 0, V = 0, rows = 0, cols = 0, nnz = 0;
+  if (lda_shape(env, lda, &k, &V) || csr_shape(env, dcsr, &rows, &cols, &nnz) ||
+      NEED(gamma0, rows * k, "ldaTopicDistribution gamma0") || NEED(out, rows * k, "ldaTopicDistribution out"))
+    return;
   jdouble* g = PIN(jdouble, Double, gamma0);
   jdouble* o = PIN(jdouble, Double, out);
   int st = stc_lda_topic_distribution(LDA(lda), CSR(dcsr), (uint64_t)gamma_seed, doc_id_base, g, o);
@@ -423,6 +514,10 @@ JNIEXPORT void JNICALL FN(ldaTopicDistribution)(JNIEnv* env, jclass c, jlong lda
 
 JNIEXPORT void JNICALL FN(ldaDescribe)(JNIEnv* env, jclass c, jlong lda, jint max_terms, jintArray idx_out,
                                        jdoubleArray weight_out) {
+  int64_t k = 0, V = 0;
+  if (lda_shape(env, lda, &k, &V)) return;
+  const int64_t N = max_terms < V ? (max_terms > 0 ? max_terms : 0) : V;
+  if (NEED(idx_out, k * N, "ldaDescribe idxOut") || NEED(weight_out, k * N, "ldaDescribe weightOut")) return;
   jint* ix = PIN(jint, Int, idx_out);
   jdouble* w = PIN(jdouble, Double, weight_out);
   int st = stc_lda_describe(LDA(lda), max_terms, (int32_t*)ix, w);
@@ -436,6 +531,7 @@ JNIEXPORT void JNICALL FN(ldaEnableTiming)(JNIEnv* env, jclass c, jlong lda, jbo
 }
 
 JNIEXPORT void JNICALL FN(ldaCounters)(JNIEnv* env, jclass c, jlong lda, jlongArray out) {
+  if (NEED(out, 4, "ldaCounters out")) return;
   jlong* p = PIN(jlong, Long, out);
   int st = stc_lda_counters(LDA(lda), (int64_t*)p);
   UNPIN(Long, out, p, 0);
@@ -445,6 +541,7 @@ JNIEXPORT void JNICALL FN(ldaCounters)(JNIEnv* env, jclass c, jlong lda, jlongAr
 /* msOut[5]; returns the number of timed steps */
 JNIEXPORT jlong JNICALL FN(ldaPhaseTimes)(JNIEnv* env, jclass c, jlong lda, jdoubleArray ms_out) {
   int64_t steps = 0;
+  if (NEED(ms_out, 5, "ldaPhaseTimes msOut")) return 0;
   jdouble* p = PIN(jdouble, Double, ms_out);
   int st = stc_lda_phase_times(LDA(lda), p, &steps);
   UNPIN(Double, ms_out, p, 0);

@@ -78,6 +78,8 @@ public final class StcNative {
   public static native void ldaGetAlpha(long lda, double[] out);
   public static native double ldaGetEta(long lda);
   public static native long ldaGetIteration(long lda);
+  /** {k, vocabSize} of the handle */
+  public static native long[] ldaShape(long lda);
   /** stats (nullable, 7): batchDocs, nonemptyDocs, batchEntries, innerIters, innerItersMax, capHits, rho */
   public static native void ldaStep(long lda, long[] batchDocIds, double[] gamma0, double[] stats);
   public static native void ldaNext(long lda, double[] stats);

@@ -416,6 +416,15 @@ bool launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamCh
   return ok;
 }
 
+// development switch: STC_G64=grid runs lda_grid64.hip's topic-split kernel instead of the rows split
+bool use_old_grid64() {
+  static const bool v = [] {
+    const char* e = getenv("STC_G64");
+    return e && std::string(e) == "grid";
+  }();
+  return v;
+}
+
 // fast kernel on slots [0, n_short), workgroup kernel on [n_short, n); mean_rows = the launch's mean
 // entries per document (the many-topic kernel's team size)
 template <typename T>
@@ -432,7 +441,8 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
       // launched (a refused cooperative grid falls through to the one-CU kernel)
     } else if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
     else if constexpr (std::is_same<T, float>::value) lda::launch_estep_wave(s, w, stats, bound);
-    else lda::launch_estep_grid64(s, w, stats, bound, m.max_row < 0 || m.max_row > lda::grid64_onchip_rows(L.k));
+    else if (use_old_grid64()) lda::launch_estep_grid64(s, w, stats, bound, m.max_row < 0 || m.max_row > lda::grid64_onchip_rows(L.k));
+    else lda::launch_estep_rows64(s, w, stats, bound, m.max_row < 0 || m.max_row > lda::rows64_onchip_rows(L.k));
   }
   if (n > n_short) {
     a.slot0 = n_short;
@@ -1467,6 +1477,14 @@ int stc_lda_get_eta(stc_lda* L, double* eta_out) {
   return guard([&] {
     STC_REQUIRE(L && eta_out, "lda/eta_out");
     *eta_out = L->eta;
+  });
+}
+
+int stc_lda_shape(const stc_lda* L, int32_t* k_out, int64_t* vocab_out) {
+  return guard([&] {
+    STC_REQUIRE(L, "lda");
+    if (k_out) *k_out = L->k;
+    if (vocab_out) *vocab_out = L->V;
   });
 }
 

@@ -98,6 +98,10 @@ void launch_estep_grid(hipStream_t s, const EStepArgs<float>& a, bool stats, boo
 int grid64_row_cap(int k);
 int grid64_onchip_rows(int k);  // rows past this are streamed (a second launch, `long_docs`)
 void launch_estep_grid64(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs);
+// fp64 rows-split E-step (lda_rows64.hip): same k / row caps as the grid kernel
+int rows64_row_cap(int k);
+int rows64_onchip_rows(int k);
+void launch_estep_rows64(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs);
 // many-topic E-step (lda_wide.hip): topics across a 512-thread workgroup, k <= 2048, nnz <= wide_row_cap(k)
 int wide_row_cap(int k);
 // a team of P CUs per document for the many-topic E-step (lda_wide.hip k_estep_wide_mc)

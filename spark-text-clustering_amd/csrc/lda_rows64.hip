@@ -1,0 +1,462 @@
+// lda_rows64.hip — K6 at Spark's precision: the ROWS-split fp64 E-step for k ≤ 104
+// ([U] OnlineLDAOptimizer.variationalTopicInference in Breeze Double, called per document inside
+// submitMiniBatch behind lda.run, TextClustering/src/main/scala/LDAClustering.scala:61).
+//
+// One document per workgroup of four waves.  Wave w holds rows n = 32·j + 8·w + rl (row set j < R,
+// R = ⌈nnz/32⌉ chosen per document) for EVERY topic; inside a wave lane = tl + 8·rl, and topic lane
+// tl holds topics [KL·tl, KL·tl + KL) of its R rows: R·KL doubles (k ≤ 104: KL = 13, 26·R VGPRs for
+// R ≤ 5, a sixth row set in LDS; documents with 7–8 row sets run in a second launch with all eight
+// sets in VGPRs at one workgroup per CU).
+//   φ_n = B_n·eθ : KL lane-local FMAs per row; the eight topic lanes' partials go to the wave's own
+//     LDS rows and worker lane q (one per wave row) adds them in a fixed order, forms r_q = cts/φ
+//     once and publishes it to the wave.  The exchange never leaves the wave: no block barrier.
+//   s = Bᵀr : R lane-local FMAs per topic, KL partials per lane to LDS, ONE block barrier; then the
+//     ψ waves of this iteration read a topic's 32 partials per lane, update γ and compute
+//     eθ = exp(ψ(γ) − ψ(Σγ')) for ⌈kp/2⌉ topics each (k > 64: two ψ waves, alternating between
+//     waves {0,1} and {2,3} by iteration parity so every SIMD carries the transcendental chain every
+//     other iteration; k ≤ 64: one, rotating over the four waves), publish eθ and γ, second barrier.
+//   ψ(Σγ') from Σγ' = Σα + Σ_n cts_n − Σ_n r_n·ε'_n (exact in real arithmetic): a per-document
+//     constant unless some row's ε' is visible at fp64 resolution (ε' ≥ 2^-53·φ).
+//   Spark's stop rule Σ|Δγ|/k ≤ 1e-3 is one comparison against EStepArgs::stop_thr; the ψ waves'
+//     Σ|Δγ| partials ride the second barrier.
+// Against lda_grid64.hip's topic split (each wave a 26-topic slice, the s reduction a 32-lane DPP /
+// permlane reduce-scatter of 13 values in every wave, ψ/exp in all four waves) this removes ≈ 75
+// cross-lane and ≈ 200 transcendental VALU instructions per document-iteration and the scratch
+// reload the old loop carried; the cost is LDS traffic (13 8-byte stores per lane and iteration),
+// which the LDS array absorbs beside the VALU (MI355X_MICROARCH.md §LDS).
+// Numerics as lda.hip: Bp row-scaled by e^{-m_v}, Spark's 1e-100 carried as ε'_n = 1e-100·e^{-m_v}.
+#include "estep_common.h"
+
+#ifndef R64_LOAD_BATCH
+#define R64_LOAD_BATCH 2  // row sets whose B loads are in flight together in the load phase
+#endif
+#ifndef R64_LONG_OCC
+#define R64_LONG_OCC 1  // long-document kernel workgroups per CU the register budget is cut for
+#endif
+
+namespace stc {
+namespace lda {
+
+namespace {
+
+constexpr int kW = 4;          // waves per document
+constexpr int kSbPitch = 34;   // s-partial row pitch (doubles): conflict-free 8-B stores, 16-B reads
+constexpr int kOnChipSets = 6; // row sets the common kernel holds (5 in VGPRs + 1 in LDS)
+constexpr int kMaxSets = 8;    // one worker lane per wave row: 8 row lanes × 8 sets = 64 lanes
+
+template <int KL_, int RREG_, int RMAX_>
+struct RShape {
+  static constexpr int KL = KL_;             // topics per topic lane (8 topic lanes: k ≤ 8·KL)
+  static constexpr int KLP = (KL_ + 1) / 2 * 2;
+  static constexpr int KT = 8 * KL_;
+  static constexpr int RREG = RREG_;         // row sets in VGPRs
+  static constexpr int RMAX = RMAX_;         // row sets handled (≤ kMaxSets)
+  static constexpr int NOVF = RMAX_ > RREG_ ? RMAX_ - RREG_ : 0;  // row sets in LDS
+};
+template <int KL>
+using RCommon = RShape<KL, 5, kOnChipSets>;
+template <int KL>
+using RLong = RShape<KL, kMaxSets, kMaxSets>;
+
+template <class S>
+struct RLds {
+  double eth[8][S::KLP] __attribute__((aligned(16)));  // eθ, topic t at [t / KL][t % KL]
+  double gam[S::KT];               // γ
+  double dgv[128];                 // |Δγ| of the last update per topic (0 past kp): Σ → the stop rule
+  double2 rowce[kW][8 * S::RMAX] __attribute__((aligned(16)));  // per (wave, wave row): {cts, 2^53·ε'}
+  double esum[kW] __attribute__((aligned(16)));  // Σ r·ε' over a wave's rows (0 unless an ε' is visible)
+  double part[kW][4];              // per-wave partial sums (init: Σγ₀, Σα, Σcts; end: Σγ, bound terms)
+  double cs;                       // ψ(Σγ') of the current eθ (the bound's scale)
+  union {
+    double sb[S::KT][kSbPitch];            // s partials (topic, row lane 8·w + rl)
+    double stage[kW][8][S::KT + 2];        // load phase: eight B rows per wave at a time
+  } u __attribute__((aligned(16)));
+  double ovf[S::NOVF > 0 ? S::NOVF * kW * S::KL * 64 : 1];  // row sets past RREG ([set][w][p][lane])
+};
+
+template <class S, int R, bool STATS, bool BOUND>
+__device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& sm, int64_t slot, int64_t row,
+                                           int64_t mem, int64_t s0, int64_t e0, int nnz) {
+  constexpr int KL = S::KL, KLP = S::KLP;
+  constexpr int RG = R < S::RREG ? R : S::RREG;  // row sets in VGPRs; [RG, R) in sm.ovf
+  static_assert(R >= 1 && R <= S::RMAX && R - RG <= S::NOVF, "row sets");
+  STAMP_DECL
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tl = lane & 7, rl = lane >> 3;
+  const int k = a.k, kp = a.kp;
+  // ψ-lane topic map: k > 64 two ψ waves of `half` topics (t = (w & 1)·half + lane), else one
+  const int npsi = kp > 64 ? 2 : 1;
+  const int half = npsi == 2 ? (kp + 1) / 2 : kp;
+  const int pw = npsi == 2 ? (w & 1) : 0;
+  const int tt = pw * half + lane;
+  const bool tval = lane < half && tt < kp;  // γ / eθ slot (the fp64 pad column included)
+  const bool town = lane < half && tt < k;   // a real topic
+  const int ttl = tt / KL, ttp = tt - ttl * KL;
+  const double alp = town ? a.alpha[tt] : 0.0;
+
+  // ---- this lane's rows n = 32·j + 8·w + rl: ids, counts, ε' (the topic-lane-0 copy goes to LDS)
+  int ids[R];
+  double ct = 0.0;
+  bool any = false;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    const int n = 32 * j + 8 * w + rl;
+    const bool v = n < nnz;
+    const int64_t e = v ? s0 + n : 0;
+    ids[j] = v ? a.indices[e] : 0;
+    const double c = v ? a.values[e] : 0.0;
+    any |= c != 0.0;
+    ct += c;
+    if (tl == 0) {
+      // ε'_n = 1e-100·e^{-m_v} held as 2^53·ε' (the test 2^53·ε' ≥ φ is then direct), capped at 1e300
+      // where e^{-m_v} overflows (Spark's unscaled row is 0 there; r ≈ cts·1e-284 reproduces that).
+      // Padding rows hold −2^53 (φ = −1, r = −0, never live).
+      const double e2 = v ? fmin(0x1p53 * exp(kLogEps - a.logscale[ids[j]]), 1e300) : -0x1p53;
+      sm.rowce[w][8 * j + rl] = make_double2(c, e2);
+    }
+  }
+
+  // ---- B rows, coalesced: per row set the wave copies its eight rows (kp doubles each) with
+  // 16-byte loads, stages them in LDS and every lane picks up its (row lane, topic lane) part
+  double B[RG][KL];
+  double* const ovf = sm.ovf + (size_t)w * KL * 64 + lane;  // set RG + i at ovf[i·kW·KL·64 + 64·p]
+#define BV(j, p) ((j) < RG ? B[(j) < RG ? (j) : 0][p] : ovf[((j) - RG) * kW * KL * 64 + 64 * (p)])
+  {
+    const int C2 = kp >> 1;                     // double2 pieces per row
+    constexpr int NP = (8 * (S::KT / 2) + 63) / 64;  // pieces per lane per row set (upper bound)
+    double* const stg = &sm.u.stage[w][0][0];
+    constexpr int SP = S::KT + 2;
+#pragma unroll
+    for (int j0 = 0; j0 < R; j0 += R64_LOAD_BATCH) {
+      double2 pc[R64_LOAD_BATCH][NP];
+#pragma unroll
+      for (int jj = 0; jj < R64_LOAD_BATCH; ++jj) {
+        const int j = j0 + jj;
+        if (j >= R) break;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const int c = lane + 64 * i;
+          const int srow = c / C2, q = c - srow * C2;
+          const int id = __builtin_amdgcn_ds_bpermute((8 * (srow & 7)) << 2, ids[j]);  // row lane srow
+          const bool keep = c < 8 * C2 && 32 * j + 8 * w + srow < nnz;
+          const double2 x = *reinterpret_cast<const double2*>(a.Bp + (int64_t)(keep ? id : 0) * kp + 2 * (keep ? q : 0));
+          pc[jj][i] = keep ? x : make_double2(0.0, 0.0);
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < R64_LOAD_BATCH; ++jj) {
+        const int j = j0 + jj;
+        if (j >= R) break;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const int c = lane + 64 * i;
+          const int srow = c / C2, q = c - srow * C2;
+          if (c < 8 * C2) *reinterpret_cast<double2*>(stg + srow * SP + 2 * q) = pc[jj][i];
+        }
+        __builtin_amdgcn_wave_barrier();  // one wave writes and reads its stage; LDS is in order per wave
+#pragma unroll
+        for (int p = 0; p < KL; ++p) {
+          const int t = KL * tl + p;
+          const double v = t < k ? stg[rl * SP + t] : 0.0;
+          if (j < RG) B[j < RG ? j : 0][p] = v;
+          else ovf[(j - RG) * kW * KL * 64 + 64 * p] = v;  // read back only by this lane
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+
+  // ---- γ₀ / α partials (the first npsi waves hold the topics), Σcts, eθ and |Δγ| pads
+  double g0 = 0.0;
+  if (w < npsi) {
+    if (town) {
+      if (a.gamma0) {
+        g0 = a.gamma0[mem * k + tt];
+      } else {
+        const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, mem) : (uint64_t)(a.doc_id_base + row);
+        g0 = gamma_sample(doc_stream(a.seed, key), tt, a.gamma_shape);
+      }
+    }
+    if (tval) sm.gam[tt] = g0;
+  }
+  for (int i = threadIdx.x; i < 8 * KLP; i += 64 * kW) (&sm.eth[0][0])[i] = 0.0;
+  if (threadIdx.x < 128) sm.dgv[threadIdx.x] = 0.0;
+  {
+    const double gs = wave_sum_d(g0), as = wave_sum_d(alp), cts = wave_sum_d(tl == 0 ? ct : 0.0);
+    if (lane == 0) {
+      sm.part[w][0] = w < npsi ? gs : 0.0;
+      sm.part[w][1] = w < npsi ? as : 0.0;
+      sm.part[w][2] = cts;
+    }
+  }
+  const bool nonempty = __syncthreads_or(any) != 0;  // (also publishes γ₀, rowce and the partials)
+  const double gsum0 = (sm.part[0][0] + sm.part[1][0]) + (sm.part[2][0] + sm.part[3][0]);
+  const double asum = (sm.part[0][1] + sm.part[1][1]) + (sm.part[2][1] + sm.part[3][1]);
+  const double ctot = (sm.part[0][2] + sm.part[1][2]) + (sm.part[2][2] + sm.part[3][2]);
+
+  if (!nonempty) {
+    if (w < npsi) {
+      if (town) {
+        if (a.gamma) a.gamma[mem * k + tt] = 0.0;
+        if (STATS) a.elogth[slot * k + tt] = 0.0;
+      }
+      if (STATS && tval) a.eth[slot * kp + tt] = 0.0;
+    }
+    if (threadIdx.x == 0) {
+      if (a.iters) a.iters[mem] = 0;
+      if (a.nonempty) a.nonempty[mem] = 0;
+      if (BOUND) a.bound[mem] = 0.0;
+    }
+    return;
+  }
+  // eθ = exp(ψ(γ) − ψ(Σγ)): Spark's unscaled exp(E[log θ]); inside the loop ψ(Σγ') comes from the
+  // Σα + Σcts − Σ r·ε' identity, so without a visible ε' it is one constant per document
+  const double cs_flat = digamma_fast_d(asum + ctot);
+  {
+    const double cs0 = digamma_fast_d(gsum0);
+    if (w < npsi && town) sm.eth[ttl][ttp] = exp_digamma_minus_fast(g0, cs0);
+    if (threadIdx.x == 0) sm.cs = cs0;
+  }
+  __syncthreads();
+
+  double* const sb = &sm.u.sb[0][0];
+  double rr[R], dt[R];  // r = cts/φ and φ without ε' of the lane's rows (final values are the outputs)
+  int it = 0;
+  STAMP(0);  // loads, γ₀, first eθ, two barriers
+  while (true) {
+    // Σ|Δγ| of the last update (Spark: meanGammaChange = Σ|Δγ| / k), every wave from the same LDS
+    // values in the same order, so the stop decision is block-uniform; reads issued with eθ's
+    const double dg2 = sm.dgv[lane] + sm.dgv[lane + 64];
+    double2 ce[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) ce[j] = sm.rowce[w][8 * j + rl];
+    // Phase A: φ over the lane's KL topics, then all-reduced over the row's eight topic lanes
+    // (xor-1, xor-2, mirror-8 butterfly; a + b == b + a, so all eight lanes hold identical bits)
+    {
+      double acc[R];
+#pragma unroll
+      for (int j = 0; j < R; ++j) acc[j] = 0.0;
+#pragma unroll
+      for (int c = 0; c < KLP / 2; ++c) {
+        const double2 e = *reinterpret_cast<const double2*>(&sm.eth[tl][2 * c]);
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+          acc[j] = fma(BV(j, 2 * c), e.x, acc[j]);
+          if (2 * c + 1 < KL) acc[j] = fma(BV(j, 2 * c + 1), e.y, acc[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j) acc[j] += dpp_d<DPP_QP_1032>(acc[j]);
+#pragma unroll
+      for (int j = 0; j < R; ++j) acc[j] += dpp_d<DPP_QP_2301>(acc[j]);
+#pragma unroll
+      for (int j = 0; j < R; ++j) dt[j] = acc[j] + dpp_d<DPP_ROW_HALF_MIRROR>(acc[j]);
+    }
+    STAMP(1);  // eθ reads, φ FMAs, the topic-lane all-reduce
+    bool live = false;
+    double ev = 0.0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const double ph = fma(ce[j].y, 0x1p-53, dt[j]);
+      rr[j] = ce[j].x * rcp_nr(ph);
+      live |= ce[j].y >= ph;  // ε' visible at fp64 resolution
+      ev = fma(rr[j], ce[j].y * 0x1p-53, ev);
+    }
+    const double dsum = wave_sum_d(dg2);
+    if (__builtin_amdgcn_ballot_w64(live) != 0) {
+      const double e = wave_sum_d(tl == 0 ? ev : 0.0);  // each row once (topic lane 0)
+      if (lane == 0) sm.esum[w] = e;
+    } else if (lane == 0) {
+      sm.esum[w] = 0.0;
+    }
+    STAMP(2);  // r, ε' ballot, Σ|Δγ|
+    // Spark: while (meanGammaChange > 1e-3)
+    if ((it > 0 && dsum <= a.stop_thr) || it >= a.max_iter) break;
+
+    // Phase B: s partials over the lane's R rows, one row lane's slot per topic
+#pragma unroll
+    for (int p = 0; p < KL; ++p) {
+      double x = 0.0;
+#pragma unroll
+      for (int j = 0; j < R; ++j) x = fma(BV(j, p), rr[j], x);
+      sb[(KL * tl + p) * kSbPitch + 8 * w + rl] = x;
+    }
+    STAMP(3);  // s FMAs + partial stores
+    __syncthreads();  // (1) s partials and esum published
+    STAMP(4);  // barrier 1
+    const bool psi = npsi == 2 ? ((w >> 1) == (it & 1)) : (w == (it & 3));
+    if (psi) {
+      if (town) {
+        // the phase's LDS reads in two batches (16 partials each, with γ, eθ and the ε' sums)
+        const double2* const sp = reinterpret_cast<const double2*>(sb + tt * kSbPitch);
+        const double g = sm.gam[tt], eo = sm.eth[ttl][ttp];
+        const double2 e01 = *reinterpret_cast<const double2*>(&sm.esum[0]);
+        const double2 e23 = *reinterpret_cast<const double2*>(&sm.esum[2]);
+        double c4[4];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          double2 xs[8];
+#pragma unroll
+          for (int h = 0; h < 8; ++h) xs[h] = sp[8 * b + h];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const double2 x0 = xs[4 * h], x1 = xs[4 * h + 1], x2 = xs[4 * h + 2], x3 = xs[4 * h + 3];
+            c4[2 * b + h] = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
+          }
+        }
+        const double s = (c4[0] + c4[1]) + (c4[2] + c4[3]);
+        const double et = (e01.x + e01.y) + (e23.x + e23.y);
+        const double csn = et != 0.0 ? digamma_fast_d(asum + ctot - et) : cs_flat;
+        const double gn = fma(eo, s, alp);  // γ ← eθ ⊙ s + α
+        sm.dgv[tt] = fabs(gn - g);
+        sm.gam[tt] = gn;
+        sm.eth[ttl][ttp] = exp_digamma_minus_fast(gn, csn);
+        if (tt == 0) sm.cs = csn;
+      }
+    }
+    STAMP(psi ? 5 : 8);  // ψ phase (ψ waves; non-ψ waves: nothing)
+    __syncthreads();  // (2) eθ, γ, |Δγ| published
+    STAMP(psi ? 6 : 9);  // barrier 2 (ψ waves / the others)
+    ++it;
+  }
+#undef BV
+
+  // ---- outputs.  Exact Σγ of the final γ (ψ(Σγ) of E[log θ] and the bound)
+  const double gfin = (w < npsi && town) ? sm.gam[tt] : 0.0;
+  {
+    const double gs = wave_sum_d(gfin);
+    double bt = 0.0, bc = 0.0;
+    if (BOUND && tl == 0) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const int n = 32 * j + 8 * w + rl;
+        const double c = sm.rowce[w][8 * j + rl].x;
+        if (n < nnz && c != 0.0) {
+          bt += c * (log(fmax(dt[j], 0x1p-1074)) + a.logscale[a.indices[s0 + n]]);
+          bc += c;
+        }
+      }
+    }
+    if (BOUND) {
+      bt = wave_sum_d(bt);
+      bc = wave_sum_d(bc);
+    }
+    if (lane == 0) {
+      sm.part[w][0] = w < npsi ? gs : 0.0;
+      sm.part[w][1] = bt;
+      sm.part[w][2] = bc;
+    }
+  }
+  __syncthreads();
+  const double gsum = (sm.part[0][0] + sm.part[1][0]) + (sm.part[2][0] + sm.part[3][0]);
+  const double psisum = digamma_t<double>(gsum);
+  double topic = 0.0;
+  if (w < npsi) {
+    if (town) {
+      const double el = digamma_t<double>(gfin) - psisum;
+      if (a.gamma) a.gamma[mem * k + tt] = gfin;
+      if (STATS) a.elogth[slot * k + tt] = el;
+      if (BOUND) topic = (alp - gfin) * el + (lgamma(gfin) - lgamma(alp));
+    }
+    if (STATS && tval) a.eth[slot * kp + tt] = sm.eth[ttl][ttp];  // the eθ the final φ used
+  }
+  if (tl == 0) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int n = 32 * j + 8 * w + rl;
+      if (n < nnz) {
+        a.r[e0 + n] = rr[j];
+        if (STATS) {
+          a.keys[e0 + n] = (uint32_t)a.indices[s0 + n];
+          a.vals[e0 + n] = entry_val<double>(slot, e0 + n, rr[j]);
+        }
+      }
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (a.iters) a.iters[mem] = it;
+    if (a.nonempty) a.nonempty[mem] = 1;
+  }
+  STAMP(7);
+  STAMP_FLUSH
+  if (BOUND) {
+    topic = wave_sum_d(topic);
+    if (lane == 0) sm.part[w][3] = topic;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double tok = 0.0, ctk = 0.0, tp = 0.0;
+#pragma unroll
+      for (int v = 0; v < kW; ++v) {
+        tok += sm.part[v][1];
+        ctk += sm.part[v][2];
+        tp += sm.part[v][3];
+      }
+      const double elog_max = sm.cs - psisum;  // log of the scale eθ carried (≈ 0)
+      a.bound[mem] = tok + ctk * elog_max + tp + (lgamma(asum) - lgamma(gsum));
+    }
+  }
+}
+
+// LONG = false: documents with ≤ kOnChipSets row sets; LONG = true: 7–8 sets.  Both kernels run over
+// the same slots and each skips the other's documents.
+template <class S, bool STATS, bool BOUND, bool LONG>
+__global__ __launch_bounds__(64 * kW, LONG ? R64_LONG_OCC : 2) void k_estep_rows64(EStepArgs<double> a) {
+  __shared__ RLds<S> sm;
+  if ((int64_t)blockIdx.x >= a.n) return;
+  const int64_t slot = a.slot0 + blockIdx.x;
+  const int64_t row = a.batch ? (int64_t)a.batch[slot] : slot;
+  const int64_t mem = a.orig ? (int64_t)a.orig[slot] : slot;
+  const int64_t s0 = a.indptr[row];
+  const int nnz = (int)(a.indptr[row + 1] - s0);
+  const int rsets = (nnz + 31) >> 5;
+  if (LONG ? rsets <= kOnChipSets : rsets > kOnChipSets) return;  // the other kernel's document
+  const int64_t e0 = a.bptr ? a.bptr[slot] : s0;
+  if constexpr (LONG) {
+    if (rsets == 7) rows64_doc<S, 7, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz);
+    else rows64_doc<S, 8, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz);
+  } else {
+    switch (rsets) {
+      case 0:
+      case 1: rows64_doc<S, 1, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz); break;
+      case 2: rows64_doc<S, 2, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz); break;
+      case 3: rows64_doc<S, 3, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz); break;
+      case 4: rows64_doc<S, 4, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz); break;
+      case 5: rows64_doc<S, 5, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz); break;
+      default: rows64_doc<S, 6, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz); break;
+    }
+  }
+}
+
+template <class S, bool LONG>
+void launch_r1(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound) {
+  const dim3 grid((unsigned)a.n);
+  const int threads = 64 * kW;
+  if (stats) k_estep_rows64<S, true, false, LONG><<<grid, threads, 0, s>>>(a);
+  else if (bound) k_estep_rows64<S, false, true, LONG><<<grid, threads, 0, s>>>(a);
+  else k_estep_rows64<S, false, false, LONG><<<grid, threads, 0, s>>>(a);
+  KERNEL_CHECK();
+}
+// the 7–8-set documents first (`long_docs` = false when the caller knows there are none), then the rest
+template <int KL>
+void launch_r(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs) {
+  if (long_docs) launch_r1<RLong<KL>, true>(s, a, stats, bound);
+  launch_r1<RCommon<KL>, false>(s, a, stats, bound);
+}
+
+}  // namespace
+
+int rows64_row_cap(int k) { return k <= 104 ? 32 * kMaxSets : 0; }
+int rows64_onchip_rows(int k) { return k <= 104 ? 32 * kOnChipSets : 0; }
+
+void launch_estep_rows64(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs) {
+  if (a.n == 0) return;
+  if (a.kp > 8 * 13 || a.kp < a.k || (a.kp & 1)) throw Error(STC_ERR_INVALID_ARG, "fp64 rows E-step: bad k / kp");
+  if (a.k <= 32) launch_r<4>(s, a, stats, bound, long_docs);
+  else if (a.k <= 56) launch_r<7>(s, a, stats, bound, long_docs);
+  else launch_r<13>(s, a, stats, bound, long_docs);
+}
+
+STC_STAMP_READER(stc_debug_stamps_rows64)
+
+}  // namespace lda
+}  // namespace stc

@@ -1,0 +1,28 @@
+#!/bin/bash
+# A/B of an E-step change: the LDA parity tests, the headline (and planted) bench lines with the new
+# kernel (and, with OLD=1, with STC_G64=grid — the previous one), then the stamp build's phase split
+# (STAMP=1).  One time limit per step; stops at the first failure.
+mkdir -p gpurun_out; : > gpurun_out/status.log
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" >> gpurun_out/status.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+  return 0
+}
+B="python bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-secondary --no-hbm-copy"
+P="--corpus zipf-lda --state planted"
+if [ "${TESTS:-default}" != "none" ]; then
+  step t_lda ${T_SECS:-500} python -u -m pytest ${TESTS/default/tests/test_gpu_lda.py tests/test_gpu_shapes.py tests/test_gpu_config1.py} -x -v -m gpu --timeout 150 --timeout-method thread
+fi
+step b_new 240 $B
+step p_new 240 $B $P
+if [ -n "$OLD" ]; then
+  step b_old 240 env STC_G64=grid $B
+  step p_old 240 env STC_G64=grid $B $P
+fi
+if [ -n "$STAMP" ]; then
+  step stamp 200 env STC_LIB=spark-text-clustering_amd/stc/libstc_stamp.so python tools/stamp_rows64.py
+  step stampp 200 env STC_LIB=spark-text-clustering_amd/stc/libstc_stamp.so python tools/stamp_rows64.py --corpus zipf-lda
+fi
