@@ -141,9 +141,11 @@ int stc_hash_tokens(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const in
  * tokens kept, trailing empty tokens dropped, a separator-free string is one token ("" → [""]) —
  * laid out as stc_hashing_tf's input: the separator-free lower-cased blob utf8_out (capacity
  * n_bytes), tok_off_out (capacity n_bytes + n_docs + 1) and doc_off_out[n_docs+1].
- * Lower-casing is Java 8's String.toLowerCase (root locale) for every code point up to U+07FF
- * (Latin, Greek, Cyrillic, Armenian, …); U+0130, U+03A3, U+023A, U+023E and cased characters past
- * U+07FF fail with STC_ERR_INVALID_ARG (caseless punctuation/CJK/emoji blocks pass through).   */
+ * Lower-casing is Java 8's String.toLowerCase (root locale, Unicode 6.2) for every code point: the BMP
+ * through a generated table, Deseret inline, characters Java 8 does not case passed through.  The 18
+ * code points whose mapping is not a same-length 1:1 map (U+0130 İ, U+03A3 Σ's Final_Sigma rule, and
+ * capitals whose lower case changes UTF-8 length: U+023A, U+023E, U+1E9E, U+2126, U+212A, U+212B,
+ * U+2C62, U+2C64, U+2C6D–U+2C70, U+2C7E, U+2C7F, U+A78D, U+A7AA) fail with STC_ERR_INVALID_ARG.   */
 int stc_tokenize(stc_ctx* ctx, const uint8_t* text, int64_t n_bytes, const int64_t* text_off,
                  int64_t n_docs, uint8_t* utf8_out, int64_t* n_out_bytes, int64_t* tok_off_out,
                  int64_t* n_tok_out, int64_t* doc_off_out);

@@ -132,20 +132,28 @@ def java_split_whitespace(s: str):
 
 
 # Spark 2.4.3 runs on Java 8 (Unicode 6.2): code points assigned later are unassigned there and
-# toLowerCase leaves them alone; Python's newer database lower-cases these (the ones below are the
-# cased additions in U+0000–U+07FF, the range the GPU kernel maps).  Case pairs are otherwise stable
+# toLowerCase leaves them alone; Python's newer database (3.10: Unicode 13.0) lower-cases the cased
+# additions of Unicode 7.0–13.0 (U+037F, U+0528–U+052F, U+A698–U+A69F, U+A794–U+A79F, U+A7AB–U+A7FF,
+# Georgian Mtavruli U+1C90–U+1CBF; supplementary: Warang Citi, Old Hungarian, Osage, Medefaidrin,
+# Adlam) and the Cherokee letters U+13A0–U+13FF, caseless in 6.2.  Case pairs are otherwise stable
 # across Unicode versions, and String.toLowerCase(Locale.ROOT)'s special casings (U+0130 → "i̇",
-# Final_Sigma for U+03A3) are Python's str.lower too.
-_JAVA8_UNASSIGNED = frozenset([0x37F] + list(range(0x528, 0x530)))
+# Final_Sigma for U+03A3) are Python's str.lower too.  (tools/gen_case_table.py holds the same BMP set.)
+_JAVA8_IDENTITY_RANGES = ((0x37F, 0x37F), (0x528, 0x52F), (0x13A0, 0x13FF), (0x1C90, 0x1CBF), (0xA698, 0xA69F),
+                          (0xA794, 0xA79F), (0xA7AB, 0xA7FF), (0x104B0, 0x104FF), (0x10C80, 0x10CFF),
+                          (0x118A0, 0x118FF), (0x16E40, 0x16E9F), (0x1E900, 0x1E95F))
+
+
+def java8_identity(cp: int) -> bool:
+    return any(lo <= cp <= hi for lo, hi in _JAVA8_IDENTITY_RANGES)
 
 
 def java_lower(text: str) -> str:
     """[U] java.lang.String.toLowerCase(Locale.ROOT) on Java 8, restated with str.lower."""
-    if not any(ord(ch) in _JAVA8_UNASSIGNED for ch in text):
+    if not any(java8_identity(ord(ch)) for ch in text if ord(ch) >= 0x37F):
         return text.lower()
     out, seg = [], []
     for ch in text:
-        if ord(ch) in _JAVA8_UNASSIGNED:
+        if java8_identity(ord(ch)):
             out.append("".join(seg).lower())
             out.append(ch)
             seg = []

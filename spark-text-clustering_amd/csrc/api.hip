@@ -67,6 +67,7 @@ struct stc_lda {
   int team_force = 0;
   DevBuf team_words, team_x;
   unsigned* htmo = nullptr;  // pinned copy of the team kernel's timeout word
+  bool team_ran = false;     // the current call launched a team kernel (its timeout word is checked)
 
   // M-step sharding over the vocabulary (multi-GPU): rank r owns λ / expElogβ rows [r·Vs, (r+1)·Vs);
   // Vs is a multiple of the λ-update block so the per-block colsum partials (and hence colsum) are
@@ -375,13 +376,36 @@ TeamChoice team_choice(const stc_lda& L, double mean_rows) {
   return {std::max(2, std::min(4, (L.k + 1023) / 1024)), true};
 }
 
-// the team kernel's timeout word (copied to pinned memory after each launch; read once the stream has
-// passed it): a team whose partner never arrived gave up instead of hanging
-void check_team_timeout(stc_lda& L) {
-  if (L.htmo && *L.htmo) {
-    *L.htmo = 0;
-    throw Error(STC_ERR_HIP, "many-topic team E-step: a team member did not arrive (timed out)");
+// The team kernel's timeout word: a team whose partner never arrived gave up instead of hanging.  The
+// word gates the same call's M-step on the device (launch_gate_on_timeout poisons the non-empty count,
+// so λ, expElogβ', colsum and α stay as they were) and is copied to pinned memory after the launch;
+// finish_team() waits for the stream at the end of the call and raises the failure there — from the
+// call that failed, never from a later one.  `rollback`: undo the host-side step bookkeeping.
+void finish_team(stc_lda& L, bool rollback, int64_t n, int64_t E) {
+  if (!L.team_ran) return;
+  L.team_ran = false;
+  HIP_CHECK(hipStreamSynchronize(L.ctx->stream));
+  bool failed = L.htmo && *L.htmo;
+  if (rollback && !failed) {  // another rank's team timed out: its poisoned count reached this rank too
+    double gate = 0.0;
+    HIP_CHECK(hipMemcpy(&gate, L.small.as<double>() + L.k, sizeof(double), hipMemcpyDeviceToHost));
+    failed = gate < 0.0;
   }
+  if (failed) {
+    if (L.htmo) *L.htmo = 0;
+    if (rollback) {
+      L.iteration -= 1;
+      L.cum_docs -= n;
+      L.cum_entries -= E;
+    }
+    throw Error(STC_ERR_HIP, "many-topic team E-step: a team member did not arrive (timed out); the model "
+                             "was left unchanged");
+  }
+}
+// debug knob STC_TEAM_FAULT=m: member m of team 0 never publishes (its partners time out quickly)
+int team_fault_member() {
+  const char* e = getenv("STC_TEAM_FAULT");
+  return e ? atoi(e) : -1;
 }
 
 template <typename T>
@@ -407,12 +431,17 @@ bool launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamCh
   }
   wt.tmo = L.team_words.as<unsigned>();
   wt.xbuf = L.team_x.p;
+  wt.fault_member = team_fault_member();
+  if (wt.fault_member >= 0) wt.spin_limit = 1u << 14;
   // every polled word zeroed before every launch: the timeout word, and the granules' epoch tags
   // (a tag left by an earlier launch could equal an epoch this launch waits for)
   HIP_CHECK(hipMemsetAsync(L.team_words.p, 0, 16, s));
   HIP_CHECK(hipMemsetAsync(L.team_x.p, 0, xbytes, s));
   const bool ok = tc.topics ? lda::launch_estep_wide_tc<T>(s, w, stats, wt) : lda::launch_estep_wide_mc<T>(s, w, stats, wt);
-  if (ok) HIP_CHECK(hipMemcpyAsync(L.htmo, wt.tmo, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  if (ok) {
+    HIP_CHECK(hipMemcpyAsync(L.htmo, wt.tmo, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    L.team_ran = true;
+  }
   return ok;
 }
 
@@ -490,7 +519,7 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   a.iters = L.iters.as<int32_t>();
   a.nonempty = L.nonempty.as<int32_t>();
   record(L, 1);
-  check_team_timeout(L);
+  L.team_ran = false;
   launch_split<T>(L, *L.corpus, a, n, n_short, true, false, n > 0 ? (double)E / (double)n : 0.0);
   record(L, 2);
   HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.vpad * L.kp, s));  // padded rows stay zero
@@ -512,6 +541,7 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
     HIP_CHECK(hipMemsetAsync(L.small.p, 0, sizeof(double) * (L.k + 1), s));
     HIP_CHECK(hipMemsetAsync(L.stats4.p, 0, sizeof(int64_t) * 4, s));
   }
+  if (L.team_ran) lda::launch_gate_on_timeout(s, L.team_words.as<unsigned>(), L.small.as<double>(), L.k);
   record(L, 3);
 }
 
@@ -649,6 +679,7 @@ void step_ids(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, s
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
   estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1);
   train_tail<T>(L, n, p.E, st);
+  finish_team(L, true, n, p.E);
 }
 
 // sample draw `draw` on the device: per-doc counts (Poisson / Bernoulli), their scans, and (n, E,
@@ -732,6 +763,7 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
   L.pre_draw = draw + 1;
   estep_and_stats<T>(L, n, ns32, E, nullptr, L.iteration + 1);
   train_tail<T>(L, n, E, st);
+  finish_team(L, true, n, E);
 }
 
 template <typename T>
@@ -747,6 +779,7 @@ void estep_only(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0,
   L.timing = false;
   estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1);
   L.timing = t;
+  finish_team(L, false, n, p.E);
   if (gamma_out && n > 0) {
     std::vector<T> g((size_t)(n * L.k));
     HIP_CHECK(hipMemcpyAsync(g.data(), L.gamma.p, sizeof(T) * g.size(), hipMemcpyDeviceToHost, s));
@@ -793,8 +826,9 @@ void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const
   a.gamma = gamma_out ? L.gamma.as<T>() : nullptr;
   a.iters = L.iters.as<int32_t>();
   a.bound = bound ? L.bound.as<double>() : nullptr;
-  check_team_timeout(L);
+  L.team_ran = false;
   launch_split<T>(L, docs, a, n, p.n_short, false, bound, n > 0 ? (double)docs.nnz / (double)n : 0.0);
+  finish_team(L, false, 0, 0);
   if (gamma_out && n > 0) {
     std::vector<T> g((size_t)(n * L.k));
     HIP_CHECK(hipMemcpyAsync(g.data(), L.gamma.p, sizeof(T) * g.size(), hipMemcpyDeviceToHost, s));

@@ -543,7 +543,7 @@ __global__ __launch_bounds__(256) void k_lambda_update(double* __restrict__ lam,
                                                        double rho, double scale, double eta,
                                                        const double* __restrict__ gate,
                                                        double* __restrict__ colpart) {
-  if (gate && gate[0] == 0.0) return;  // Spark: no non-empty docs ⇒ no update
+  if (gate && !(gate[0] > 0.0)) return;  // Spark: no non-empty docs ⇒ no update (< 0: a team timed out)
   __shared__ double s_acc[256];
   const int tid = threadIdx.x;
   const int TW = k < 256 ? k : 256;
@@ -597,7 +597,7 @@ __global__ __launch_bounds__(256) void k_colsum_reduce(const double* __restrict_
                                                        int64_t nblocks, int k,
                                                        const double* __restrict__ gate,
                                                        double* __restrict__ colsum) {
-  if (gate && gate[0] == 0.0) return;
+  if (gate && !(gate[0] > 0.0)) return;
   __shared__ double s[256];
   const int t = blockIdx.x;
   double acc = 0.0;
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(256) void k_expelogbeta(const double* __restrict__ 
                                                      const double* __restrict__ colsum, int64_t V,
                                                      int k, int kp, const double* __restrict__ gate,
                                                      T* __restrict__ Bp, double* __restrict__ logscale) {
-  if (gate && gate[0] == 0.0) return;
+  if (gate && !(gate[0] > 0.0)) return;
   extern __shared__ double s_psic[];
   for (int t = threadIdx.x; t < k; t += 256) s_psic[t] = digamma_fast_d(colsum[t]);
   __syncthreads();
@@ -753,7 +753,7 @@ __global__ __launch_bounds__(256) void k_update_alpha(double* __restrict__ alpha
   extern __shared__ double s_g[];  // gradf[k], q[k]
   __shared__ double s_r[4 * 4];
   const double N = small[k];
-  if (N == 0.0) return;
+  if (!(N > 0.0)) return;
   double* s_q = s_g + k;
   double asum = 0.0, z = 0.0, dz = -INFINITY;
   for (int t = threadIdx.x; t < k; t += 256) asum += alpha[t];
@@ -782,6 +782,14 @@ __global__ __launch_bounds__(256) void k_update_alpha(double* __restrict__ alpha
   block_reduce3(bad, z2, dz3, s_r);
   if (bad == 0.0)
     for (int t = threadIdx.x; t < k; t += 256) alpha[t] += rho * s_g[t];
+}
+
+__global__ void k_gate_on_timeout(const unsigned* __restrict__ tmo, double* __restrict__ small, int k) {
+  if (*tmo) small[k] = -1e300;
+}
+void launch_gate_on_timeout(hipStream_t s, const unsigned* tmo, double* small, int k) {
+  k_gate_on_timeout<<<1, 1, 0, s>>>(tmo, small, k);
+  KERNEL_CHECK();
 }
 
 void launch_update_alpha(hipStream_t s, double* alpha, const double* small, int k, double rho) {

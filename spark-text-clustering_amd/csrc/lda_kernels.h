@@ -112,7 +112,12 @@ struct WideTeam {
   void* xbuf = nullptr;      // [teams][2][P][xstride] 16-byte {epoch, value} granules (zeroed before each launch)
   int64_t xstride = 0;       // granules per member: rows split kp + 1 (s partials, Σ r·φ); topics split
                              // 512 + 2 (φ partials, Σ|Δγ|, Σγ)
+  unsigned spin_limit = 1u << 22;  // polls before a member gives up (a few seconds)
+  int fault_member = -1;     // debug (STC_TEAM_FAULT): this member of team 0 never publishes
 };
+// after the E-step's logphat: a timed-out team poisons the non-empty count (small[k] = −1e300, negative
+// after any all-reduce over ranks), which gates the λ / colsum / expElogβ' / α updates off
+void launch_gate_on_timeout(hipStream_t s, const unsigned* tmo, double* small, int k);
 template <typename T>
 int wide_resident_rows(int k);
 // false: the runtime refused the cooperative grid (nothing launched; the caller runs the one-CU kernel)

@@ -41,6 +41,7 @@ namespace {
 
 constexpr int kW = 4;          // waves per document
 constexpr int kSbPitch = 34;   // s-partial row pitch (doubles): conflict-free 8-B stores, 16-B reads
+constexpr int kPaPitch = 10;   // φ-partial row pitch (doubles): conflict-free 16-B worker reads
 constexpr int kOnChipSets = 6; // row sets the common kernel holds (5 in VGPRs + 1 in LDS)
 constexpr int kMaxSets = 8;    // one worker lane per wave row: 8 row lanes × 8 sets = 64 lanes
 
@@ -58,18 +59,112 @@ using RCommon = RShape<KL, 5, kOnChipSets>;
 template <int KL>
 using RLong = RShape<KL, kMaxSets, kMaxSets>;
 
+// ---- the per-topic ψ/exp chain of the ψ phase, shaped for VALU count: every polynomial in Horner
+// form with its coefficient as the instruction's SGPR operand (a GFX9 VOP3 takes one constant-bus
+// operand), so no constant costs a v_mov pair; branch-free (the shift part is computed for every lane
+// and selected), so the compiler cannot sink it into a divergent branch.  Same Breeze series and
+// truncation fix as stc_internal.h exp_digamma_minus_d; exp() is Cody–Waite + a degree-13 Taylor
+// polynomial in even/odd halves (truncation 4e-18 relative).
+__device__ __forceinline__ double fma_s(double a, double b, double c) {  // a·b + c, c in an SGPR pair
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+  return d;
+}
+__device__ __forceinline__ double fma_sb(double a, double b, double c) {  // a·b + c, b in an SGPR pair
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ double mul_s(double a, double b) {
+  double d;
+  asm("v_mul_f64 %0, %1, %2" : "=v"(d) : "v"(a), "s"(b));
+  return d;
+}
+__device__ __forceinline__ double add_s(double a, double b) {
+  double d;
+  asm("v_add_f64 %0, %1, %2" : "=v"(d) : "v"(a), "s"(b));
+  return d;
+}
+__device__ __forceinline__ double sub_s(double b, double a) {  // b − a, b in an SGPR pair
+  double d;
+  asm("v_add_f64 %0, -%1, %2" : "=v"(d) : "v"(a), "s"(b));
+  return d;
+}
+// Breeze's truncation term E(y) = f⁹·P(f), f = 1/y² (tools/fit_breeze_digamma.py)
+__device__ __forceinline__ double trunc_f(double f) {
+  double a = add_s(mul_s(f, -12318.55039822477), 2372.137971404805);
+  a = fma_s(a, f, -260.94994774566294);
+  a = fma_s(a, f, 26.284421368293753);
+  a = fma_s(a, f, -3.053401198888146);
+  const double f2 = f * f, f4 = f2 * f2;
+  return ((f4 * f4) * f) * a;
+}
+__device__ __forceinline__ double exp_digamma_minus_s(double x, double cst) {
+  const bool sh = x <= 5.0;
+  const double xs = sh ? x : 1.0;
+  // Σ_{i<6} 1/(xs+i) = p/q, q = xs(xs+1)…(xs+5)
+  double q = fma_s(add_s(xs, 15.0), xs, 85.0);
+  q = fma_s(q, xs, 225.0);
+  q = fma_s(q, xs, 274.0);
+  q = fma_s(q, xs, 120.0) * xs;
+  double p = fma_s(add_s(mul_s(xs, 6.0), 75.0), xs, 340.0);
+  p = fma_s(p, xs, 675.0);
+  p = fma_s(p, xs, 548.0);
+  p = fma_s(p, xs, 120.0);
+  const double iq = rcp_nr(q);
+  double c = p * iq;
+  c = fma(fma(-q, c, p), iq, c);
+  const double y = sh ? add_s(x, 6.0) : x;
+  const double iy = rcp_nr(y);
+  const double f = iy * iy;
+  double t = add_s(mul_s(f, 3617.0 / 8160.0), -1.0 / 12.0);
+  t = fma_s(t, f, 691.0 / 32760.0);
+  t = fma_s(t, f, -1.0 / 132.0);
+  t = fma_s(t, f, 1.0 / 240.0);
+  t = fma_s(t, f, -1.0 / 252.0);
+  t = fma_s(t, f, 1.0 / 120.0);
+  t = fma_s(t, f, -1.0 / 12.0) * f;
+  const double yb = xs + (floor(sub_s(5.0, xs)) + 1.0);  // Breeze's y ∈ (5, 6] (E needs ~1e-4 relative)
+  const double rb = __builtin_amdgcn_rcp(yb);
+  const double fix = trunc_f(f) - trunc_f(rb * rb);
+  const double shift = sh ? fix - c : 0.0;
+  const double z = ((shift - 0.5 * iy) + t) - cst;
+  // exp(z): n = rint(z / ln2), r = z − n·ln2 (hi/lo), e^r = E(r²) + r·O(r²)
+  const double n = __builtin_rint(mul_s(z, 1.4426950408889634));
+  double r = fma_sb(n, -6.93147180369123816490e-01, z);
+  r = fma_sb(n, -1.90821492927058770002e-10, r);
+  const double r2 = r * r;
+  double e = add_s(mul_s(r2, 1.0 / 479001600.0), 1.0 / 3628800.0);
+  e = fma_s(e, r2, 1.0 / 40320.0);
+  e = fma_s(e, r2, 1.0 / 720.0);
+  e = fma_s(e, r2, 1.0 / 24.0);
+  e = fma(e, r2, 0.5);
+  e = fma(e, r2, 1.0);
+  double o = add_s(mul_s(r2, 1.0 / 6227020800.0), 1.0 / 39916800.0);
+  o = fma_s(o, r2, 1.0 / 362880.0);
+  o = fma_s(o, r2, 1.0 / 5040.0);
+  o = fma_s(o, r2, 1.0 / 120.0);
+  o = fma_s(o, r2, 1.0 / 6.0);
+  o = fma(o, r2, 1.0);
+  const double ez = __builtin_ldexp(fma(r, o, e), (int)fmax(n, -1100.0));  // n < -1100: 0
+  return y * ez;
+}
+
 template <class S>
 struct RLds {
   double eth[8][S::KLP] __attribute__((aligned(16)));  // eθ, topic t at [t / KL][t % KL]
   double gam[S::KT];               // γ
-  double dgv[128];                 // |Δγ| of the last update per topic (0 past kp): Σ → the stop rule
-  double2 rowce[kW][8 * S::RMAX] __attribute__((aligned(16)));  // per (wave, wave row): {cts, 2^53·ε'}
+  double rrow[kW][8 * S::RMAX];    // r = cts/φ per (wave, wave row)
+  double dsum[2];                  // Σ|Δγ| of the last update per ψ wave
   double esum[kW] __attribute__((aligned(16)));  // Σ r·ε' over a wave's rows (0 unless an ε' is visible)
   double part[kW][4];              // per-wave partial sums (init: Σγ₀, Σα, Σcts; end: Σγ, bound terms)
   double cs;                       // ψ(Σγ') of the current eθ (the bound's scale)
   union {
-    double sb[S::KT][kSbPitch];            // s partials (topic, row lane 8·w + rl)
-    double stage[kW][8][S::KT + 2];        // load phase: eight B rows per wave at a time
+    struct {
+      double pa[kW][8 * S::RMAX][kPaPitch];  // φ partials (wave, wave row, topic lane)
+      double sb[S::KT][kSbPitch];            // s partials (topic, row lane 8·w + rl)
+    } l;
+    double stage[kW][8][S::KT + 2];          // load phase: eight B rows per wave at a time
   } u __attribute__((aligned(16)));
   double ovf[S::NOVF > 0 ? S::NOVF * kW * S::KL * 64 : 1];  // row sets past RREG ([set][w][p][lane])
 };
@@ -94,27 +189,17 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
   const int ttl = tt / KL, ttp = tt - ttl * KL;
   const double alp = town ? a.alpha[tt] : 0.0;
 
-  // ---- this lane's rows n = 32·j + 8·w + rl: ids, counts, ε' (the topic-lane-0 copy goes to LDS)
-  int ids[R];
-  double ct = 0.0;
-  bool any = false;
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-    const int n = 32 * j + 8 * w + rl;
-    const bool v = n < nnz;
-    const int64_t e = v ? s0 + n : 0;
-    ids[j] = v ? a.indices[e] : 0;
-    const double c = v ? a.values[e] : 0.0;
-    any |= c != 0.0;
-    ct += c;
-    if (tl == 0) {
-      // ε'_n = 1e-100·e^{-m_v} held as 2^53·ε' (the test 2^53·ε' ≥ φ is then direct), capped at 1e300
-      // where e^{-m_v} overflows (Spark's unscaled row is 0 there; r ≈ cts·1e-284 reproduces that).
-      // Padding rows hold −2^53 (φ = −1, r = −0, never live).
-      const double e2 = v ? fmin(0x1p53 * exp(kLogEps - a.logscale[ids[j]]), 1e300) : -0x1p53;
-      sm.rowce[w][8 * j + rl] = make_double2(c, e2);
-    }
-  }
+  // ---- worker lane: wave row q = lane (set q >> 3, row lane q & 7) → document row qn
+  const int qn = 32 * (lane >> 3) + 8 * w + (lane & 7);
+  const bool wv = lane < 8 * R && qn < nnz;
+  const int64_t qe = wv ? s0 + qn : 0;
+  const int qid = wv ? a.indices[qe] : 0;
+  const double qc = wv ? a.values[qe] : 0.0;
+  const double qls = a.logscale[qid];
+  // ε'_q = 1e-100·e^{-m_v} held as 2^53·ε' (the test 2^53·ε' ≥ φ is then direct), capped at 1e300
+  // where e^{-m_v} overflows (Spark's unscaled row is 0 there; r ≈ cts·1e-284 reproduces that).
+  // Padding rows hold −2^53 (φ = −1, r = −0, never live).
+  const double qe2 = wv ? fmin(0x1p53 * exp(kLogEps - qls), 1e300) : -0x1p53;
 
   // ---- B rows, coalesced: per row set the wave copies its eight rows (kp doubles each) with
   // 16-byte loads, stages them in LDS and every lane picks up its (row lane, topic lane) part
@@ -137,7 +222,7 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
         for (int i = 0; i < NP; ++i) {
           const int c = lane + 64 * i;
           const int srow = c / C2, q = c - srow * C2;
-          const int id = __builtin_amdgcn_ds_bpermute((8 * (srow & 7)) << 2, ids[j]);  // row lane srow
+          const int id = __builtin_amdgcn_ds_bpermute((8 * j + (srow & 7)) << 2, qid);  // its worker lane
           const bool keep = c < 8 * C2 && 32 * j + 8 * w + srow < nnz;
           const double2 x = *reinterpret_cast<const double2*>(a.Bp + (int64_t)(keep ? id : 0) * kp + 2 * (keep ? q : 0));
           pc[jj][i] = keep ? x : make_double2(0.0, 0.0);
@@ -166,7 +251,7 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
     }
   }
 
-  // ---- γ₀ / α partials (the first npsi waves hold the topics), Σcts, eθ and |Δγ| pads
+  // ---- γ₀ / α partials (the first npsi waves hold the topics), Σcts, eθ pads
   double g0 = 0.0;
   if (w < npsi) {
     if (town) {
@@ -180,16 +265,15 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
     if (tval) sm.gam[tt] = g0;
   }
   for (int i = threadIdx.x; i < 8 * KLP; i += 64 * kW) (&sm.eth[0][0])[i] = 0.0;
-  if (threadIdx.x < 128) sm.dgv[threadIdx.x] = 0.0;
   {
-    const double gs = wave_sum_d(g0), as = wave_sum_d(alp), cts = wave_sum_d(tl == 0 ? ct : 0.0);
+    const double gs = wave_sum_d(g0), as = wave_sum_d(alp), cts = wave_sum_d(qc);
     if (lane == 0) {
       sm.part[w][0] = w < npsi ? gs : 0.0;
       sm.part[w][1] = w < npsi ? as : 0.0;
       sm.part[w][2] = cts;
     }
   }
-  const bool nonempty = __syncthreads_or(any) != 0;  // (also publishes γ₀, rowce and the partials)
+  const bool nonempty = __syncthreads_or(wv && qc != 0.0) != 0;  // (also publishes γ₀ and the partials)
   const double gsum0 = (sm.part[0][0] + sm.part[1][0]) + (sm.part[2][0] + sm.part[3][0]);
   const double asum = (sm.part[0][1] + sm.part[1][1]) + (sm.part[2][1] + sm.part[3][1]);
   const double ctot = (sm.part[0][2] + sm.part[1][2]) + (sm.part[2][2] + sm.part[3][2]);
@@ -214,24 +298,21 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
   const double cs_flat = digamma_fast_d(asum + ctot);
   {
     const double cs0 = digamma_fast_d(gsum0);
-    if (w < npsi && town) sm.eth[ttl][ttp] = exp_digamma_minus_fast(g0, cs0);
+    if (w < npsi && town) sm.eth[ttl][ttp] = exp_digamma_minus_s(g0, cs0);
     if (threadIdx.x == 0) sm.cs = cs0;
   }
   __syncthreads();
 
-  double* const sb = &sm.u.sb[0][0];
-  double rr[R], dt[R];  // r = cts/φ and φ without ε' of the lane's rows (final values are the outputs)
+  double* const pa = &sm.u.l.pa[w][0][0];
+  double* const sb = &sm.u.l.sb[0][0];
+  double rr[R];
+  double qdt = 0.0, qr = 0.0;  // worker: φ without ε', r of its row (final values are the outputs)
+  double dsum = 0.0;
   int it = 0;
   STAMP(0);  // loads, γ₀, first eθ, two barriers
   while (true) {
-    // Σ|Δγ| of the last update (Spark: meanGammaChange = Σ|Δγ| / k), every wave from the same LDS
-    // values in the same order, so the stop decision is block-uniform; reads issued with eθ's
-    const double dg2 = sm.dgv[lane] + sm.dgv[lane + 64];
-    double2 ce[R];
-#pragma unroll
-    for (int j = 0; j < R; ++j) ce[j] = sm.rowce[w][8 * j + rl];
-    // Phase A: φ over the lane's KL topics, then all-reduced over the row's eight topic lanes
-    // (xor-1, xor-2, mirror-8 butterfly; a + b == b + a, so all eight lanes hold identical bits)
+    // Phase A: φ partials over the lane's KL topics; worker lane q (one per wave row) adds the eight
+    // topic lanes' partials in a fixed order, forms r_q = cts/φ once and publishes it (wave-local LDS)
     {
       double acc[R];
 #pragma unroll
@@ -246,31 +327,32 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
         }
       }
 #pragma unroll
-      for (int j = 0; j < R; ++j) acc[j] += dpp_d<DPP_QP_1032>(acc[j]);
-#pragma unroll
-      for (int j = 0; j < R; ++j) acc[j] += dpp_d<DPP_QP_2301>(acc[j]);
-#pragma unroll
-      for (int j = 0; j < R; ++j) dt[j] = acc[j] + dpp_d<DPP_ROW_HALF_MIRROR>(acc[j]);
+      for (int j = 0; j < R; ++j) pa[(8 * j + rl) * kPaPitch + tl] = acc[j];
     }
-    STAMP(1);  // eθ reads, φ FMAs, the topic-lane all-reduce
+    STAMP(1);  // eθ reads, φ FMAs, partial stores
+    __builtin_amdgcn_wave_barrier();
     bool live = false;
-    double ev = 0.0;
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const double ph = fma(ce[j].y, 0x1p-53, dt[j]);
-      rr[j] = ce[j].x * rcp_nr(ph);
-      live |= ce[j].y >= ph;  // ε' visible at fp64 resolution
-      ev = fma(rr[j], ce[j].y * 0x1p-53, ev);
+    if (lane < 8 * R) {
+      const double2* const pr = reinterpret_cast<const double2*>(pa + lane * kPaPitch);
+      const double2 x0 = pr[0], x1 = pr[1], x2 = pr[2], x3 = pr[3];
+      qdt = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
+      const double ph = fma(qe2, 0x1p-53, qdt);
+      qr = qc * rcp_nr(ph);
+      live = qe2 >= ph;  // ε' visible at fp64 resolution
+      sm.rrow[w][lane] = qr;
     }
-    const double dsum = wave_sum_d(dg2);
     if (__builtin_amdgcn_ballot_w64(live) != 0) {
-      const double e = wave_sum_d(tl == 0 ? ev : 0.0);  // each row once (topic lane 0)
+      const double e = wave_sum_d(lane < 8 * R ? qr * (qe2 * 0x1p-53) : 0.0);
       if (lane == 0) sm.esum[w] = e;
     } else if (lane == 0) {
       sm.esum[w] = 0.0;
     }
-    STAMP(2);  // r, ε' ballot, Σ|Δγ|
-    // Spark: while (meanGammaChange > 1e-3)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < R; ++j) rr[j] = sm.rrow[w][8 * j + rl];
+    STAMP(2);  // worker sums, r, ε' ballot, r reads
+    // Spark: while (meanGammaChange > 1e-3); dsum is block-uniform (every wave adds the same LDS
+    // values in the same order)
     if ((it > 0 && dsum <= a.stop_thr) || it >= a.max_iter) break;
 
     // Phase B: s partials over the lane's R rows, one row lane's slot per topic
@@ -286,36 +368,37 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
     STAMP(4);  // barrier 1
     const bool psi = npsi == 2 ? ((w >> 1) == (it & 1)) : (w == (it & 3));
     if (psi) {
+      double dg = 0.0;
       if (town) {
-        // the phase's LDS reads in two batches (16 partials each, with γ, eθ and the ε' sums)
+        // every LDS read of the phase issued together: the 32 partials, γ, eθ, the four ε' sums
         const double2* const sp = reinterpret_cast<const double2*>(sb + tt * kSbPitch);
+        double2 xs[16];
+#pragma unroll
+        for (int h = 0; h < 16; ++h) xs[h] = sp[h];
         const double g = sm.gam[tt], eo = sm.eth[ttl][ttp];
         const double2 e01 = *reinterpret_cast<const double2*>(&sm.esum[0]);
         const double2 e23 = *reinterpret_cast<const double2*>(&sm.esum[2]);
         double c4[4];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          double2 xs[8];
-#pragma unroll
-          for (int h = 0; h < 8; ++h) xs[h] = sp[8 * b + h];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const double2 x0 = xs[4 * h], x1 = xs[4 * h + 1], x2 = xs[4 * h + 2], x3 = xs[4 * h + 3];
-            c4[2 * b + h] = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
-          }
+        for (int h = 0; h < 4; ++h) {
+          const double2 x0 = xs[4 * h], x1 = xs[4 * h + 1], x2 = xs[4 * h + 2], x3 = xs[4 * h + 3];
+          c4[h] = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
         }
         const double s = (c4[0] + c4[1]) + (c4[2] + c4[3]);
         const double et = (e01.x + e01.y) + (e23.x + e23.y);
         const double csn = et != 0.0 ? digamma_fast_d(asum + ctot - et) : cs_flat;
         const double gn = fma(eo, s, alp);  // γ ← eθ ⊙ s + α
-        sm.dgv[tt] = fabs(gn - g);
+        dg = fabs(gn - g);
         sm.gam[tt] = gn;
-        sm.eth[ttl][ttp] = exp_digamma_minus_fast(gn, csn);
+        sm.eth[ttl][ttp] = exp_digamma_minus_s(gn, csn);
         if (tt == 0) sm.cs = csn;
       }
+      const double d = wave_sum_d(dg);
+      if (lane == 0) sm.dsum[pw] = d;
     }
     STAMP(psi ? 5 : 8);  // ψ phase (ψ waves; non-ψ waves: nothing)
-    __syncthreads();  // (2) eθ, γ, |Δγ| published
+    __syncthreads();  // (2) eθ, γ, Σ|Δγ| published
+    dsum = npsi == 2 ? sm.dsum[0] + sm.dsum[1] : sm.dsum[0];
     STAMP(psi ? 6 : 9);  // barrier 2 (ψ waves / the others)
     ++it;
   }
@@ -326,16 +409,9 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
   {
     const double gs = wave_sum_d(gfin);
     double bt = 0.0, bc = 0.0;
-    if (BOUND && tl == 0) {
-#pragma unroll
-      for (int j = 0; j < R; ++j) {
-        const int n = 32 * j + 8 * w + rl;
-        const double c = sm.rowce[w][8 * j + rl].x;
-        if (n < nnz && c != 0.0) {
-          bt += c * (log(fmax(dt[j], 0x1p-1074)) + a.logscale[a.indices[s0 + n]]);
-          bc += c;
-        }
-      }
+    if (BOUND && wv && qc != 0.0) {
+      bt = qc * (log(fmax(qdt, 0x1p-1074)) + qls);
+      bc = qc;
     }
     if (BOUND) {
       bt = wave_sum_d(bt);
@@ -360,17 +436,11 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
     }
     if (STATS && tval) a.eth[slot * kp + tt] = sm.eth[ttl][ttp];  // the eθ the final φ used
   }
-  if (tl == 0) {
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const int n = 32 * j + 8 * w + rl;
-      if (n < nnz) {
-        a.r[e0 + n] = rr[j];
-        if (STATS) {
-          a.keys[e0 + n] = (uint32_t)a.indices[s0 + n];
-          a.vals[e0 + n] = entry_val<double>(slot, e0 + n, rr[j]);
-        }
-      }
+  if (wv) {
+    a.r[e0 + qn] = qr;
+    if (STATS) {
+      a.keys[e0 + qn] = (uint32_t)qid;
+      a.vals[e0 + qn] = entry_val<double>(slot, e0 + qn, qr);
     }
   }
   if (threadIdx.x == 0) {

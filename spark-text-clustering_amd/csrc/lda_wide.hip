@@ -546,7 +546,6 @@ __device__ __forceinline__ T ld_sc1(const T* p) {
     return __builtin_bit_cast(T, __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-constexpr unsigned kSpinLimit = 1u << 22;  // a few seconds of polling: far past any legitimate wait
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kSc1 = 16;  // buffer aux bit: sc1 (write-through store / L1-bypassing load)
@@ -556,19 +555,22 @@ __device__ __forceinline__ void put_granule(__amdgpu_buffer_rsrc_t rs, int idx, 
   unsigned long long bits;
   if constexpr (sizeof(T) == 8) bits = __builtin_bit_cast(unsigned long long, v);
   else bits = __builtin_bit_cast(unsigned int, v);
-  const u32x4 g = {epoch, 0u, (unsigned)bits, (unsigned)(bits >> 32)};
+  // the epoch in both 8-byte halves: a reader takes the granule only when both tags match, so a
+  // store whose halves become visible at different times is re-polled, never consumed torn (the
+  // memory model guarantees single-copy atomicity up to 64 bits only)
+  const u32x4 g = {epoch, (unsigned)bits, epoch, (unsigned)(bits >> 32)};
   __builtin_amdgcn_raw_buffer_store_b128(g, rs, idx * 16, 0, kSc1);
 }
 template <typename T>
 __device__ __forceinline__ bool get_granule(__amdgpu_buffer_rsrc_t rs, int idx, unsigned epoch, T& v) {
   const u32x4 g = __builtin_amdgcn_raw_buffer_load_b128(rs, idx * 16, 0, kSc1);
-  const unsigned long long bits = ((unsigned long long)g.w << 32) | g.z;
+  const unsigned long long bits = ((unsigned long long)g.w << 32) | g.y;
   if constexpr (sizeof(T) == 8) v = __builtin_bit_cast(T, bits);
   else v = __builtin_bit_cast(T, (unsigned)bits);
-  return g.x == epoch;
+  return g.x == epoch && g.z == epoch;
 }
-__device__ __forceinline__ bool spin_give_up(unsigned spins, unsigned* tmo) {
-  if (spins < kSpinLimit &&
+__device__ __forceinline__ bool spin_give_up(unsigned spins, unsigned* tmo, unsigned limit) {
+  if (spins < limit &&
       __hip_atomic_load((gu32*)tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
     return false;
   __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -589,6 +591,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = (int)blockIdx.x, il = b / 8;
   const int member = il % P, team = (il / P) * 8 + (b % 8), nteams = (int)gridDim.x / P;
+  const bool pub = !(team == 0 && member == wt.fault_member);  // debug: a member that never publishes
   // this team's granules [parity][member][xstride], 16 B each
   const int team_granules = 2 * P * (int)wt.xstride;
   unsigned char* const xb = reinterpret_cast<unsigned char*>(wt.xbuf) + (int64_t)team * team_granules * 16;
@@ -789,8 +792,8 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
       const int base = (int)(epoch & 1) * P * (int)wt.xstride;
 #pragma unroll
       for (int q = 0; q < Q; ++q)
-        if (t0 + q < kp) put_granule<T>(rs, base + member * (int)wt.xstride + t0 + q, epoch, s[q]);
-      if (tid == 0) put_granule<T>(rs, base + member * (int)wt.xstride + kp, epoch, sgl);
+        if (pub && t0 + q < kp) put_granule<T>(rs, base + member * (int)wt.xstride + t0 + q, epoch, s[q]);
+      if (pub && tid == 0) put_granule<T>(rs, base + member * (int)wt.xstride + kp, epoch, sgl);
       T st[Q];
       T sg = T(0);
 #pragma unroll
@@ -825,7 +828,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
             if (t0 + q < kp) ok &= get_granule<T>(rs, g0 + t0 + q, epoch, v[q]);
           }
           if (__all(ok)) break;
-          if (spin_give_up(spins, wt.tmo)) {
+          if (spin_give_up(spins, wt.tmo, wt.spin_limit)) {
             if (lane == 0) s_abort = 1;
             break;
           }
@@ -915,6 +918,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = (int)blockIdx.x, il = b / 8;
   const int member = il % P, team = (il / P) * 8 + (b % 8), nteams = (int)gridDim.x / P;
+  const bool pub_ok = !(team == 0 && member == wt.fault_member);  // debug: a member that never publishes
   const int team_granules = 2 * P * (int)wt.xstride;
   unsigned char* const xb = reinterpret_cast<unsigned char*>(wt.xbuf) + (int64_t)team * team_granules * 16;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(xb, 0, team_granules * 16, 0x00020000);
@@ -927,7 +931,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
   // over the team (every lane of a wave takes part in the poll; `need` = this lane reads the slot)
   auto exchange = [&](int idx, T mine, bool pub, bool need) -> T {
     const int base = (int)(epoch & 1) * P * (int)wt.xstride;
-    if (pub) put_granule<T>(rs, base + member * (int)wt.xstride + idx, epoch, mine);
+    if (pub && pub_ok) put_granule<T>(rs, base + member * (int)wt.xstride + idx, epoch, mine);
     T sum = T(0);
     for (int m = 0; m < P; ++m) {
       T v = T(0);
@@ -937,7 +941,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
         for (unsigned spins = 0;; ++spins) {
           const bool ok = !need || get_granule<T>(rs, base + m * (int)wt.xstride + idx, epoch, v);
           if (__all(ok)) break;
-          if (spin_give_up(spins, wt.tmo)) {
+          if (spin_give_up(spins, wt.tmo, wt.spin_limit)) {
             if (lane == 0) s_abort = 1;
             break;
           }
@@ -1104,8 +1108,8 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
       {
         const int base = (int)(epoch & 1) * P * (int)wt.xstride;
         const bool row = tid < nnz;
-        if (row) put_granule<T>(rs, base + member * (int)wt.xstride + tid, epoch, dotp);
-        if (tid == 0) put_granule<T>(rs, base + member * (int)wt.xstride + GD, epoch, dsp);
+        if (pub_ok && row) put_granule<T>(rs, base + member * (int)wt.xstride + tid, epoch, dotp);
+        if (pub_ok && tid == 0) put_granule<T>(rs, base + member * (int)wt.xstride + GD, epoch, dsp);
         for (int m = 0; m < P; ++m) {
           T v = T(0), w = T(0);
           if (m == member) {
@@ -1116,7 +1120,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
               bool ok = get_granule<T>(rs, base + m * (int)wt.xstride + GD, epoch, w);
               if (row) ok &= get_granule<T>(rs, base + m * (int)wt.xstride + tid, epoch, v);
               if (__all(ok)) break;
-              if (spin_give_up(spins, wt.tmo)) {
+              if (spin_give_up(spins, wt.tmo, wt.spin_limit)) {
                 if (lane == 0) s_abort = 1;
                 break;
               }

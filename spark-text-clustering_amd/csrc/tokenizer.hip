@@ -8,14 +8,14 @@
 // The reference's own CoreNLP/OpenNLP front-end (LDAClustering.scala:116-139) stays out of scope.
 //
 // Lower-casing as Java 8's String.toLowerCase (root locale) — the JVM Spark 2.4.3 runs on — for every
-// code point with a two-byte or shorter UTF-8 form: ASCII, Latin-1 (U+00C0–U+00DE except ×) and,
-// through the generated table case_table.h, U+0100–U+07FF (Latin Extended-A/B, IPA, Greek and Coptic,
-// Cyrillic + Supplement, Armenian, and the caseless Hebrew/Arabic/Syriac/Thaana/NKo blocks).  All of
-// these keep the UTF-8 length, so output byte i is a function of input bytes i−1, i, i+1.  Characters
-// whose Java mapping is not such a map (U+0130 İ, U+03A3 Σ with its Final_Sigma context rule, U+023A,
-// U+023E) and three-byte/four-byte code points outside the caseless blocks U+2000–U+20BF (punctuation,
-// quotes, dashes, currency), U+3000–U+9FFF (CJK) and U+1F000–U+1FFFF (emoji) are REJECTED loudly
-// (STC_ERR_INVALID_ARG with the byte position), never silently mis-cased.
+// code point: ASCII inline, the BMP through the generated two-level table case_table.h (Unicode 6.2
+// semantics: characters assigned later pass through, as Java 8 leaves them), Deseret (the one cased
+// supplementary block in 6.2) inline, everything else passed through.  Every mapping kept keeps its
+// UTF-8 length, so output byte i is a function of the character that contains byte i.  Characters whose
+// Java mapping is not such a map (U+0130 İ → "i̇", U+03A3 Σ with its Final_Sigma context rule, and the
+// capitals whose lower case changes UTF-8 length: U+023A/U+023E, U+1E9E ẞ, U+2126 Ω, U+212A K, U+212B Å,
+// U+2C62…, U+A78D, U+A7AA — 18 code points) are REJECTED loudly (STC_ERR_INVALID_ARG with the byte
+// position), never silently mis-cased.
 //
 // Layout: in = one UTF-8 blob + int64 text offsets per document.  Out = the lower-cased blob with
 // the separator bytes removed, so token t is the contiguous out[tok_off[t] .. tok_off[t+1]) and
@@ -38,27 +38,61 @@ __device__ __forceinline__ bool is_java_space(uint32_t b) {
   return b == 0x20u || (b >= 0x09u && b <= 0x0Du);  // \t \n \x0B \f \r and ' '
 }
 
-// the two-byte code point whose lead byte is b (0xC4–0xDF) and continuation byte c
-__device__ __forceinline__ uint32_t cp2(uint32_t b, uint32_t c) { return ((b & 0x1Fu) << 6) | (c & 0x3Fu); }
+// UTF-8 length from the lead byte (0: a continuation byte)
+__device__ __forceinline__ int utf8_len(uint32_t b) { return b < 0x80u ? 1 : b < 0xC0u ? 0 : b < 0xE0u ? 2 : b < 0xF0u ? 3 : 4; }
 
-// true when the UTF-8 lead byte `b` (followed by `nx`) starts a code point outside the supported set
-__device__ __forceinline__ bool unsupported(uint32_t b, uint32_t nx) {
-  if (b < 0xC4u) return false;                           // ASCII, continuation, U+0080–U+00FF
-  if (b <= 0xDFu) return kLower2[cp2(b, nx) - kCaseLo] == 0;  // U+0100–U+07FF: the table's rejects
-  if (b == 0xE2u) return nx < 0x80u || nx > 0x82u;       // U+2000–U+20BF only
-  if (b >= 0xE3u && b <= 0xE9u) return false;            // U+3000–U+9FFF
-  if (b == 0xF0u) return nx != 0x9Fu;                    // U+1F000–U+1FFFF only
-  return true;
+// Java 8 lower case of a BMP code point (0: rejected — see case_table.h)
+__device__ __forceinline__ uint32_t lower_bmp(uint32_t cp) {
+  const uint32_t pg = kCasePage[cp >> 8];
+  return pg ? kCasePages[pg - 1][cp & 0xFFu] : cp;
+}
+// ... of any code point: the BMP table, Deseret U+10400–U+10427 → +0x28, the rest unchanged
+__device__ __forceinline__ uint32_t lower_cp(uint32_t cp) {
+  if (cp < 0x10000u) return lower_bmp(cp);
+  return (cp >= 0x10400u && cp <= 0x10427u) ? cp + 0x28u : cp;
+}
+// the code point of the n-byte UTF-8 sequence at text[j] (j + n <= e), or ~0 when malformed
+__device__ __forceinline__ uint32_t decode_at(const uint8_t* __restrict__ text, int64_t j, int n) {
+  uint32_t cp = text[j] & (0xFFu >> (n + 1));
+  for (int q = 1; q < n; ++q) {
+    const uint32_t c = text[j + q];
+    if ((c & 0xC0u) != 0x80u) return ~0u;
+    cp = (cp << 6) | (c & 0x3Fu);
+  }
+  return cp;
+}
+// byte `pos` (0 = lead) of code point cp's n-byte UTF-8 form
+__device__ __forceinline__ uint32_t utf8_byte(uint32_t cp, int n, int pos) {
+  if (pos == 0) return n == 2 ? (0xC0u | (cp >> 6)) : n == 3 ? (0xE0u | (cp >> 12)) : (0xF0u | (cp >> 18));
+  return 0x80u | ((cp >> (6 * (n - 1 - pos))) & 0x3Fu);
 }
 
-// output byte for input byte b between prev and nx (same-length mappings only, see the header)
-__device__ __forceinline__ uint32_t to_lower(uint32_t b, uint32_t prev, uint32_t nx) {
-  if (b >= 0x41u && b <= 0x5Au) return b + 0x20u;                                // A–Z
-  if (prev == 0xC3u && b >= 0x80u && b <= 0x9Eu && b != 0x97u) return b + 0x20u;  // À–Þ except ×
-  if (b >= 0xC4u && b <= 0xDFu) return 0xC0u | (kLower2[cp2(b, nx) - kCaseLo] >> 6);       // lead byte
-  if (prev >= 0xC4u && prev <= 0xDFu && (b & 0xC0u) == 0x80u)                                // its tail
-    return 0x80u | (kLower2[cp2(prev, b) - kCaseLo] & 0x3Fu);
-  return b;
+// true when the lead byte at text[i] starts a character the kernel must reject (see the header)
+__device__ __forceinline__ bool unsupported_at(const uint8_t* __restrict__ text, int64_t i, int64_t e) {
+  const int n = utf8_len(text[i]);
+  if (n < 2 || n > 3 || i + n > e) return false;  // ASCII, continuation, 4-byte, truncated: pass through
+  const uint32_t cp = decode_at(text, i, n);
+  return cp != ~0u && lower_bmp(cp) == 0u;
+}
+
+// output byte for input byte b = text[i] of the document [s, e) (same-length mappings only)
+__device__ __forceinline__ uint32_t to_lower_at(const uint8_t* __restrict__ text, int64_t s, int64_t e, int64_t i,
+                                                uint32_t b) {
+  if (b < 0x80u) return (b >= 0x41u && b <= 0x5Au) ? b + 0x20u : b;  // ASCII: A–Z
+  // the character holding byte i: its lead at i − pos (malformed sequences pass through unchanged)
+  int pos = 0;
+  int64_t j = i;
+  while (utf8_len(text[j]) == 0) {
+    if (pos == 3 || j == s) return b;
+    --j;
+    ++pos;
+  }
+  const int n = utf8_len(text[j]);
+  if (n < 2 || pos >= n || j + n > e) return b;
+  const uint32_t cp = decode_at(text, j, n);
+  if (cp == ~0u) return b;
+  const uint32_t lc = lower_cp(cp);
+  return lc == 0u ? b : utf8_byte(lc, n, pos);
 }
 
 __device__ __forceinline__ int64_t lanes_below(uint64_t m, int lane) {
@@ -87,10 +121,7 @@ __global__ __launch_bounds__(64 * kWaves) void k_count(const uint8_t* __restrict
         const bool in = i >= s && i < e;
         const uint32_t b = (word >> (8 * j)) & 0xFFu;
         const bool sep = is_java_space(b);
-        if (in && b >= 0xC4u) {
-          const uint32_t nx = (i + 1 < e) ? text[i + 1] : 0u;
-          if (unsupported(b, nx)) atomicMin(bad, (unsigned long long)i);
-        }
+        if (in && b >= 0xC4u && unsupported_at(text, i, e)) atomicMin(bad, (unsigned long long)i);
         const uint64_t sm = __ballot(in && sep), km = __ballot(in && !sep);
         seps += __popcll(sm);
         if (km) {
@@ -130,13 +161,11 @@ __global__ __launch_bounds__(64 * kWaves) void k_emit(const uint8_t* __restrict_
       const int64_t i = c + lane;
       const bool in = i < e;
       const uint32_t b = in ? text[i] : 0x20u;
-      const uint32_t prev = (in && i > s) ? text[i - 1] : 0u;
-      const uint32_t nx = (in && i + 1 < e) ? text[i + 1] : 0x80u;  // (validated by k_count)
       const bool sep = is_java_space(b);
       const uint64_t sm = __ballot(in && sep);
       const int64_t j = seps + lanes_below(sm, lane);  // separators before byte i in this doc
       if (in) {
-        if (!sep) out[base + (i - s) - j] = (uint8_t)to_lower(b, prev, nx);
+        if (!sep) out[base + (i - s) - j] = (uint8_t)to_lower_at(text, s, e, i, b);
         else if (j + 1 < nt) tok_off[tb + j + 1] = base + (i - s) - j;
       }
       seps += __popcll(sm);

@@ -102,6 +102,7 @@ SIGNATURES = {
     "stc_lda_get_alpha": (_int, [_p, _pdbl]),
     "stc_lda_get_eta": (_int, [_p, _pdbl]),
     "stc_lda_get_iteration": (_int, [_p, _pi64]),
+    "stc_lda_shape": (_int, [_p, _pi32, _pi64]),
     "stc_lda_step": (_int, [_p, _pi64, _i64, _pdbl, C.POINTER(StepStats)]),
     "stc_lda_next": (_int, [_p, C.POINTER(StepStats)]),
     "stc_lda_estep": (_int, [_p, _pi64, _i64, _pdbl, _pdbl, _pdbl, _pi32]),

@@ -36,6 +36,7 @@ import numpy as np
 
 REF = "/root/reference/TextClustering/src/main/resources"
 OUT = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(OUT))
 
 
 def _read_table(d):
@@ -178,20 +179,20 @@ def make_vocab():
     print(f"en_vocab.txt: {len(vocab)} terms")
 
 
-def _kernel_supported(ch):
-    """The tokenizer kernel's accepted set (tokenizer.hip header): U+0000–U+07FF except the four
-    rejected capitals, and the caseless blocks U+2000–U+20BF, U+3000–U+9FFF, U+1F000–U+1FFFF."""
-    o = ord(ch)
-    if o < 0x800:
-        return o not in (0x130, 0x3A3, 0x23A, 0x23E)
-    return 0x2000 <= o <= 0x20BF or 0x3000 <= o <= 0x9FFF or 0x1F000 <= o <= 0x1FFFF
+# the lines of the reference's books that the round-2 kernel rejected (Greek Extended, U+2116 "№"):
+# one slice around each goes into the fixture as well
+TARGET_LINES = [("English", "Walden - Henry David Thoreau.txt", 1593),
+                ("Russian", "2012 20 eink - Unknown.txt", 141),
+                ("Russian", "Adiutant iegho prievoskhoditiel'stva - Vladimir Galaktionovich Korolienko.txt", 14),
+                ("Russian", "Stat'i ob okhotie - Sierghiei Timofieievich Aksakov.txt", 15),
+                ("Ukrainian", "Ia (Romantika) - Mikola Khvil'ovii.txt", 308)]
 
 
 def make_text_samples(per_lang=3, width=2500):
-    """F6 ``books_text.json`` — raw text slices of the reference's own corpora (resources/books/<Lang>,
-    three books per language, ``width`` characters from a third of the way in, moved forward past any
-    character the GPU tokenizer rejects): the Cyrillic (Russian, Ukrainian) and Latin-script inputs
-    of the tokenizer's lower-casing tests."""
+    """F6 ``books_text.json`` — raw text slices of the reference's own corpora (resources/books/<Lang>):
+    three books per language, ``width`` characters from a third of the way in, plus one slice around
+    each line of TARGET_LINES (key "targets").  No slice is moved or filtered: the tokenizer's lower-casing
+    tests take the text as it is."""
     out = {}
     base = os.path.join(REF, "books")
     for lang in sorted(os.listdir(base)):
@@ -200,12 +201,39 @@ def make_text_samples(per_lang=3, width=2500):
         for b in books:
             t = open(os.path.join(base, lang, b), encoding="utf-8").read()
             p = len(t) // 3
-            while p + width < len(t) and not all(_kernel_supported(c) for c in t[p:p + width]):
-                p += 97
             samples.append({"book": b, "offset": p, "text": t[p:p + width]})
         out[lang] = samples
+    targets = []
+    for lang, b, line in TARGET_LINES:
+        t = open(os.path.join(base, lang, b), encoding="utf-8").read()
+        lines = t.split("\n")
+        p = len("\n".join(lines[:line - 1])) + 1  # the line's first character (1-based line numbers)
+        # centred on the line's first character past U+0FFF (the Greek Extended letter, the "№")
+        q = next(i for i in range(p, p + len(lines[line - 1])) if ord(t[i]) > 0xFFF)
+        lo = max(0, q - width // 2)
+        targets.append({"book": f"{lang}/{b}", "line": line, "offset": lo, "text": t[lo:lo + width]})
+    out["targets"] = targets
     json.dump(out, open(os.path.join(OUT, "books_text.json"), "w", encoding="utf-8"), ensure_ascii=False, indent=0)
     print("books_text.json:", {k: len(v) for k, v in out.items()})
+
+
+def check_all_books():
+    """Every character of every book under resources/books is one the tokenizer kernel accepts (the
+    generated case table's rejects: tools/gen_case_table.py).  Prints the count; raises otherwise."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_case_table as g
+
+    idx, data = g.pages()
+    rejected = {(idx.index(pi + 1) << 8) + i for pi, ent in enumerate(data) for i, e in enumerate(ent) if e == 0} - {0}
+    base = os.path.join(REF, "books")
+    n = 0
+    for lang in sorted(os.listdir(base)):
+        for b in sorted(os.listdir(os.path.join(base, lang))):
+            t = open(os.path.join(base, lang, b), encoding="utf-8").read()
+            bad = sorted({hex(ord(c)) for c in t if ord(c) in rejected})
+            assert not bad, (lang, b, bad)
+            n += 1
+    print(f"all {n} books: every character accepted by the tokenizer kernel")
 
 
 if __name__ == "__main__":
@@ -214,6 +242,7 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["--text"]:  # the F5/F6 fixtures only (the npz files stay byte-identical)
         make_vocab()
         make_text_samples()
+        check_all_books()
         sys.exit(0)
     ip, ix, tf, meta = make_idf("LdaModel_EN_1591049082850", "en")
     make_idf("LdaModel_GE_1591070442475", "ge")

@@ -448,3 +448,36 @@ def test_team_estep_many_documents(ctx, dtype, k, monkeypatch):
             l1 = np.abs(g[same] - g1[same]).sum(axis=1)
             assert np.all(l1 <= 1e-3 * k + 1e-4 * g1[same].sum(axis=1)), (P, l1.max())
         np.testing.assert_allclose(st.sum(), s1.sum(), rtol=1e-6)
+
+
+@pytest.mark.parametrize("k", [300, 700])
+def test_team_timeout_fails_the_same_call_and_keeps_the_model(ctx, k, monkeypatch):
+    """A team member that never publishes (debug knob STC_TEAM_FAULT=1, team forced to P = 2; k = 300
+    splits rows, k = 700 topics) makes its partner give up.  The SAME step call raises (STC_ERR_HIP),
+    λ, α and the iteration count are bit-identical to before it (the timeout word gated the M-step on
+    the device), topicDistribution raises the same way, and without the knob training continues."""
+    import stc
+
+    monkeypatch.setenv("STC_WIDE_TEAM", "2")
+    rng = np.random.default_rng(31 + k)
+    D, V = 48, 2048
+    corpus = random_corpus(rng, D, V, 100, 300)
+    lam = rng.gamma(100.0, 0.01, size=(V, k))
+    g0 = rng.gamma(100.0, 0.01, size=(D, k))
+    h, d = _handle(ctx, corpus, k, "f64", lam)
+    ids = np.arange(D)
+    h.step(ids, g0)
+    lam1, a1, it1 = h.topics(), h.alpha(), h.iteration()
+    monkeypatch.setenv("STC_TEAM_FAULT", "1")
+    with pytest.raises(stc.StcError) as e:
+        h.step(ids, g0)
+    assert "did not arrive" in str(e.value)
+    np.testing.assert_array_equal(h.topics(), lam1)
+    np.testing.assert_array_equal(h.alpha(), a1)
+    assert h.iteration() == it1
+    with pytest.raises(stc.StcError):
+        h.topic_distribution(d)
+    monkeypatch.delenv("STC_TEAM_FAULT")
+    h.step(ids, g0)
+    assert h.iteration() == it1 + 1
+    assert not np.array_equal(h.topics(), lam1)

@@ -10,7 +10,12 @@ pytestmark = pytest.mark.gpu
 
 _ALPHABET = list("abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789.,;'\"-") + \
     ["Ä", "Ö", "Ü", "ß", "é", "È", "Ç", "×", "Þ", "µ", "\u00a0", "—", "“", "”", "€", "漢", "字", "😀",
-     "Ж", "ж", "Ё", "Ї", "Ґ", "Ω", "ς", "Ğ", "Ł", "Ŋ", "Ǆ", "ǅ", "Ա", "Ͳ", "Ϳ", "Ԩ", "\u0301", "א", "ب"]
+     "Ж", "ж", "Ё", "Ї", "Ґ", "Ω", "ς", "Ğ", "Ł", "Ŋ", "Ǆ", "ǅ", "Ա", "Ͳ", "Ϳ", "Ԩ", "\u0301", "א", "ب",
+     # three- and four-byte: Greek Extended, Latin Extended Additional, letterlike / enclosed / fullwidth
+     # capitals, Glagolitic, Coptic, Georgian, Cherokee and Mtavruli (Java 8: unchanged), Latin Extended-D
+     # (mapped up to U+A7AA, unchanged past it), Deseret, Osage (unchanged), "№"
+     "Ἀ", "ἱ", "Ὠ", "ᾈ", "Ḃ", "ạ", "Ⅻ", "Ⓐ", "Ａ", "ｚ", "Ⰰ", "Ⲁ", "Ⴀ", "ა", "Ꭰ", "Ა", "Ꝁ", "Ꞓ", "Ꞡ", "Ꞵ",
+     "\U00010400", "\U00010427", "\U00010428", "\U000104B0", "№", "ℤ", "ﬀ"]
 _SPACES = [" ", " ", " ", "\t", "\n", "\x0b", "\f", "\r"]
 
 
@@ -49,12 +54,13 @@ def test_random_texts_bit_exact(ctx, oracle, n, max_len):
 
 
 def test_unsupported_case_mapping_fails_loudly(ctx):
-    """Characters whose Java mapping is not a same-length 1:1 map (İ → "i̇", Σ's Final_Sigma rule,
-    Ⱥ → U+2C65), and cased blocks past U+07FF (fullwidth, Greek Extended), raise — never mis-cased."""
+    """Characters whose Java mapping is not a same-length 1:1 map (İ → "i̇", Σ's Final_Sigma rule, and the
+    capitals whose lower case changes UTF-8 length: Ⱥ → U+2C65, ẞ → ß, Ω → ω, K → k, Ɫ → ɫ, Ɦ → ɦ) raise —
+    never mis-cased."""
     import stc
 
     tok = stc.Tokenizer(ctx=ctx)
-    for bad in ["İstanbul", "ΣΟΦΙΑ", "Ⱥx", "ＡＢＣ", "Ἀθῆναι"]:
+    for bad in ["İstanbul", "ΣΟΦΙΑ", "Ⱥx", "STRAẞE", "10 Ω", "300 K", "Ɫa", "Ɦb"]:
         with pytest.raises(ValueError, match="Tokenizer"):
             tok.transform(["fine text", bad])
 
@@ -69,6 +75,21 @@ def test_two_byte_scripts_lower_cased(ctx, oracle):
     assert got == [oracle.tokenize(t) for t in texts]
     assert got[0] == ["москва", "привет", "ёлка"] and got[2] == ["αθηνα", "ωμέγα"]
     assert got[5] == ["Ϳ", "Ԩ", "Ԯ"]  # assigned after Unicode 6.2: Java 8 leaves them as they are
+
+
+def test_three_and_four_byte_scripts_lower_cased(ctx, oracle):
+    """Past U+07FF: Greek Extended (Walden's γεἱβω), Latin Extended Additional, letterlike, enclosed and
+    fullwidth capitals, Glagolitic, Coptic, Georgian, Deseret; "№" and CJK pass; the scripts Java 8 does
+    not case (Cherokee, Mtavruli, Latin Extended-D past U+A7AA, Osage) stay as they are."""
+    import stc
+
+    texts = ["ἈΘΗΝΑΙ γεἱβω ὉΔΟΥ", "ḂḞḞ ẠẸỊ ỲỸ", "ⅫⅣ ⒶⒷ ＡＢＣ ｘｙｚ", "ⰀⰁ ⲀⲂ ႠႡ", "\U00010400\U00010410\U00010427 x",
+             "Лицензия № 2", "ᎠᎡ ᲐᲑ ꞫꞲ \U000104B0", "漢字 😀 ℤ ﬀ"]
+    got = stc.Tokenizer(ctx=ctx).transform(texts)
+    assert got == [oracle.tokenize(t) for t in texts]
+    assert got[0] == ["ἀθηναι", "γεἱβω", "ὁδου"] and got[5] == ["лицензия", "№", "2"]
+    assert got[4][0] == "\U00010428\U00010438\U0001044f"
+    assert got[6] == ["ᎠᎡ", "ᲐᲑ", "ꞫꞲ", "\U000104B0"]
 
 
 def test_reference_books_bit_exact(ctx, oracle):

@@ -45,20 +45,72 @@ def test_java8_lower_known_answers():
     assert O.java_lower("ǅ Ǆ") == "ǆ ǆ"              # titlecase and capital digraph
 
 
-def test_case_table_matches_oracle():
-    """The kernel's generated table (csrc/case_table.h) agrees with the oracle's lower-casing on every
-    accepted two-byte code point, and rejects exactly the non-1:1 ones."""
+def test_java8_lower_past_two_byte_code_points():
+    """Three- and four-byte code points: Greek Extended, Latin Extended Additional, letterlike and
+    enclosed capitals, fullwidth Latin, Glagolitic, Coptic, Deseret map 1:1; caseless characters such as
+    U+2116 "№" stay; the Unicode 7.0+ / 8.0 cased additions Java 8 does not know (Cherokee capitals,
+    Georgian Mtavruli, Latin Extended-D past U+A7AA, Osage, Adlam) stay as they are."""
+    assert O.java_lower("ἈΘΗΝΑΙ Ἱ ὁ") == "ἀθηναι ἱ ὁ"
+    assert O.java_lower("ḂẞẠ") == "ḃßạ"            # U+1E9E ẞ → ß (the kernel rejects it: 3 → 2 bytes)
+    assert O.java_lower("ⅫⒶＡＺ") == "ⅻⓐａｚ"
+    assert O.java_lower("ⰀⲀ") == "ⰰⲁ"
+    assert O.java_lower("\U00010400\U00010427") == "\U00010428\U0001044f"
+    assert O.java_lower("№ 2 ©") == "№ 2 ©"
+    assert O.java_lower("ᎠᏴ") == "ᎠᏴ"                # Cherokee: caseless in Unicode 6.2
+    assert O.java_lower("ᲐᲿ") == "ᲐᲿ"                # Georgian Mtavruli: Unicode 11.0
+    assert O.java_lower("ꞫꞲꟂ") == "ꞫꞲꟂ"              # Latin Extended-D: Unicode 7.0–12.0
+    assert O.java_lower("Ɦ") == "ɦ"                  # U+A7AA: Unicode 6.1, mapped (3 → 2 bytes: rejected)
+    assert O.java_lower("\U000104B0\U0001E900") == "\U000104B0\U0001E900"  # Osage, Adlam
+
+
+def _case_table():
+    """csrc/case_table.h parsed back: {page: [256 entries]} for the pages that are not identity"""
     import os
     import re
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     txt = open(os.path.join(root, "spark-text-clustering_amd", "csrc", "case_table.h")).read()
-    body = txt[txt.index("{", txt.index("kLower2")) + 1:txt.index("};")]
-    vals = [int(x, 16) for x in re.findall(r"0x[0-9A-Fa-f]+", body)]
-    assert len(vals) == 0x700
-    rejected = {cp for cp in range(0x100, 0x800) if vals[cp - 0x100] == 0}
-    assert rejected == {0x130, 0x3A3, 0x23A, 0x23E}
-    for cp in range(0x100, 0x800):
-        if cp in rejected:
+    idx_body = txt[txt.index("{", txt.index("kCasePage[256]")) + 1:]
+    idx = [int(x) for x in re.findall(r"-?\d+", idx_body[:idx_body.index("};")])]
+    assert len(idx) == 256
+    pages_body = txt[txt.index("kCasePages[kCasePagesN][256] = {") + 32:]
+    pages_body = pages_body[:pages_body.index("\n};")]
+    pages = re.findall(r"\{\s*// U\+([0-9A-F]{4})[^\n]*\n(.*?)\n\s*\}", pages_body, re.S)
+    out = {}
+    for start, body in pages:
+        vals = [int(x, 16) for x in re.findall(r"0x[0-9A-Fa-f]+", body)]
+        assert len(vals) == 256
+        out[int(start, 16) >> 8] = vals
+    # pages are emitted in code point order, page i + 1 of the index being the i-th emitted
+    assert [idx[p] for p in out] == list(range(1, len(out) + 1)), "page index and page data disagree"
+    assert sum(1 for i in idx if i) == len(out)
+    return out
+
+
+def test_case_table_matches_oracle():
+    """The kernel's generated table (csrc/case_table.h) agrees with the oracle's Java 8 lower-casing on
+    every BMP code point it accepts (identity pages included), and rejects exactly the non-1:1 ones:
+    İ (SpecialCasing), Σ (Final_Sigma) and the capitals whose lower case has another UTF-8 length."""
+    pages = _case_table()
+    expected_rejects = {0x130, 0x3A3, 0x23A, 0x23E, 0x1E9E, 0x2126, 0x212A, 0x212B, 0x2C62, 0x2C64, 0x2C6D,
+                        0x2C6E, 0x2C6F, 0x2C70, 0x2C7E, 0x2C7F, 0xA78D, 0xA7AA}
+    rejected = set()
+    for cp in range(0x80, 0x10000):
+        if 0xD800 <= cp <= 0xDFFF:
             continue
-        assert O.java_lower(chr(cp)) == chr(vals[cp - 0x100]), hex(cp)
+        ent = pages[cp >> 8][cp & 0xFF] if (cp >> 8) in pages else cp
+        if ent == 0:
+            rejected.add(cp)
+            continue
+        assert O.java_lower(chr(cp)) == chr(ent), hex(cp)
+    assert rejected == expected_rejects
+
+
+def test_reference_book_slices_hold_the_round2_rejects():
+    """tests/golden/books_text.json carries slices of every book line the round-2 kernel rejected
+    (Walden's Greek Extended letters, four "№" lines) — no slice of the fixture is filtered."""
+    from helpers import golden_json
+
+    books = golden_json("books_text.json")
+    joined = "".join(t["text"] for t in books["targets"])
+    assert "\u1f31" in joined and "\u1f41" in joined and joined.count("\u2116") >= 4
