@@ -251,6 +251,44 @@ int stc_lda_enable_timing(stc_lda* lda, int on);
 int stc_lda_counters(stc_lda* lda, int64_t out[4]);
 int stc_lda_phase_times(stc_lda* lda, double* ms_out /* 5 */, int64_t* steps_out);
 
+/* ---- one process, N devices ---------------------------------------------------------------
+ * The reference trains in ONE JVM (Spark local[*], LDATraining.scala:7), so its drop-in drives every GPU
+ * of the node from one handle ("single-process multi-device").  stc_group_create makes
+ * one context and one LDA handle per device (distinct devices: one RCCL communicator, ncclCommInitAll;
+ * the same device repeated: an in-process transport, the multi-GPU decomposition on one GPU), and every
+ * group call runs the per-device call on one host thread per member.  The corpus is given once, on the
+ * host, and sharded by contiguous document ranges balanced by entries (document ids stay global).  Each
+ * group call = the same stc_lda_* call on every member (the collectives pair up by construction). */
+typedef struct stc_group stc_group;
+int stc_group_create(const int* device_ids, int n_devices, const stc_lda_config* cfg, stc_group** out);
+int stc_group_destroy(stc_group* g);
+int stc_group_size(const stc_group* g, int* n_out);
+/* member i's handle (counters, timing); do not call its collective entry points directly */
+int stc_group_member(stc_group* g, int i, stc_lda** lda_out);
+/* the training corpus (rows = documents, values in the group's dtype on device) */
+int stc_group_set_corpus(stc_group* g, int64_t n_rows, int64_t n_cols, const int64_t* indptr,
+                         const int32_t* indices, const double* values);
+int stc_group_init_random(stc_group* g, uint64_t seed);
+int stc_group_set_topics(stc_group* g, const double* topics, int layout);
+int stc_group_get_topics(stc_group* g, double* topics_out, int layout);
+int stc_group_get_alpha(stc_group* g, double* alpha_out /* k */);
+int stc_group_get_iteration(stc_group* g, int64_t* iteration_out);
+/* OnlineLDAOptimizer.next() over every member's documents; stats summed over the members */
+int stc_group_next(stc_group* g, stc_step_stats* stats);
+/* submitMiniBatch over injected GLOBAL document ids (gamma0 n×k in the same order, may be NULL) */
+int stc_group_step(stc_group* g, const int64_t* batch_doc_ids, int64_t n, const double* gamma0,
+                   stc_step_stats* stats);
+int stc_group_describe(stc_group* g, int32_t max_terms, int32_t* idx_out, double* weight_out);
+/* logLikelihood / topicDistribution of host documents, sharded over the members; γ₀ keys are
+ * doc_id_base + global row, so the results equal a single handle's over the same rows */
+int stc_group_bound(stc_group* g, int64_t n_rows, int64_t n_cols, const int64_t* indptr,
+                    const int32_t* indices, const double* values, uint64_t gamma_seed, int64_t doc_id_base,
+                    const double* gamma0, double* bound_out, double* corpus_part_out,
+                    double* topics_part_out, double* token_count_out);
+int stc_group_topic_distribution(stc_group* g, int64_t n_rows, int64_t n_cols, const int64_t* indptr,
+                                 const int32_t* indices, const double* values, uint64_t gamma_seed,
+                                 int64_t doc_id_base, const double* gamma0, double* out /* rows×k */);
+
 #ifdef __cplusplus
 }
 #endif

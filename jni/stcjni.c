@@ -31,6 +31,7 @@
 #define CTX(h) ((stc_ctx*)(intptr_t)(h))
 #define CSR(h) ((stc_dcsr*)(intptr_t)(h))
 #define LDA(h) ((stc_lda*)(intptr_t)(h))
+#define GRP(h) ((stc_group*)(intptr_t)(h))
 
 static int check(JNIEnv* env, int st) {
   if (st == STC_OK) return 0;
@@ -547,4 +548,204 @@ JNIEXPORT jlong JNICALL FN(ldaPhaseTimes)(JNIEnv* env, jclass c, jlong lda, jdou
   UNPIN(Double, ms_out, p, 0);
   check(env, st);
   return steps;
+}
+
+/* ---- one process, N devices (stc_group) ---------------------------------------------------------- */
+/* the same parameters as ldaCreate, plus the device ids */
+JNIEXPORT jlong JNICALL FN(groupCreate)(JNIEnv* env, jclass c, jintArray devices, jint k, jlong vocab,
+                                        jdoubleArray alpha, jdouble eta, jdouble tau0, jdouble kappa, jdouble frac,
+                                        jdouble gamma_shape, jboolean optimize_alpha, jboolean with_replacement,
+                                        jlong seed, jint dtype, jint max_inner_iter) {
+  if (!devices || LEN(devices) < 1) {
+    throw_iae(env, "groupCreate: at least one device id");
+    return 0;
+  }
+  stc_lda_config cfg;
+  stc_lda_config_default(&cfg);
+  jdouble* a = PIN(jdouble, Double, alpha);
+  jint* dv = PIN(jint, Int, devices);
+  cfg.k = k;
+  cfg.vocab_size = vocab;
+  cfg.doc_concentration = a;
+  cfg.doc_concentration_len = (int32_t)LEN(alpha);
+  cfg.topic_concentration = eta;
+  cfg.tau0 = tau0;
+  cfg.kappa = kappa;
+  cfg.mini_batch_fraction = frac;
+  cfg.gamma_shape = gamma_shape;
+  cfg.optimize_doc_concentration = optimize_alpha ? 1 : 0;
+  cfg.sample_with_replacement = with_replacement ? 1 : 0;
+  cfg.seed = (uint64_t)seed;
+  cfg.dtype = dtype;
+  cfg.max_inner_iter = max_inner_iter;
+  stc_group* out = NULL;
+  int st = stc_group_create((const int*)dv, (int)LEN(devices), &cfg, &out);
+  UNPIN(Int, devices, dv, JNI_ABORT);
+  UNPIN(Double, alpha, a, JNI_ABORT);
+  if (check(env, st)) return 0;
+  return (jlong)(intptr_t)out;
+}
+
+JNIEXPORT void JNICALL FN(groupDestroy)(JNIEnv* env, jclass c, jlong g) { check(env, stc_group_destroy(GRP(g))); }
+
+JNIEXPORT jint JNICALL FN(groupSize)(JNIEnv* env, jclass c, jlong g) {
+  int n = 0;
+  check(env, stc_group_size(GRP(g), &n));
+  return n;
+}
+
+JNIEXPORT jlong JNICALL FN(groupMember)(JNIEnv* env, jclass c, jlong g, jint i) {
+  stc_lda* l = NULL;
+  if (check(env, stc_group_member(GRP(g), i, &l))) return 0;
+  return (jlong)(intptr_t)l;
+}
+
+/* the host CSR of a group call: indptr[rows + 1], indices / values[indptr[rows]] */
+static int csr_args(JNIEnv* env, jlong rows, jlongArray indptr, jintArray indices, jdoubleArray values,
+                    const char* what) {
+  if (rows < 0 || !indptr || NEED(indptr, rows + 1, what)) {
+    if (!(*env)->ExceptionCheck(env)) throw_iae(env, "indptr[rows + 1] is required");
+    return 1;
+  }
+  jlong last = 0;
+  (*env)->GetLongArrayRegion(env, indptr, (jsize)rows, 1, &last);
+  return NEED(indices, last, what) || NEED(values, last, what);
+}
+
+JNIEXPORT void JNICALL FN(groupSetCorpus)(JNIEnv* env, jclass c, jlong g, jlong rows, jlong cols, jlongArray indptr,
+                                          jintArray indices, jdoubleArray values) {
+  if (csr_args(env, rows, indptr, indices, values, "groupSetCorpus")) return;
+  jlong* ip = PIN(jlong, Long, indptr);
+  jint* ix = PIN(jint, Int, indices);
+  jdouble* vs = PIN(jdouble, Double, values);
+  int st = stc_group_set_corpus(GRP(g), rows, cols, (const int64_t*)ip, (const int32_t*)ix, vs);
+  UNPIN(Double, values, vs, JNI_ABORT);
+  UNPIN(Int, indices, ix, JNI_ABORT);
+  UNPIN(Long, indptr, ip, JNI_ABORT);
+  check(env, st);
+}
+
+JNIEXPORT void JNICALL FN(groupInitRandom)(JNIEnv* env, jclass c, jlong g, jlong seed) {
+  check(env, stc_group_init_random(GRP(g), (uint64_t)seed));
+}
+
+static int group_shape(JNIEnv* env, jlong g, int64_t* k, int64_t* vocab) {
+  stc_lda* l = NULL;
+  if (check(env, stc_group_member(GRP(g), 0, &l))) return 1;
+  return lda_shape(env, (jlong)(intptr_t)l, k, vocab);
+}
+
+JNIEXPORT void JNICALL FN(groupSetTopics)(JNIEnv* env, jclass c, jlong g, jdoubleArray topics, jint layout) {
+  int64_t k = 0, V = 0;
+  if (group_shape(env, g, &k, &V) || NEED(topics, k * V, "groupSetTopics topics")) return;
+  jdouble* p = PIN(jdouble, Double, topics);
+  int st = stc_group_set_topics(GRP(g), p, layout);
+  UNPIN(Double, topics, p, JNI_ABORT);
+  check(env, st);
+}
+
+JNIEXPORT void JNICALL FN(groupGetTopics)(JNIEnv* env, jclass c, jlong g, jdoubleArray out, jint layout) {
+  int64_t k = 0, V = 0;
+  if (group_shape(env, g, &k, &V) || NEED(out, k * V, "groupGetTopics out")) return;
+  jdouble* p = PIN(jdouble, Double, out);
+  int st = stc_group_get_topics(GRP(g), p, layout);
+  UNPIN(Double, out, p, 0);
+  check(env, st);
+}
+
+JNIEXPORT void JNICALL FN(groupGetAlpha)(JNIEnv* env, jclass c, jlong g, jdoubleArray out) {
+  int64_t k = 0, V = 0;
+  if (group_shape(env, g, &k, &V) || NEED(out, k, "groupGetAlpha out")) return;
+  jdouble* p = PIN(jdouble, Double, out);
+  int st = stc_group_get_alpha(GRP(g), p);
+  UNPIN(Double, out, p, 0);
+  check(env, st);
+}
+
+JNIEXPORT jlong JNICALL FN(groupGetIteration)(JNIEnv* env, jclass c, jlong g) {
+  int64_t it = 0;
+  check(env, stc_group_get_iteration(GRP(g), &it));
+  return it;
+}
+
+JNIEXPORT void JNICALL FN(groupNext)(JNIEnv* env, jclass c, jlong g, jdoubleArray stats) {
+  stc_step_stats s;
+  memset(&s, 0, sizeof s);
+  if (!check(env, stc_group_next(GRP(g), stats ? &s : NULL))) stats_out(env, stats, &s);
+}
+
+JNIEXPORT void JNICALL FN(groupStep)(JNIEnv* env, jclass c, jlong g, jlongArray ids, jdoubleArray gamma0,
+                                     jdoubleArray stats) {
+  stc_step_stats s;
+  memset(&s, 0, sizeof s);
+  int64_t k = 0, V = 0;
+  if (group_shape(env, g, &k, &V) || NEED(gamma0, LEN(ids) * k, "groupStep gamma0")) return;
+  jlong* p = PIN(jlong, Long, ids);
+  jdouble* g0 = PIN(jdouble, Double, gamma0);
+  int st = stc_group_step(GRP(g), (const int64_t*)p, LEN(ids), g0, stats ? &s : NULL);
+  UNPIN(Double, gamma0, g0, JNI_ABORT);
+  UNPIN(Long, ids, p, JNI_ABORT);
+  if (!check(env, st)) stats_out(env, stats, &s);
+}
+
+JNIEXPORT void JNICALL FN(groupDescribe)(JNIEnv* env, jclass c, jlong g, jint max_terms, jintArray idx_out,
+                                         jdoubleArray weight_out) {
+  int64_t k = 0, V = 0;
+  if (group_shape(env, g, &k, &V)) return;
+  const int64_t N = max_terms < V ? (max_terms > 0 ? max_terms : 0) : V;
+  if (NEED(idx_out, k * N, "groupDescribe idxOut") || NEED(weight_out, k * N, "groupDescribe weightOut")) return;
+  jint* ix = PIN(jint, Int, idx_out);
+  jdouble* w = PIN(jdouble, Double, weight_out);
+  int st = stc_group_describe(GRP(g), max_terms, (int32_t*)ix, w);
+  UNPIN(Double, weight_out, w, 0);
+  UNPIN(Int, idx_out, ix, 0);
+  check(env, st);
+}
+
+/* {bound, corpusPart, topicsPart, tokenCount} */
+JNIEXPORT jdoubleArray JNICALL FN(groupBound)(JNIEnv* env, jclass c, jlong g, jlong rows, jlong cols,
+                                              jlongArray indptr, jintArray indices, jdoubleArray values,
+                                              jlong gamma_seed, jlong doc_id_base, jdoubleArray gamma0) {
+  int64_t k = 0, V = 0;
+  if (csr_args(env, rows, indptr, indices, values, "groupBound") || group_shape(env, g, &k, &V) ||
+      NEED(gamma0, rows * k, "groupBound gamma0"))
+    return NULL;
+  double r[4] = {0, 0, 0, 0};
+  jlong* ip = PIN(jlong, Long, indptr);
+  jint* ix = PIN(jint, Int, indices);
+  jdouble* vs = PIN(jdouble, Double, values);
+  jdouble* g0 = PIN(jdouble, Double, gamma0);
+  int st = stc_group_bound(GRP(g), rows, cols, (const int64_t*)ip, (const int32_t*)ix, vs, (uint64_t)gamma_seed,
+                           doc_id_base, g0, &r[0], &r[1], &r[2], &r[3]);
+  UNPIN(Double, gamma0, g0, JNI_ABORT);
+  UNPIN(Double, values, vs, JNI_ABORT);
+  UNPIN(Int, indices, ix, JNI_ABORT);
+  UNPIN(Long, indptr, ip, JNI_ABORT);
+  if (check(env, st)) return NULL;
+  jdoubleArray out = (*env)->NewDoubleArray(env, 4);
+  if (out) (*env)->SetDoubleArrayRegion(env, out, 0, 4, r);
+  return out;
+}
+
+JNIEXPORT void JNICALL FN(groupTopicDistribution)(JNIEnv* env, jclass c, jlong g, jlong rows, jlong cols,
+                                                  jlongArray indptr, jintArray indices, jdoubleArray values,
+                                                  jlong gamma_seed, jlong doc_id_base, jdoubleArray gamma0,
+                                                  jdoubleArray out) {
+  int64_t k = 0, V = 0;
+  if (csr_args(env, rows, indptr, indices, values, "groupTopicDistribution") || group_shape(env, g, &k, &V) ||
+      NEED(gamma0, rows * k, "groupTopicDistribution gamma0") || NEED(out, rows * k, "groupTopicDistribution out"))
+    return;
+  jlong* ip = PIN(jlong, Long, indptr);
+  jint* ix = PIN(jint, Int, indices);
+  jdouble* vs = PIN(jdouble, Double, values);
+  jdouble* g0 = PIN(jdouble, Double, gamma0);
+  jdouble* o = PIN(jdouble, Double, out);
+  int st = stc_group_topic_distribution(GRP(g), rows, cols, (const int64_t*)ip, (const int32_t*)ix, vs,
+                                        (uint64_t)gamma_seed, doc_id_base, g0, o);
+  UNPIN(Double, out, o, 0);
+  UNPIN(Double, gamma0, g0, JNI_ABORT);
+  UNPIN(Double, values, vs, JNI_ABORT);
+  UNPIN(Int, indices, ix, JNI_ABORT);
+  UNPIN(Long, indptr, ip, JNI_ABORT);
+  check(env, st);
 }

@@ -115,4 +115,29 @@ public final class StcNative {
     }
     return new Object[] {indptr, indices, values};
   }
+
+  // ---- one process, N devices (stc_group): the multi-GPU form of the drop-in inside one JVM ----------
+  public static native long groupCreate(int[] deviceIds, int k, long vocabSize, double[] alpha, double eta,
+                                        double tau0, double kappa, double miniBatchFraction, double gammaShape,
+                                        boolean optimizeAlpha, boolean withReplacement, long seed, int dtype,
+                                        int maxInnerIter);
+  public static native void groupDestroy(long group);
+  public static native int groupSize(long group);
+  public static native long groupMember(long group, int i);
+  public static native void groupSetCorpus(long group, long rows, long cols, long[] indptr, int[] indices,
+                                           double[] values);
+  public static native void groupInitRandom(long group, long seed);
+  public static native void groupSetTopics(long group, double[] topics, int layout);
+  public static native void groupGetTopics(long group, double[] out, int layout);
+  public static native void groupGetAlpha(long group, double[] out);
+  public static native long groupGetIteration(long group);
+  public static native void groupNext(long group, double[] stats);
+  public static native void groupStep(long group, long[] batchDocIds, double[] gamma0, double[] stats);
+  public static native void groupDescribe(long group, int maxTerms, int[] idxOut, double[] weightOut);
+  /** {bound, corpusPart, topicsPart, tokenCount} */
+  public static native double[] groupBound(long group, long rows, long cols, long[] indptr, int[] indices,
+                                           double[] values, long gammaSeed, long docIdBase, double[] gamma0);
+  public static native void groupTopicDistribution(long group, long rows, long cols, long[] indptr, int[] indices,
+                                                   double[] values, long gammaSeed, long docIdBase,
+                                                   double[] gamma0, double[] out);
 }

@@ -10,8 +10,12 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
+#include <exception>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <type_traits>
 
 #include "lda_kernels.h"
@@ -122,6 +126,132 @@ struct RcclType<double> {
   static constexpr ncclDataType_t v = ncclFloat64;
 };
 
+// ---------------------------------------------------------------------------------------
+// Collectives.  RCCL over the context's communicator — or, for the members of one stc_group that share a
+// device (a group of N handles on one GPU: the multi-GPU decomposition exercised on one device), an
+// in-process transport: every member runs on its own host thread, the members exchange device pointers
+// under a barrier and sum / copy with the kernels below, in member order (so every member's result is
+// bit-identical).  Same call sequence on every member, as with RCCL.
+// ---------------------------------------------------------------------------------------
+}  // namespace
+
+struct stc::LocalColl {
+  int n = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool broken = false;
+  std::vector<void*> ptr;
+  explicit LocalColl(int members) : n(members), ptr((size_t)members, nullptr) {}
+  void barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    if (broken) throw Error(STC_ERR_STATE, "another member of the group failed");
+    const uint64_t g = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return;
+    }
+    cv.wait(lk, [&] { return gen != g || broken; });
+    if (broken && gen == g) throw Error(STC_ERR_STATE, "another member of the group failed");
+  }
+  void fail() {
+    std::lock_guard<std::mutex> lk(m);
+    broken = true;
+    cv.notify_all();
+  }
+};
+
+namespace {
+
+constexpr int kMaxMembers = 16;
+struct MemberPtrs {
+  const void* p[kMaxMembers];
+};
+template <typename T>
+__global__ void k_sum_members(T* __restrict__ out, MemberPtrs src, int n, int64_t off, int64_t count) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+    T acc = static_cast<const T*>(src.p[0])[off + i];
+    for (int m = 1; m < n; ++m) acc += static_cast<const T*>(src.p[m])[off + i];
+    out[i] = acc;
+  }
+}
+size_t dt_size(ncclDataType_t t) { return t == ncclFloat32 ? 4 : 8; }
+void launch_sum_members(hipStream_t s, ncclDataType_t t, void* out, const MemberPtrs& src, int n, int64_t off,
+                        int64_t count) {
+  if (count == 0) return;
+  const int grid = (int)std::min<int64_t>(ceil_div(count, 256), 4096);
+  if (t == ncclFloat64) k_sum_members<double><<<grid, 256, 0, s>>>(static_cast<double*>(out), src, n, off, count);
+  else if (t == ncclFloat32) k_sum_members<float><<<grid, 256, 0, s>>>(static_cast<float*>(out), src, n, off, count);
+  else if (t == ncclInt64) k_sum_members<int64_t><<<grid, 256, 0, s>>>(static_cast<int64_t*>(out), src, n, off, count);
+  else throw Error(STC_ERR_STATE, "in-process collective: unsupported type");
+  KERNEL_CHECK();
+}
+MemberPtrs published(const LocalColl& L) {
+  MemberPtrs p{};
+  for (int m = 0; m < L.n; ++m) p.p[m] = L.ptr[(size_t)m];
+  return p;
+}
+
+void coll_group_start(Ctx& c) {
+  if (c.comm) RCCL_CHECK(ncclGroupStart());
+}
+void coll_group_end(Ctx& c) {
+  if (c.comm) RCCL_CHECK(ncclGroupEnd());
+}
+// in place: buf ← Σ over members
+void coll_all_reduce(Ctx& c, void* buf, size_t count, ncclDataType_t t, hipStream_t s) {
+  if (c.comm) {
+    RCCL_CHECK(ncclAllReduce(buf, buf, count, t, ncclSum, c.comm, s));
+    return;
+  }
+  LocalColl& L = *c.local;
+  HIP_CHECK(hipStreamSynchronize(s));
+  L.ptr[(size_t)c.rank] = buf;
+  L.barrier();
+  c.coll_tmp.reserve(dt_size(t) * std::max<size_t>(count, 1));
+  launch_sum_members(s, t, c.coll_tmp.p, published(L), L.n, 0, (int64_t)count);
+  HIP_CHECK(hipStreamSynchronize(s));
+  L.barrier();  // every member has read every buffer
+  HIP_CHECK(hipMemcpyAsync(buf, c.coll_tmp.p, dt_size(t) * count, hipMemcpyDeviceToDevice, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+}
+// recv (recvcount elements) ← Σ over members of their send[rank·recvcount, +recvcount); recv may be
+// the member's own slice of send
+void coll_reduce_scatter(Ctx& c, const void* send, void* recv, size_t recvcount, ncclDataType_t t, hipStream_t s) {
+  if (c.comm) {
+    RCCL_CHECK(ncclReduceScatter(send, recv, recvcount, t, ncclSum, c.comm, s));
+    return;
+  }
+  LocalColl& L = *c.local;
+  HIP_CHECK(hipStreamSynchronize(s));
+  L.ptr[(size_t)c.rank] = const_cast<void*>(send);
+  L.barrier();
+  launch_sum_members(s, t, recv, published(L), L.n, (int64_t)(c.rank * recvcount), (int64_t)recvcount);
+  HIP_CHECK(hipStreamSynchronize(s));
+  L.barrier();
+}
+// recv[q·sendcount, +sendcount) ← member q's send, on every member (send may be its own slice of recv)
+void coll_all_gather(Ctx& c, const void* send, void* recv, size_t sendcount, ncclDataType_t t, hipStream_t s) {
+  if (c.comm) {
+    RCCL_CHECK(ncclAllGather(send, recv, sendcount, t, c.comm, s));
+    return;
+  }
+  LocalColl& L = *c.local;
+  const size_t bytes = dt_size(t) * sendcount;
+  HIP_CHECK(hipStreamSynchronize(s));
+  L.ptr[(size_t)c.rank] = recv;
+  L.barrier();
+  for (int q = 0; q < L.n; ++q) {
+    char* dst = static_cast<char*>(L.ptr[(size_t)q]) + (size_t)c.rank * bytes;
+    if (dst != send && bytes) HIP_CHECK(hipMemcpyAsync(dst, send, bytes, hipMemcpyDeviceToDevice, s));
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  L.barrier();
+}
+
 inline int bits_for(int64_t n) {
   int b = 1;
   while ((int64_t(1) << b) < n) ++b;
@@ -159,7 +289,7 @@ void claim_event_set(stc_lda& L) {
 // chunks); the padded rows of stat are zero, those of λ / Bp never read.  Called before a step; a
 // change of shard count (comm initialised after the handle) keeps λ and recomputes the rest.
 void ensure_layout(stc_lda& L) {
-  const int want = L.ctx->comm && (L.ctx->n_ranks > 1 || L.force_coll) ? L.ctx->n_ranks : L.virt;
+  const int want = L.ctx->coll() && (L.ctx->n_ranks > 1 || L.force_coll) ? L.ctx->n_ranks : L.virt;
   if (want == L.shards && L.Vs > 0) return;
   if (L.lam_stale) throw Error(STC_ERR_STATE, "the shard count changed after sharded steps");
   const int64_t RB = lda::kRowsPerBlock;
@@ -575,18 +705,17 @@ template <typename T>
 void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
   Ctx& c = *L.ctx;
   hipStream_t s = c.stream;
-  const bool ranks = c.comm && (c.n_ranks > 1 || L.force_coll);
-  if (c.comm) {
-    RCCL_CHECK(ncclGroupStart());
+  const bool ranks = c.coll() && (c.n_ranks > 1 || L.force_coll);
+  if (c.coll()) {
+    coll_group_start(c);
     if (ranks) {
       const size_t cnt = (size_t)(L.Vs * L.kp);
-      RCCL_CHECK(ncclReduceScatter(L.stat.p, L.stat.as<T>() + (size_t)c.rank * cnt, cnt, RcclType<T>::v, ncclSum,
-                                   c.comm, s));
+      coll_reduce_scatter(c, L.stat.p, L.stat.as<T>() + (size_t)c.rank * cnt, cnt, RcclType<T>::v, s);
     }
-    RCCL_CHECK(ncclAllReduce(L.small.p, L.small.p, (size_t)(L.k + 1), ncclFloat64, ncclSum, c.comm, s));
+    coll_all_reduce(c, L.small.p, (size_t)(L.k + 1), ncclFloat64, s);
     if (L.pre_inflight)  // the next draw's global batch size (word 3), for the next call
-      RCCL_CHECK(ncclAllReduce(L.dcnt.as<int64_t>() + 3, L.dcnt.as<int64_t>() + 3, 1, ncclInt64, ncclSum, c.comm, s));
-    RCCL_CHECK(ncclGroupEnd());
+      coll_all_reduce(c, L.dcnt.as<int64_t>() + 3, 1, ncclInt64, s);
+    coll_group_end(c);
   }
   if (L.pre_inflight) {
     HIP_CHECK(hipMemcpyAsync(L.hpre, L.dcnt.p, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -604,16 +733,14 @@ void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
   if (ranks) {
     const size_t nbs = (size_t)(L.Vs / lda::kRowsPerBlock);
     mstep_slice<T>(L, c.rank, rho, scale, gate);
-    RCCL_CHECK(ncclAllGather(L.colpart.as<double>() + (size_t)c.rank * nbs * L.k, L.colpart.p, nbs * L.k,
-                             ncclFloat64, c.comm, s));
+    coll_all_gather(c, L.colpart.as<double>() + (size_t)c.rank * nbs * L.k, L.colpart.p, nbs * L.k, ncclFloat64, s);
     lda::launch_colsum_reduce(s, L.colpart.as<double>(), nb_all, L.k, gate, L.colsum.as<double>());
     eeb_slice<T>(L, c.rank, gate);
     const size_t cnt = (size_t)(L.Vs * L.kp);
-    RCCL_CHECK(ncclGroupStart());
-    RCCL_CHECK(ncclAllGather(L.Bp.as<T>() + (size_t)c.rank * cnt, L.Bp.p, cnt, RcclType<T>::v, c.comm, s));
-    RCCL_CHECK(ncclAllGather(L.logscale.as<double>() + (size_t)c.rank * L.Vs, L.logscale.p, (size_t)L.Vs,
-                             ncclFloat64, c.comm, s));
-    RCCL_CHECK(ncclGroupEnd());
+    coll_group_start(c);
+    coll_all_gather(c, L.Bp.as<T>() + (size_t)c.rank * cnt, L.Bp.p, cnt, RcclType<T>::v, s);
+    coll_all_gather(c, L.logscale.as<double>() + (size_t)c.rank * L.Vs, L.logscale.p, (size_t)L.Vs, ncclFloat64, s);
+    coll_group_end(c);
     L.lam_stale = true;
   } else {  // one GPU: all slices here (one unless STC_VIRTUAL_SHARDS)
     for (int r = 0; r < L.shards; ++r) mstep_slice<T>(L, r, rho, scale, gate);
@@ -737,8 +864,7 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
     std::copy(L.hpre, L.hpre + 4, cnt);
   } else {
     sample_draw(L, draw);
-    if (c.comm)
-      RCCL_CHECK(ncclAllReduce(L.dcnt.as<int64_t>() + 3, L.dcnt.as<int64_t>() + 3, 1, ncclInt64, ncclSum, c.comm, s));
+    if (c.coll()) coll_all_reduce(c, L.dcnt.as<int64_t>() + 3, 1, ncclInt64, s);
     HIP_CHECK(hipMemcpyAsync(L.hcnt, L.dcnt.p, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     std::copy(L.hcnt, L.hcnt + 4, cnt);
@@ -853,7 +979,7 @@ void gather_lambda(stc_lda& L) {
   if (!L.lam_stale) return;
   Ctx& c = *L.ctx;
   const size_t cnt = (size_t)(L.Vs * L.k);
-  RCCL_CHECK(ncclAllGather(L.lam.as<double>() + (size_t)c.rank * cnt, L.lam.p, cnt, ncclFloat64, c.comm, c.stream));
+  coll_all_gather(c, L.lam.as<double>() + (size_t)c.rank * cnt, L.lam.p, cnt, ncclFloat64, c.stream);
   HIP_CHECK(hipStreamSynchronize(c.stream));
   L.lam_stale = false;
 }
@@ -891,11 +1017,11 @@ void topics_part(stc_lda& L, double* elem_part, double* norm_part) {
 }
 
 void allreduce_host(Ctx& c, double* x, int64_t n) {
-  if (!c.comm || n == 0) return;
+  if (!c.coll() || n == 0) return;
   DevBuf d;
   d.reserve(sizeof(double) * n);
   HIP_CHECK(hipMemcpyAsync(d.p, x, sizeof(double) * n, hipMemcpyHostToDevice, c.stream));
-  RCCL_CHECK(ncclAllReduce(d.p, d.p, (size_t)n, ncclFloat64, ncclSum, c.comm, c.stream));
+  coll_all_reduce(c, d.p, (size_t)n, ncclFloat64, c.stream);
   HIP_CHECK(hipMemcpyAsync(x, d.p, sizeof(double) * n, hipMemcpyDeviceToHost, c.stream));
   HIP_CHECK(hipStreamSynchronize(c.stream));
 }
@@ -1275,14 +1401,14 @@ int stc_idf_fit(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, double* 
     idf.reserve(8 * tf->cols);
     idf::doc_freq(*ctx, *tf, df.as<int64_t>());
     int64_t m = tf->rows;
-    if (ctx->comm) {  // DocumentFrequencyAggregator.merge over ranks
+    if (ctx->coll()) {  // DocumentFrequencyAggregator.merge over ranks
       DevBuf mm;
       mm.reserve(8);
       HIP_CHECK(hipMemcpyAsync(mm.p, &m, 8, hipMemcpyHostToDevice, s));
-      RCCL_CHECK(ncclGroupStart());
-      RCCL_CHECK(ncclAllReduce(df.p, df.p, (size_t)tf->cols, ncclInt64, ncclSum, ctx->comm, s));
-      RCCL_CHECK(ncclAllReduce(mm.p, mm.p, 1, ncclInt64, ncclSum, ctx->comm, s));
-      RCCL_CHECK(ncclGroupEnd());
+      coll_group_start(*ctx);
+      coll_all_reduce(*ctx, df.p, (size_t)tf->cols, ncclInt64, s);
+      coll_all_reduce(*ctx, mm.p, 1, ncclInt64, s);
+      coll_group_end(*ctx);
       HIP_CHECK(hipMemcpyAsync(&m, mm.p, 8, hipMemcpyDeviceToHost, s));
       HIP_CHECK(hipStreamSynchronize(s));
     }
@@ -1680,6 +1806,348 @@ int stc_lda_counters(stc_lda* L, int64_t out[4]) {
     out[1] = L->cum_entries;
     out[2] = c2[0];
     out[3] = c2[1];
+  });
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// stc_group: one process driving N devices (stc_init(device_ids, n)).  The JVM runs
+// the reference in ONE process (Spark local[*], LDATraining.scala:7), so its drop-in needs the N GPUs of
+// the node behind one handle: N contexts joined by one communicator (ncclCommInitAll over distinct
+// devices; the in-process transport above when every member shares one device), N LDA handles over
+// contiguous document shards (balanced by entries), each call run on one host thread per member.
+// ---------------------------------------------------------------------------------------
+struct stc_group {
+  std::vector<stc_ctx*> ctx;
+  std::vector<stc_lda*> lda;
+  std::vector<stc_dcsr*> shard;
+  std::vector<int64_t> row0;  // first corpus row of each member's shard (n + 1 entries)
+  std::unique_ptr<LocalColl> local;
+  int64_t rows = 0, cols = 0;
+  int dtype = STC_F64;
+  int n() const { return (int)ctx.size(); }
+};
+
+namespace {
+
+void member_ok(int rc) {
+  if (rc != STC_OK) throw Error(rc, stc_last_error());
+}
+// f(i) for every member on its own thread (device set); the first failure is rethrown here
+template <typename F>
+void for_members(stc_group& g, F f) {
+  const int n = g.n();
+  std::vector<std::exception_ptr> err((size_t)n);
+  std::mutex fm;
+  int first = -1;  // the member that failed first (the others may only report "another member failed")
+  auto run = [&](int i) {
+    try {
+      g.ctx[(size_t)i]->use();
+      f(i);
+    } catch (...) {
+      err[(size_t)i] = std::current_exception();
+      {
+        std::lock_guard<std::mutex> lk(fm);
+        if (first < 0) first = i;
+      }
+      if (g.local) g.local->fail();  // release the members waiting in a barrier
+    }
+  };
+  if (n == 1) {
+    run(0);
+  } else {
+    std::vector<std::thread> th;
+    th.reserve((size_t)n);
+    for (int i = 0; i < n; ++i) th.emplace_back(run, i);
+    for (auto& t : th) t.join();
+  }
+  if (g.local) {  // a failed call leaves the transport usable for the next one
+    std::lock_guard<std::mutex> lk(g.local->m);
+    g.local->broken = false;
+    g.local->arrived = 0;
+  }
+  if (first >= 0) std::rethrow_exception(err[(size_t)first]);
+}
+// contiguous row ranges of a host CSR, one per member, balanced by entries
+std::vector<int64_t> shard_rows(const int64_t* indptr, int64_t rows, int n) {
+  std::vector<int64_t> r0((size_t)n + 1, rows);
+  r0[0] = 0;
+  const int64_t nnz = indptr[rows];
+  int64_t r = 0;
+  for (int q = 1; q < n; ++q) {
+    const int64_t target = (nnz * q + n - 1) / n;
+    while (r < rows && indptr[r] < target) ++r;
+    r0[(size_t)q] = std::max(r, r0[(size_t)q - 1]);
+  }
+  return r0;
+}
+// member i's rows [r0[i], r0[i+1]) of a host CSR uploaded to its device (indptr rebased)
+stc_dcsr* upload_rows(stc_ctx* ctx, int64_t lo, int64_t hi, int64_t cols, const int64_t* indptr,
+                      const int32_t* indices, const double* values, int dtype) {
+  std::vector<int64_t> ip((size_t)(hi - lo + 1));
+  for (int64_t r = lo; r <= hi; ++r) ip[(size_t)(r - lo)] = indptr[r] - indptr[lo];
+  stc_dcsr* d = nullptr;
+  member_ok(stc_dcsr_upload(ctx, hi - lo, cols, ip.data(), indices ? indices + indptr[lo] : nullptr,
+                            values ? values + indptr[lo] : nullptr, dtype, &d));
+  return d;
+}
+void check_host_csr(int64_t rows, int64_t cols, const int64_t* indptr, const int32_t* indices,
+                    const double* values) {
+  STC_REQUIRE(indptr && rows >= 0, "indptr / rows");
+  STC_REQUIRE(indptr[rows] == 0 || (indices && values), "indices / values");
+  check_csr_host(rows, cols, indptr, indices);
+}
+
+}  // namespace
+
+extern "C" {
+
+int stc_group_create(const int* device_ids, int n_devices, const stc_lda_config* cfg, stc_group** out) {
+  return guard([&] {
+    STC_REQUIRE(device_ids && cfg && out, "device_ids/cfg/out");
+    STC_REQUIRE(n_devices >= 1 && n_devices <= kMaxMembers, "1 <= n_devices <= 16");
+    int nd = 0;
+    HIP_CHECK(hipGetDeviceCount(&nd));
+    bool same = true, distinct = true;
+    for (int i = 0; i < n_devices; ++i) {
+      STC_REQUIRE(device_ids[i] >= 0 && device_ids[i] < nd, "device index out of range");
+      same &= device_ids[i] == device_ids[0];
+      for (int j = 0; j < i; ++j) distinct &= device_ids[i] != device_ids[j];
+    }
+    STC_REQUIRE(same || distinct, "device_ids: all distinct (RCCL) or all the same device (in-process)");
+    auto g = std::make_unique<stc_group>();
+    struct Cleanup {
+      stc_group* g;
+      ~Cleanup() {
+        if (!g) return;
+        for (auto* l : g->lda) (void)stc_lda_destroy(l);
+        for (auto* c : g->ctx) (void)stc_destroy(c);
+      }
+    } cleanup{g.get()};
+    for (int i = 0; i < n_devices; ++i) {
+      stc_ctx* c = nullptr;
+      member_ok(stc_init(device_ids[i], &c));
+      g->ctx.push_back(c);
+    }
+    if (n_devices > 1 && same) {
+      g->local = std::make_unique<LocalColl>(n_devices);
+    }
+    if (n_devices > 1 || !same) {
+      std::vector<ncclComm_t> comms((size_t)n_devices, nullptr);
+      if (!g->local) RCCL_CHECK(ncclCommInitAll(comms.data(), n_devices, device_ids));
+      for (int i = 0; i < n_devices; ++i) {
+        g->ctx[(size_t)i]->comm = comms[(size_t)i];
+        g->ctx[(size_t)i]->local = g->local.get();
+        g->ctx[(size_t)i]->n_ranks = n_devices;
+        g->ctx[(size_t)i]->rank = i;
+      }
+    }
+    for (int i = 0; i < n_devices; ++i) {
+      stc_lda* l = nullptr;
+      member_ok(stc_lda_create(g->ctx[(size_t)i], cfg, &l));
+      g->lda.push_back(l);
+    }
+    g->dtype = g->lda[0]->dtype;
+    g->row0.assign((size_t)n_devices + 1, 0);
+    cleanup.g = nullptr;
+    *out = g.release();
+  });
+}
+
+int stc_group_destroy(stc_group* g) {
+  return guard([&] {
+    if (!g) return;
+    for (auto* l : g->lda) (void)stc_lda_destroy(l);
+    for (auto* d : g->shard) (void)stc_dcsr_free(d);
+    for (auto* c : g->ctx) {
+      c->local = nullptr;
+      (void)stc_destroy(c);
+    }
+    delete g;
+  });
+}
+
+int stc_group_size(const stc_group* g, int* n_out) {
+  return guard([&] {
+    STC_REQUIRE(g && n_out, "group/n_out");
+    *n_out = g->n();
+  });
+}
+
+int stc_group_member(stc_group* g, int i, stc_lda** lda_out) {
+  return guard([&] {
+    STC_REQUIRE(g && lda_out && i >= 0 && i < g->n(), "group/member index");
+    *lda_out = g->lda[(size_t)i];
+  });
+}
+
+int stc_group_set_corpus(stc_group* g, int64_t n_rows, int64_t n_cols, const int64_t* indptr, const int32_t* indices,
+                         const double* values) {
+  return guard([&] {
+    STC_REQUIRE(g, "group");
+    check_host_csr(n_rows, n_cols, indptr, indices, values);
+    const std::vector<int64_t> r0 = shard_rows(indptr, n_rows, g->n());
+    std::vector<stc_dcsr*> shard((size_t)g->n(), nullptr);
+    try {
+      for_members(*g, [&](int i) {
+        shard[(size_t)i] = upload_rows(g->ctx[(size_t)i], r0[(size_t)i], r0[(size_t)i + 1], n_cols, indptr, indices,
+                                       values, g->dtype);
+        member_ok(stc_lda_set_corpus(g->lda[(size_t)i], shard[(size_t)i], n_rows));
+      });
+    } catch (...) {
+      for (auto* d : shard) (void)stc_dcsr_free(d);
+      throw;
+    }
+    for (auto* d : g->shard) (void)stc_dcsr_free(d);
+    g->shard = shard;
+    g->row0 = r0;
+    g->rows = n_rows;
+    g->cols = n_cols;
+  });
+}
+
+int stc_group_init_random(stc_group* g, uint64_t seed) {
+  return guard([&] {
+    STC_REQUIRE(g, "group");
+    for_members(*g, [&](int i) { member_ok(stc_lda_init_random(g->lda[(size_t)i], seed)); });
+  });
+}
+
+int stc_group_set_topics(stc_group* g, const double* topics, int layout) {
+  return guard([&] {
+    STC_REQUIRE(g && topics, "group/topics");
+    for_members(*g, [&](int i) { member_ok(stc_lda_set_topics(g->lda[(size_t)i], topics, layout)); });
+  });
+}
+
+int stc_group_get_topics(stc_group* g, double* topics_out, int layout) {
+  return guard([&] {
+    STC_REQUIRE(g && topics_out, "group/topics_out");
+    // gathering the sharded λ is collective: member 0 copies it out, the others only take part
+    for_members(*g, [&](int i) {
+      if (i == 0) member_ok(stc_lda_get_topics(g->lda[0], topics_out, layout));
+      else gather_lambda(*g->lda[(size_t)i]);
+    });
+  });
+}
+
+int stc_group_get_alpha(stc_group* g, double* alpha_out) {
+  return guard([&] {
+    STC_REQUIRE(g && alpha_out, "group/alpha_out");
+    g->ctx[0]->use();
+    member_ok(stc_lda_get_alpha(g->lda[0], alpha_out));  // α is replicated on every member
+  });
+}
+
+int stc_group_get_iteration(stc_group* g, int64_t* iteration_out) {
+  return guard([&] {
+    STC_REQUIRE(g && iteration_out, "group/iteration_out");
+    *iteration_out = g->lda[0]->iteration;
+  });
+}
+
+static void merge_stats(stc_step_stats* out, const std::vector<stc_step_stats>& st) {
+  if (!out) return;
+  *out = stc_step_stats{};
+  for (const auto& s : st) {
+    out->batch_docs += s.batch_docs;
+    out->batch_entries += s.batch_entries;
+    out->inner_iters += s.inner_iters;
+    out->inner_iters_max = std::max(out->inner_iters_max, s.inner_iters_max);
+    out->cap_hits += s.cap_hits;
+  }
+  out->nonempty_docs = st[0].nonempty_docs;  // already summed over the members
+  out->rho = st[0].rho;
+}
+
+int stc_group_next(stc_group* g, stc_step_stats* stats) {
+  return guard([&] {
+    STC_REQUIRE(g, "group");
+    std::vector<stc_step_stats> st((size_t)g->n());
+    for_members(*g, [&](int i) { member_ok(stc_lda_next(g->lda[(size_t)i], stats ? &st[(size_t)i] : nullptr)); });
+    merge_stats(stats, st);
+  });
+}
+
+int stc_group_step(stc_group* g, const int64_t* batch_doc_ids, int64_t n, const double* gamma0, stc_step_stats* stats) {
+  return guard([&] {
+    STC_REQUIRE(g && (batch_doc_ids || n == 0) && n >= 0, "group/batch_doc_ids");
+    const int m = g->n();
+    const int64_t k = g->lda[0]->k;
+    std::vector<std::vector<int64_t>> ids((size_t)m);
+    std::vector<std::vector<double>> g0((size_t)m);
+    for (int64_t j = 0; j < n; ++j) {
+      const int64_t d = batch_doc_ids[j];
+      STC_REQUIRE(d >= 0 && d < g->rows, "batch doc id out of range");
+      const int q = (int)(std::upper_bound(g->row0.begin(), g->row0.end(), d) - g->row0.begin()) - 1;
+      ids[(size_t)q].push_back(d - g->row0[(size_t)q]);
+      if (gamma0) g0[(size_t)q].insert(g0[(size_t)q].end(), gamma0 + j * k, gamma0 + (j + 1) * k);
+    }
+    std::vector<stc_step_stats> st((size_t)m);
+    for_members(*g, [&](int i) {
+      const auto& v = ids[(size_t)i];
+      member_ok(stc_lda_step(g->lda[(size_t)i], v.data(), (int64_t)v.size(), gamma0 ? g0[(size_t)i].data() : nullptr,
+                             stats ? &st[(size_t)i] : nullptr));
+    });
+    merge_stats(stats, st);
+  });
+}
+
+int stc_group_describe(stc_group* g, int32_t max_terms, int32_t* idx_out, double* weight_out) {
+  return guard([&] {
+    STC_REQUIRE(g && idx_out && weight_out, "group/idx_out/weight_out");
+    for_members(*g, [&](int i) {
+      if (i == 0) member_ok(stc_lda_describe(g->lda[0], max_terms, idx_out, weight_out));
+      else gather_lambda(*g->lda[(size_t)i]);
+    });
+  });
+}
+
+int stc_group_bound(stc_group* g, int64_t n_rows, int64_t n_cols, const int64_t* indptr, const int32_t* indices,
+                    const double* values, uint64_t gamma_seed, int64_t doc_id_base, const double* gamma0,
+                    double* bound_out, double* corpus_part_out, double* topics_part_out, double* token_count_out) {
+  return guard([&] {
+    STC_REQUIRE(g && bound_out, "group/bound_out");
+    check_host_csr(n_rows, n_cols, indptr, indices, values);
+    const std::vector<int64_t> r0 = shard_rows(indptr, n_rows, g->n());
+    const int64_t k = g->lda[0]->k;
+    double res[4] = {0, 0, 0, 0};
+    for_members(*g, [&](int i) {
+      const int64_t lo = r0[(size_t)i], hi = r0[(size_t)i + 1];
+      stc_dcsr* d = upload_rows(g->ctx[(size_t)i], lo, hi, n_cols, indptr, indices, values, g->dtype);
+      double r[4] = {0, 0, 0, 0};
+      // every member's γ₀ keys continue the global row numbering (doc_id_base + row), so the bound is
+      // the one a single handle computes over all rows
+      const int rc = stc_lda_bound(g->lda[(size_t)i], d, gamma_seed, doc_id_base + lo, gamma0 ? gamma0 + lo * k : nullptr,
+                                   &r[0], &r[1], &r[2], &r[3]);
+      (void)stc_dcsr_free(d);
+      member_ok(rc);
+      if (i == 0) std::copy(r, r + 4, res);  // the bound is all-reduced: every member holds the total
+    });
+    *bound_out = res[0];
+    if (corpus_part_out) *corpus_part_out = res[1];
+    if (topics_part_out) *topics_part_out = res[2];
+    if (token_count_out) *token_count_out = res[3];
+  });
+}
+
+int stc_group_topic_distribution(stc_group* g, int64_t n_rows, int64_t n_cols, const int64_t* indptr,
+                                 const int32_t* indices, const double* values, uint64_t gamma_seed,
+                                 int64_t doc_id_base, const double* gamma0, double* out) {
+  return guard([&] {
+    STC_REQUIRE(g && out, "group/out");
+    check_host_csr(n_rows, n_cols, indptr, indices, values);
+    const std::vector<int64_t> r0 = shard_rows(indptr, n_rows, g->n());
+    const int64_t k = g->lda[0]->k;
+    for_members(*g, [&](int i) {
+      const int64_t lo = r0[(size_t)i], hi = r0[(size_t)i + 1];
+      stc_dcsr* d = upload_rows(g->ctx[(size_t)i], lo, hi, n_cols, indptr, indices, values, g->dtype);
+      const int rc = stc_lda_topic_distribution(g->lda[(size_t)i], d, gamma_seed, doc_id_base + lo,
+                                                gamma0 ? gamma0 + lo * k : nullptr, out + lo * k);
+      (void)stc_dcsr_free(d);
+      member_ok(rc);
+    });
   });
 }
 

@@ -97,14 +97,18 @@ struct DevBuf {
 // ---------------------------------------------------------------------------------------
 // Context: one device, one stream, optional RCCL communicator.
 // ---------------------------------------------------------------------------------------
+struct LocalColl;  // in-process collectives of the stc_group members that share one device (api.hip)
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
+  LocalColl* local = nullptr;  // set instead of comm for same-device group members (owned by the group)
   int n_ranks = 1;
   int rank = 0;
   DevBuf scratch[4];  // grow-only scratch of the featurisation kernels (hashing_tf.hip)
+  DevBuf coll_tmp;    // the in-process all-reduce's staging buffer
   void use() const { HIP_CHECK(hipSetDevice(device)); }
+  bool coll() const { return comm != nullptr || local != nullptr; }
 };
 
 struct DCsr {

@@ -112,6 +112,21 @@ SIGNATURES = {
     "stc_lda_enable_timing": (_int, [_p, _int]),
     "stc_lda_phase_times": (_int, [_p, _pdbl, _pi64]),
     "stc_lda_counters": (_int, [_p, _pi64]),
+    "stc_group_create": (_int, [_pi32, _int, C.POINTER(LdaConfig), C.POINTER(_p)]),
+    "stc_group_destroy": (_int, [_p]),
+    "stc_group_size": (_int, [_p, _pi32]),
+    "stc_group_member": (_int, [_p, _int, C.POINTER(_p)]),
+    "stc_group_set_corpus": (_int, [_p, _i64, _i64, _pi64, _pi32, _pdbl]),
+    "stc_group_init_random": (_int, [_p, _u64]),
+    "stc_group_set_topics": (_int, [_p, _pdbl, _int]),
+    "stc_group_get_topics": (_int, [_p, _pdbl, _int]),
+    "stc_group_get_alpha": (_int, [_p, _pdbl]),
+    "stc_group_get_iteration": (_int, [_p, _pi64]),
+    "stc_group_next": (_int, [_p, C.POINTER(StepStats)]),
+    "stc_group_step": (_int, [_p, _pi64, _i64, _pdbl, C.POINTER(StepStats)]),
+    "stc_group_describe": (_int, [_p, _i32, _pi32, _pdbl]),
+    "stc_group_bound": (_int, [_p, _i64, _i64, _pi64, _pi32, _pdbl, _u64, _i64, _pdbl, _pdbl, _pdbl, _pdbl, _pdbl]),
+    "stc_group_topic_distribution": (_int, [_p, _i64, _i64, _pi64, _pi32, _pdbl, _u64, _i64, _pdbl, _pdbl]),
 }
 
 

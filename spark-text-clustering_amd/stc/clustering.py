@@ -33,6 +33,31 @@ ML_LDA_DEFAULT_SEED = _java_string_hash("org.apache.spark.ml.clustering.LDA")
 _DTYPES = {"f32": L.STC_F32, "float32": L.STC_F32, "f64": L.STC_F64, "float64": L.STC_F64}
 
 
+def _lda_config(lib, k, vocab_size, doc_concentration, topic_concentration, tau0, kappa, mini_batch_fraction,
+                gamma_shape, optimize_doc_concentration, sample_with_replacement, seed, dtype, max_inner_iter):
+    """stc_lda_config from the Spark-ML parameters (returns the config and the α buffer it points to)."""
+    cfg = L.LdaConfig()
+    lib.stc_lda_config_default(C.byref(cfg))
+    cfg.k = int(k)
+    cfg.vocab_size = int(vocab_size)
+    alpha_buf = None
+    if doc_concentration is not None:
+        alpha_buf = L.as_f64(np.atleast_1d(doc_concentration))
+        cfg.doc_concentration = L.ptr(alpha_buf, C.c_double)
+        cfg.doc_concentration_len = alpha_buf.size
+    cfg.topic_concentration = float(-1.0 if topic_concentration is None else topic_concentration)
+    cfg.tau0 = float(tau0)
+    cfg.kappa = float(kappa)
+    cfg.mini_batch_fraction = float(mini_batch_fraction)
+    cfg.gamma_shape = float(gamma_shape)
+    cfg.optimize_doc_concentration = int(bool(optimize_doc_concentration))
+    cfg.sample_with_replacement = int(bool(sample_with_replacement))
+    cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    cfg.dtype = _DTYPES[dtype] if isinstance(dtype, str) else int(dtype)
+    cfg.max_inner_iter = int(max_inner_iter)
+    return cfg, alpha_buf
+
+
 class LdaHandle:
     """Owns one stc_lda (optimizer state + LocalLDAModel parameters on the GPU)."""
 
@@ -41,26 +66,9 @@ class LdaHandle:
                  optimize_doc_concentration=True, sample_with_replacement=True, seed=0,
                  dtype="f64", max_inner_iter=0):
         self.ctx = ctx
-        cfg = L.LdaConfig()
-        ctx.lib.stc_lda_config_default(C.byref(cfg))
-        cfg.k = int(k)
-        cfg.vocab_size = int(vocab_size)
-        self._alpha_buf = None
-        if doc_concentration is not None:
-            a = L.as_f64(np.atleast_1d(doc_concentration))
-            self._alpha_buf = a
-            cfg.doc_concentration = L.ptr(a, C.c_double)
-            cfg.doc_concentration_len = a.size
-        cfg.topic_concentration = float(-1.0 if topic_concentration is None else topic_concentration)
-        cfg.tau0 = float(tau0)
-        cfg.kappa = float(kappa)
-        cfg.mini_batch_fraction = float(mini_batch_fraction)
-        cfg.gamma_shape = float(gamma_shape)
-        cfg.optimize_doc_concentration = int(bool(optimize_doc_concentration))
-        cfg.sample_with_replacement = int(bool(sample_with_replacement))
-        cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
-        cfg.dtype = _DTYPES[dtype] if isinstance(dtype, str) else int(dtype)
-        cfg.max_inner_iter = int(max_inner_iter)
+        cfg, self._alpha_buf = _lda_config(ctx.lib, k, vocab_size, doc_concentration, topic_concentration, tau0,
+                                           kappa, mini_batch_fraction, gamma_shape, optimize_doc_concentration,
+                                           sample_with_replacement, seed, dtype, max_inner_iter)
         h = C.c_void_p()
         L.check(ctx.lib.stc_lda_create(ctx.handle, C.byref(cfg), C.byref(h)))
         self.handle = h
@@ -183,6 +191,109 @@ class LdaHandle:
             self.close()
         except Exception:
             pass
+
+
+class LdaGroup:
+    """Owns one stc_group: the LDA over several devices from ONE process (stc_group_create; the JVM
+    drop-in's multi-GPU form).  The corpus is given on the host and sharded by the library; document ids
+    are global.  ``devices`` repeating one device runs the multi-GPU decomposition on that device."""
+
+    def __init__(self, devices, k, vocab_size, doc_concentration=None, topic_concentration=-1.0, tau0=1024.0,
+                 kappa=0.51, mini_batch_fraction=0.05, gamma_shape=100.0, optimize_doc_concentration=True,
+                 sample_with_replacement=True, seed=0, dtype="f64", max_inner_iter=0):
+        self.lib = L.load()
+        cfg, self._alpha_buf = _lda_config(self.lib, k, vocab_size, doc_concentration, topic_concentration, tau0,
+                                           kappa, mini_batch_fraction, gamma_shape, optimize_doc_concentration,
+                                           sample_with_replacement, seed, dtype, max_inner_iter)
+        devs = np.ascontiguousarray(np.asarray(devices, np.int32))
+        h = C.c_void_p()
+        L.check(self.lib.stc_group_create(L.ptr(devs, C.c_int32), devs.size, C.byref(cfg), C.byref(h)))
+        self.handle = h
+        self.devices = devs.tolist()
+        self.k, self.vocab_size = cfg.k, cfg.vocab_size
+
+    @staticmethod
+    def _csr(m: CsrMatrix):
+        return (L.as_i64(m.indptr), np.ascontiguousarray(m.indices, np.int32), L.as_f64(m.values))
+
+    def set_corpus(self, corpus: CsrMatrix):
+        ip, ix, v = self._csr(corpus)
+        L.check(self.lib.stc_group_set_corpus(self.handle, corpus.num_rows, corpus.num_cols, L.ptr(ip, C.c_int64),
+                                              L.ptr(ix, C.c_int32), L.ptr(v, C.c_double)))
+
+    def init_random(self, seed):
+        L.check(self.lib.stc_group_init_random(self.handle, int(seed) & 0xFFFFFFFFFFFFFFFF))
+
+    def set_topics(self, topics, layout=L.STC_LAYOUT_VK):
+        t = L.as_f64(topics)
+        L.check(self.lib.stc_group_set_topics(self.handle, L.ptr(t, C.c_double), layout))
+
+    def topics(self, layout=L.STC_LAYOUT_VK):
+        shape = (self.vocab_size, self.k) if layout == L.STC_LAYOUT_VK else (self.k, self.vocab_size)
+        out = np.zeros(shape, np.float64)
+        L.check(self.lib.stc_group_get_topics(self.handle, L.ptr(out, C.c_double), layout))
+        return out
+
+    def alpha(self):
+        out = np.zeros(self.k, np.float64)
+        L.check(self.lib.stc_group_get_alpha(self.handle, L.ptr(out, C.c_double)))
+        return out
+
+    def iteration(self):
+        x = C.c_int64()
+        L.check(self.lib.stc_group_get_iteration(self.handle, C.byref(x)))
+        return x.value
+
+    def step(self, batch_ids, gamma0=None, stats=True):
+        ids = L.as_i64(batch_ids)
+        g0 = None if gamma0 is None else L.as_f64(gamma0)
+        st = L.StepStats() if stats else None
+        L.check(self.lib.stc_group_step(self.handle, L.ptr(ids, C.c_int64), ids.size, L.ptr(g0, C.c_double),
+                                        C.byref(st) if stats else None))
+        return st.as_dict() if stats else None
+
+    def next(self, stats=True):
+        st = L.StepStats() if stats else None
+        L.check(self.lib.stc_group_next(self.handle, C.byref(st) if stats else None))
+        return st.as_dict() if stats else None
+
+    def describe(self, max_terms=10):
+        n = min(int(max_terms), self.vocab_size)
+        idx = np.zeros((self.k, n), np.int32)
+        w = np.zeros((self.k, n), np.float64)
+        L.check(self.lib.stc_group_describe(self.handle, int(max_terms), L.ptr(idx, C.c_int32), L.ptr(w, C.c_double)))
+        return idx, w
+
+    def bound(self, docs: CsrMatrix, gamma_seed=0, doc_id_base=0, gamma0=None):
+        ip, ix, v = self._csr(docs)
+        g0 = None if gamma0 is None else L.as_f64(gamma0)
+        b, cp, tp, tok = C.c_double(), C.c_double(), C.c_double(), C.c_double()
+        L.check(self.lib.stc_group_bound(self.handle, docs.num_rows, docs.num_cols, L.ptr(ip, C.c_int64),
+                                         L.ptr(ix, C.c_int32), L.ptr(v, C.c_double),
+                                         int(gamma_seed) & 0xFFFFFFFFFFFFFFFF, int(doc_id_base),
+                                         L.ptr(g0, C.c_double), C.byref(b), C.byref(cp), C.byref(tp), C.byref(tok)))
+        return {"bound": b.value, "corpus_part": cp.value, "topics_part": tp.value, "token_count": tok.value}
+
+    def topic_distribution(self, docs: CsrMatrix, gamma_seed=0, doc_id_base=0, gamma0=None):
+        ip, ix, v = self._csr(docs)
+        g0 = None if gamma0 is None else L.as_f64(gamma0)
+        out = np.zeros((docs.num_rows, self.k), np.float64)
+        L.check(self.lib.stc_group_topic_distribution(self.handle, docs.num_rows, docs.num_cols, L.ptr(ip, C.c_int64),
+                                                      L.ptr(ix, C.c_int32), L.ptr(v, C.c_double),
+                                                      int(gamma_seed) & 0xFFFFFFFFFFFFFFFF, int(doc_id_base),
+                                                      L.ptr(g0, C.c_double), L.ptr(out, C.c_double)))
+        return out
+
+    def close(self):
+        if self.handle:
+            self.lib.stc_group_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def _as_device(ctx, data, dtype):

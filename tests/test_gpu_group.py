@@ -1,0 +1,96 @@
+"""GPU: the single-process multi-device handle (stc_group — SURVEY.md §8(b); the JVM drop-in's multi-GPU
+form) against a single handle on the same inputs.
+
+The box has one GPU, so the groups here repeat device 0: the members run the multi-GPU decomposition
+(document shards, the stat reduce-scatter, the vocabulary-sliced λ update, the colsum / expElogβ' /
+logscale all-gathers, the sharded bound) on one device through the in-process transport — the same call
+sequence RCCL carries between distinct devices.  A one-member group is the plain single-GPU path.
+Tolerances: fp64, only the summation order of sstats across shards differs (1e-12 relative on λ)."""
+import numpy as np
+import pytest
+
+from helpers import random_corpus
+
+pytestmark = pytest.mark.gpu
+
+
+def _single(ctx, corpus, k, lam, **kw):
+    import stc
+
+    h = stc.LdaHandle(ctx, k, corpus.num_cols, dtype="f64", **kw)
+    d = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F64)
+    h.set_corpus(d, corpus.num_rows)
+    h.set_topics(lam)
+    return h, d
+
+
+@pytest.mark.parametrize("members", [1, 2, 3, 4])
+def test_group_steps_match_a_single_handle(ctx, members):
+    """Injected membership (global ids, duplicates included) and γ₀: λ, α and the iteration count after
+    three steps; then describeTopics, the bound and topicDistribution over held-out rows."""
+    import stc
+
+    rng = np.random.default_rng(100 + members)
+    D, V, k = 240, 3000, 40
+    corpus = random_corpus(rng, D, V, 1, 160, empty_every=17)
+    lam = rng.gamma(100.0, 0.01, size=(V, k))
+    kw = dict(mini_batch_fraction=0.3, optimize_doc_concentration=True)
+    h, d = _single(ctx, corpus, k, lam, **kw)
+    with stc.LdaGroup([0] * members, k, V, dtype="f64", **kw) as g:
+        g.set_corpus(corpus)
+        g.set_topics(lam)
+        for it in range(3):
+            ids = rng.integers(0, D, size=90)
+            g0 = rng.gamma(100.0, 0.01, size=(ids.size, k))
+            sh = h.step(ids, g0)
+            sg = g.step(ids, g0)
+            assert sg["batch_docs"] == sh["batch_docs"] and sg["nonempty_docs"] == sh["nonempty_docs"]
+            # step 1 starts from the same λ (identical per-document E-steps); later steps from λ that
+            # differs in the last bits (stat summed in shard order), where a document on the stop rule's
+            # boundary may take one more or one fewer iteration
+            assert abs(sg["inner_iters"] - sh["inner_iters"]) <= (0 if it == 0 else 2)
+        np.testing.assert_allclose(g.topics(), h.topics(), rtol=1e-12)
+        np.testing.assert_allclose(g.alpha(), h.alpha(), rtol=1e-12)
+        assert g.iteration() == h.iteration() == 3
+        ig, wg = g.describe(10)
+        ih, wh = h.describe(10)
+        assert np.array_equal(ig, ih)
+        np.testing.assert_allclose(wg, wh, rtol=1e-12)
+        held = random_corpus(rng, 70, V, 0, 120, empty_every=11)
+        dh = stc.DeviceCsr.upload(ctx, held, stc.STC_F64)
+        bh = h.bound(dh, gamma_seed=7, doc_id_base=1000)
+        bg = g.bound(held, gamma_seed=7, doc_id_base=1000)
+        np.testing.assert_allclose(bg["bound"], bh["bound"], rtol=1e-11)
+        assert bg["token_count"] == bh["token_count"]
+        np.testing.assert_allclose(g.topic_distribution(held, gamma_seed=7, doc_id_base=1000),
+                                   h.topic_distribution(dh, gamma_seed=7, doc_id_base=1000), rtol=1e-10, atol=1e-14)
+        dh.free()
+
+
+def test_group_next_trains_every_member(ctx):
+    """next(): each member samples its own shard; the global batch, the shared λ and α move together."""
+    import stc
+
+    rng = np.random.default_rng(3)
+    D, V, k = 400, 2048, 24
+    corpus = random_corpus(rng, D, V, 1, 100)
+    with stc.LdaGroup([0, 0, 0], k, V, dtype="f64", mini_batch_fraction=0.2, seed=11) as g:
+        g.set_corpus(corpus)
+        g.init_random(11)
+        lam0 = g.topics()
+        total = 0
+        for _ in range(4):
+            st = g.next()
+            total += st["batch_docs"]
+        assert g.iteration() == 4 and total > 0.1 * 4 * D
+        assert not np.array_equal(g.topics(), lam0)
+        assert np.all(np.isfinite(g.topics())) and np.all(g.alpha() > 0)
+
+
+def test_group_argument_errors(ctx):
+    import stc
+
+    with pytest.raises(stc.StcIllegalArgument):
+        stc.LdaGroup([0, 99], 8, 100)
+    with pytest.raises(stc.StcIllegalArgument):
+        stc.LdaGroup([], 8, 100)
