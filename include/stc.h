@@ -98,7 +98,10 @@ int stc_comm_init(stc_ctx* ctx, const uint8_t id[128], int n_ranks, int rank);
 int stc_comm_allreduce_f64(stc_ctx* ctx, double* host_inout, int64_t n); /* host scalars */
 
 /* ---- device CSR ------------------------------------------------------------------------- */
-/* values are stored on device as `value_dtype` (STC_F32 or STC_F64) */
+/* values are stored on device as `value_dtype` (STC_F32 or STC_F64).  A device object (stc_dcsr,
+ * stc_dtok) belongs to the stc_ctx that made it: every call that reads it requires that same ctx (or an
+ * LDA handle created on it) and returns STC_ERR_INVALID_ARG otherwise.  The *_free calls remember the
+ * device, not the ctx, so they remain valid after stc_destroy of the owning context. */
 int stc_dcsr_upload(stc_ctx* ctx, int64_t n_rows, int64_t n_cols, const int64_t* indptr,
                     const int32_t* indices, const double* values, int value_dtype,
                     stc_dcsr** out);

@@ -9,8 +9,10 @@ import org.apache.spark.sql.Dataset
  * [U] spark-mllib 2.4.3 ml.clustering.LDA (k = 10, maxIter = 20, learningOffset = 1024,
  * learningDecay = 0.51, subsamplingRate = 0.05, optimizeDocConcentration = true, seed, docConcentration,
  * topicConcentration), the same fit() construction of the mllib LDA — only the optimizer is
- * HipOnlineLDAOptimizer — and the same result: a stock LocalLDAModel (topicsMatrix, describeTopics,
- * logLikelihood, logPerplexity, transform, save/load work unchanged).
+ * HipOnlineLDAOptimizer — and the same result type: an ml LocalLDAModel wrapping the mllib
+ * HipLocalLDAModel, so describeTopics, logLikelihood and logPerplexity run on the GPUs that trained it
+ * (topicsMatrix, transform and save/load are Spark's own).  setDevices spreads training over several GPUs
+ * of this JVM; close the returned model's oldLocalModel (HipLocalLDAModel.close) to release them.
  *
  * {{{
  *   val model = new HipLDA().setK(100).setMaxIter(50).setSeed(1L).setFeaturesCol("features").fit(tfidf)
@@ -23,6 +25,9 @@ class HipLDA(override val uid: String) extends LDA(uid) {
   private var dtype: String = "f64"
   def setDtype(d: String): this.type = { dtype = d; this }
 
+  private var devices: Array[Int] = Array(0)
+  def setDevices(ds: Array[Int]): this.type = { devices = ds.clone(); this }
+
   override def fit(dataset: Dataset[_]): LDAModel = {
     transformSchema(dataset.schema, logging = true)
     require($(optimizer).toLowerCase == "online", s"HipLDA trains the online optimizer only, got ${$(optimizer)}")
@@ -32,6 +37,7 @@ class HipLDA(override val uid: String) extends LDA(uid) {
       .setMiniBatchFraction($(subsamplingRate))
       .setOptimizeDocConcentration($(optimizeDocConcentration))
       .setDtype(dtype)
+      .setDevices(devices)
     val oldLDA = new OldLDA()
       .setK($(k))
       .setDocConcentration(getOldDocConcentration)
@@ -41,6 +47,7 @@ class HipLDA(override val uid: String) extends LDA(uid) {
       .setCheckpointInterval($(checkpointInterval))
       .setOptimizer(opt)
     val oldData = LDA.getOldDataset(dataset, $(featuresCol))
+    // the trained HipLocalLDAModel owns the device group; close() frees it only if training failed
     val oldModel = try oldLDA.run(oldData).asInstanceOf[OldLocalLDAModel] finally opt.close()
     copyValues(new LocalLDAModel(uid, oldModel.vocabSize, oldModel, dataset.sparkSession).setParent(this))
   }

@@ -1,0 +1,117 @@
+package org.apache.spark.mllib.clustering
+
+import org.apache.spark.mllib.linalg.{Matrix, Vector, Vectors}
+import org.apache.spark.rdd.RDD
+
+/**
+ * The LocalLDAModel HipOnlineLDAOptimizer.getLDAModel returns: a stock [U] spark-mllib 2.4.3
+ * LocalLDAModel (topicsMatrix, save/load, serialisation and ml.clustering.LocalLDAModel.transform are
+ * Spark's own) whose inference calls run on the GPU group that trained it, where λ is still resident:
+ *
+ *   describeTopics      → stc_group_describe   (the reference's LDAClustering.scala describeTopics call)
+ *   logLikelihood       → stc_group_bound      (LocalLDAModel.logLikelihoodBound: corpus part + topics part)
+ *   logPerplexity       → stc_group_bound      (−bound / token count, one device pass instead of two RDD jobs)
+ *   topicDistribution(s)→ stc_group_topic_distribution (zeros for empty documents, as Spark)
+ *
+ * The documents of an RDD call are collected to the driver (the reference runs local[*], one JVM:
+ * LDATraining.scala:7) and sharded over the group's devices.  γ₀ of document i (its position in the
+ * collected RDD) comes from the counter RNG keyed (getSeed, i) — a seeded draw from Spark's
+ * Gamma(gammaShape, 1/gammaShape), not Breeze's generator stream, so results equal Spark's to the
+ * E-step's convergence tolerance, not bit for bit (DESIGN.md §3).
+ *
+ * The group handle is transient: a deserialised copy, or one after close(), has none and every method
+ * falls back to Spark's CPU implementation.
+ */
+final class HipLocalLDAModel private[clustering] (
+    topicsM: Matrix,
+    alphaV: Vector,
+    etaV: Double,
+    shape: Double,
+    @transient private var group: Long)
+  extends LocalLDAModel(topicsM, alphaV, etaV, shape) {
+
+  /** true while the model's λ is resident on the GPU group */
+  def onDevice: Boolean = group != 0L
+
+  /** Releases the GPU group (the model keeps its host copy of λ and falls back to the CPU). */
+  def close(): Unit = {
+    if (group != 0L) StcNative.groupDestroy(group)
+    group = 0L
+  }
+
+  override def describeTopics(maxTermsPerTopic: Int): Array[(Array[Int], Array[Double])] = {
+    if (group == 0L) return super.describeTopics(maxTermsPerTopic)
+    val n = math.max(0, math.min(maxTermsPerTopic, vocabSize))
+    val idx = new Array[Int](k * n)
+    val w = new Array[Double](k * n)
+    StcNative.groupDescribe(group, maxTermsPerTopic, idx, w)
+    Array.tabulate(k)(t => (idx.slice(t * n, (t + 1) * n), w.slice(t * n, (t + 1) * n)))
+  }
+
+  private def collectCsr(documents: RDD[(Long, Vector)]): (Array[Long], Array[Vector], Array[AnyRef]) = {
+    val docs = documents.collect()
+    val rows = docs.map(_._2)
+    rows.foreach(v => require(v.size == vocabSize, s"document of size ${v.size}, the model has $vocabSize terms"))
+    (docs.map(_._1), rows, StcNative.toCsr(rows))
+  }
+
+  /** {bound, corpusPart, topicsPart, tokenCount} of the documents on the GPU */
+  private def deviceBound(documents: RDD[(Long, Vector)]): Array[Double] = {
+    val (_, rows, csr) = collectCsr(documents)
+    StcNative.groupBound(group, rows.length, vocabSize, csr(0).asInstanceOf[Array[Long]],
+      csr(1).asInstanceOf[Array[Int]], csr(2).asInstanceOf[Array[Double]], getSeed, 0L, null)
+  }
+
+  override def logLikelihood(documents: RDD[(Long, Vector)]): Double =
+    if (group == 0L) super.logLikelihood(documents) else deviceBound(documents)(0)
+
+  override def logPerplexity(documents: RDD[(Long, Vector)]): Double = {
+    if (group == 0L) return super.logPerplexity(documents)
+    val r = deviceBound(documents)
+    -r(0) / r(3)
+  }
+
+  override def topicDistributions(documents: RDD[(Long, Vector)]): RDD[(Long, Vector)] = {
+    if (group == 0L) return super.topicDistributions(documents)
+    val (ids, rows, csr) = collectCsr(documents)
+    val out = new Array[Double](rows.length * k)
+    StcNative.groupTopicDistribution(group, rows.length, vocabSize, csr(0).asInstanceOf[Array[Long]],
+      csr(1).asInstanceOf[Array[Int]], csr(2).asInstanceOf[Array[Double]], getSeed, 0L, null, out)
+    val theta = Array.tabulate(rows.length)(i => (ids(i), Vectors.dense(out.slice(i * k, (i + 1) * k))))
+    documents.sparkContext.parallelize(theta, math.max(1, documents.getNumPartitions))
+  }
+
+  override def topicDistribution(document: Vector): Vector = {
+    if (group == 0L) return super.topicDistribution(document)
+    require(document.size == vocabSize, s"document of size ${document.size}, the model has $vocabSize terms")
+    val csr = StcNative.toCsr(Array(document))
+    val out = new Array[Double](k)
+    StcNative.groupTopicDistribution(group, 1, vocabSize, csr(0).asInstanceOf[Array[Long]],
+      csr(1).asInstanceOf[Array[Int]], csr(2).asInstanceOf[Array[Double]], getSeed, 0L, null, out)
+    Vectors.dense(out)
+  }
+}
+
+object HipLocalLDAModel {
+  /**
+   * A GPU copy of an already trained model, e.g. the reference's LDALoader.scala:108
+   * `LDATrainedModel.toLocal.topicDistribution(v)` becomes
+   * `HipLocalLDAModel.fromLocal(LDATrainedModel.toLocal).topicDistribution(v)`.  λ (topicsMatrix), α, η
+   * and gammaShape are the model's; the group holds no corpus (inference only).
+   */
+  def fromLocal(m: LocalLDAModel, devices: Array[Int] = Array(0), dtype: Int = StcNative.F64): HipLocalLDAModel = {
+    val g = StcNative.groupCreate(devices, m.k, m.vocabSize, m.docConcentration.toArray, m.topicConcentration,
+      1024, 0.51, 0.05, m.gammaShape, false, true, m.getSeed, dtype, 0)
+    try {
+      // topicsMatrix is V×k column-major = k×V row-major (LAYOUT_KV)
+      StcNative.groupSetTopics(g, m.topicsMatrix.toArray, StcNative.LAYOUT_KV)
+    } catch {
+      case e: Throwable =>
+        StcNative.groupDestroy(g)
+        throw e
+    }
+    val h = new HipLocalLDAModel(m.topicsMatrix, m.docConcentration, m.topicConcentration, m.gammaShape, g)
+    h.setSeed(m.getSeed)
+    h
+  }
+}

@@ -24,10 +24,16 @@ import org.apache.spark.rdd.RDD
  * E-step computes in Double like Breeze (setDtype("f32") selects the fp32 kernels).
  *
  * Layout: the reference runs Spark local[*] (LDATraining.scala:7), one JVM: initialize collects the
- * corpus once into CSR arrays and uploads it to the GPU, where it stays for every next().  In a
- * multi-executor deployment each executor owns one GPU and a partition: rank 0's
+ * corpus once into CSR arrays and hands it to a device group (stc_group_*: setDevices(0, 1, …), default
+ * device 0), which shards the documents over its GPUs, where they stay for every next().  A group of N
+ * devices runs the multi-GPU decomposition — per-device Poisson draws, the stat reduce-scatter, the
+ * vocabulary-sliced λ update and its all-gathers — over RCCL when the devices differ.  In a
+ * multi-executor deployment each executor instead owns one GPU and a partition: rank 0's
  * StcNative.commUniqueId is broadcast, every executor calls commInit, uploads its partition and
- * passes the global corpus size to ldaSetCorpus — stc_lda_next then all-reduces the sstats over RCCL.
+ * passes the global corpus size to ldaSetCorpus.
+ *
+ * getLDAModel returns a HipLocalLDAModel that takes the group over: its describeTopics,
+ * logLikelihood, logPerplexity and topicDistribution(s) run on the GPUs where λ already is.
  */
 final class HipOnlineLDAOptimizer extends LDAOptimizer {
   private var tau0: Double = 1024
@@ -37,11 +43,9 @@ final class HipOnlineLDAOptimizer extends LDAOptimizer {
   private var gammaShape: Double = 100
   private var sampleWithReplacement: Boolean = true
   private var dtype: Int = StcNative.F64
-  private var device: Int = 0
+  private var devices: Array[Int] = Array(0)
 
-  private var ctx: Long = 0L
-  private var corpus: Long = 0L
-  private var handle: Long = 0L
+  private var group: Long = 0L
   private var k: Int = 0
   private var vocabSize: Int = 0
 
@@ -88,7 +92,15 @@ final class HipOnlineLDAOptimizer extends LDAOptimizer {
     this
   }
 
-  def setDevice(d: Int): this.type = { device = d; this }
+  def setDevice(d: Int): this.type = setDevices(Array(d))
+
+  /** the GPUs of the group, one document shard each (a repeated id runs several shards on one GPU) */
+  def setDevices(ds: Array[Int]): this.type = {
+    require(ds.nonEmpty, "at least one device")
+    devices = ds.clone()
+    this
+  }
+  def getDevices: Array[Int] = devices.clone()
 
   override private[clustering] def initialize(docs: RDD[(Long, Vector)], lda: LDA): HipOnlineLDAOptimizer = {
     k = lda.getK
@@ -96,41 +108,40 @@ final class HipOnlineLDAOptimizer extends LDAOptimizer {
     val alpha = lda.getAsymmetricDocConcentration.toArray  // length 1 (−1 ⇒ 1/k) or k, resolved in C
     val rows = docs.sortByKey().values.collect()
     val csr = StcNative.toCsr(rows)
-    ctx = StcNative.init(device)
-    corpus = StcNative.dcsrUpload(ctx, rows.length, vocabSize, csr(0).asInstanceOf[Array[Long]],
-      csr(1).asInstanceOf[Array[Int]], csr(2).asInstanceOf[Array[Double]], dtype)
-    handle = StcNative.ldaCreate(ctx, k, vocabSize, alpha, lda.getTopicConcentration, tau0, kappa,
+    close()
+    group = StcNative.groupCreate(devices, k, vocabSize, alpha, lda.getTopicConcentration, tau0, kappa,
       miniBatchFraction, gammaShape, optimizeDocConcentration, sampleWithReplacement, lda.getSeed, dtype, 0)
-    StcNative.ldaSetCorpus(handle, corpus, rows.length)
-    StcNative.ldaInitRandom(handle, lda.getSeed)  // λ₀ ~ Gamma(gammaShape, 1/gammaShape)
+    StcNative.groupSetCorpus(group, rows.length, vocabSize, csr(0).asInstanceOf[Array[Long]],
+      csr(1).asInstanceOf[Array[Int]], csr(2).asInstanceOf[Array[Double]])
+    StcNative.groupInitRandom(group, lda.getSeed)  // λ₀ ~ Gamma(gammaShape, 1/gammaShape)
     this
   }
 
   /** One OnlineLDAOptimizer.next(): sample → E-step → sstats → (RCCL) → λ / α update, on the GPU. */
   override private[clustering] def next(): HipOnlineLDAOptimizer = {
-    StcNative.ldaNext(handle, null)
+    StcNative.groupNext(group, null)
     this
   }
 
   override private[clustering] def getLDAModel(iterationTimes: Array[Double]): LDAModel = {
     val topics = new Array[Double](vocabSize * k)  // k×V row-major = V×k column-major (Matrices.dense)
-    StcNative.ldaGetTopics(handle, topics, StcNative.LAYOUT_KV)
+    StcNative.groupGetTopics(group, topics, StcNative.LAYOUT_KV)
     val alpha = new Array[Double](k)
-    StcNative.ldaGetAlpha(handle, alpha)
-    val eta = StcNative.ldaGetEta(handle)
-    new LocalLDAModel(Matrices.dense(vocabSize, k, topics), Vectors.dense(alpha), eta, gammaShape)
+    StcNative.groupGetAlpha(group, alpha)
+    val eta = StcNative.ldaGetEta(StcNative.groupMember(group, 0))
+    // the model owns the group from here on (HipLocalLDAModel.close releases it)
+    val model = new HipLocalLDAModel(Matrices.dense(vocabSize, k, topics), Vectors.dense(alpha), eta, gammaShape,
+      group)
+    group = 0L
+    model
   }
 
-  /** The live GPU model (describeTopics / topicDistribution / logLikelihood on the device). */
-  def deviceHandle: Long = handle
+  /** The live device group until getLDAModel hands it to the model (0 afterwards). */
+  def deviceHandle: Long = group
 
-  /** Releases the device model, corpus and context. */
+  /** Releases the device group if no model took it (idempotent). */
   def close(): Unit = {
-    if (handle != 0L) StcNative.ldaDestroy(handle)
-    if (corpus != 0L) StcNative.dcsrFree(corpus)
-    if (ctx != 0L) StcNative.destroy(ctx)
-    handle = 0L
-    corpus = 0L
-    ctx = 0L
+    if (group != 0L) StcNative.groupDestroy(group)
+    group = 0L
   }
 }

@@ -32,7 +32,8 @@ using namespace stc;
 struct stc_ctx : Ctx {};
 struct stc_dcsr : DCsr {};
 struct stc_dtok {
-  Ctx* ctx = nullptr;
+  Ctx* ctx = nullptr;  // the context it was uploaded on; only it may read the buffers
+  int device = -1;     // for stc_tokens_free, which may run after that context is gone
   DevBuf utf8, tok_off, doc_off;
   int64_t n_bytes = 0, n_tok = 0, n_docs = 0;
 };
@@ -428,7 +429,7 @@ lda::EStepArgs<T> estep_args(stc_lda& L) {
 
 // the register-resident kernel for the (k, dtype): the grid kernels up to k = 128 (fp32) / 104 (fp64),
 // the topics-across-lanes kernel (lda_wide.hip) beyond
-bool use_wide(int k, int dtype) { return dtype == STC_F32 ? lda::wave_row_cap(k) == 0 : lda::grid64_row_cap(k) == 0; }
+bool use_wide(int k, int dtype) { return dtype == STC_F32 ? lda::grid_row_cap(k) == 0 : lda::rows64_row_cap(k) == 0; }
 
 // the fast kernel's slots [0, n_short) in descending nnz: the longest documents start first, so the
 // launch does not end on a few long documents started late (longest-processing-time-first).  Each
@@ -599,7 +600,7 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
     if (team) {
       // launched (a refused cooperative grid falls through to the one-CU kernel)
     } else if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
-    else if constexpr (std::is_same<T, float>::value) lda::launch_estep_wave(s, w, stats, bound);
+    else if constexpr (std::is_same<T, float>::value) lda::launch_estep_grid(s, w, stats, bound);
     else if (use_old_grid64()) lda::launch_estep_grid64(s, w, stats, bound, m.max_row < 0 || m.max_row > lda::grid64_onchip_rows(L.k));
     else lda::launch_estep_rows64(s, w, stats, bound, m.max_row < 0 || m.max_row > lda::rows64_onchip_rows(L.k));
   }
@@ -1130,6 +1131,7 @@ int stc_dcsr_upload(stc_ctx* ctx, int64_t n_rows, int64_t n_cols, const int64_t*
     ctx->use();
     auto m = std::make_unique<stc_dcsr>();
     m->ctx = ctx;
+    m->device = ctx->device;
     m->rows = n_rows;
     m->cols = n_cols;
     m->nnz = nnz;
@@ -1169,6 +1171,7 @@ int stc_dcsr_shape(const stc_dcsr* m, int64_t* n_rows, int64_t* n_cols, int64_t*
 int stc_dcsr_download(stc_ctx* ctx, const stc_dcsr* m, int64_t* indptr, int32_t* indices, double* values) {
   return guard([&] {
     STC_REQUIRE(ctx && m, "ctx/m");
+    STC_REQUIRE(m->ctx == ctx, "the matrix belongs to another stc_ctx");
     ctx->use();
     hipStream_t s = ctx->stream;
     if (indptr) HIP_CHECK(hipMemcpyAsync(indptr, m->indptr.p, 8 * (m->rows + 1), hipMemcpyDeviceToHost, s));
@@ -1190,7 +1193,7 @@ int stc_dcsr_download(stc_ctx* ctx, const stc_dcsr* m, int64_t* indptr, int32_t*
 int stc_dcsr_free(stc_dcsr* m) {
   return guard([&] {
     if (!m) return;
-    if (m->ctx) (void)hipSetDevice(m->ctx->device);
+    if (m->device >= 0) (void)hipSetDevice(m->device);
     delete m;
   });
 }
@@ -1228,6 +1231,7 @@ int stc_tokens_upload(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const 
     ctx->use();
     auto t = std::make_unique<stc_dtok>();
     t->ctx = ctx;
+    t->device = ctx->device;
     TokenUpload u;
     upload_tokens(*ctx, u, utf8, n_bytes, tok_off, n_tok, doc_off, n_docs);
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
@@ -1247,7 +1251,7 @@ int stc_tokens_upload(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const 
 int stc_tokens_free(stc_dtok* t) {
   return guard([&] {
     if (!t) return;
-    if (t->ctx) (void)hipSetDevice(t->ctx->device);
+    if (t->device >= 0) (void)hipSetDevice(t->device);
     delete t;
   });
 }
@@ -1256,12 +1260,14 @@ int stc_hashing_tf_tokens(stc_ctx* ctx, const stc_dtok* tokens, int32_t num_feat
                           int hash_variant, int value_dtype, stc_dcsr** out) {
   return guard([&] {
     STC_REQUIRE(ctx && tokens && out, "ctx/tokens/out");
+    STC_REQUIRE(tokens->ctx == ctx, "tokens were uploaded on another stc_ctx");
     STC_REQUIRE(num_features > 0, "numFeatures must be > 0");
     STC_REQUIRE(hash_variant == STC_HASH_STANDARD || hash_variant == STC_HASH_SPARK24, "hash_variant");
     STC_REQUIRE(value_dtype == STC_F32 || value_dtype == STC_F64, "value_dtype");
     ctx->use();
     auto m = std::make_unique<stc_dcsr>();
     m->ctx = ctx;
+    m->device = ctx->device;
     hashing::build_csr(*ctx, tokens->utf8.as<uint8_t>(), tokens->tok_off.as<int64_t>(), tokens->n_tok,
                        tokens->doc_off.as<int64_t>(), tokens->n_docs, num_features, binary, hash_variant,
                        value_dtype, *m);
@@ -1300,6 +1306,7 @@ int stc_hashing_tf_dev(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const
     upload_tokens(*ctx, u, utf8, n_bytes, tok_off, n_tok, doc_off, n_docs);
     auto m = std::make_unique<stc_dcsr>();
     m->ctx = ctx;
+    m->device = ctx->device;
     hashing::build_csr(*ctx, u.utf8.as<uint8_t>(), u.tok_off.as<int64_t>(), n_tok, u.doc_off.as<int64_t>(),
                        n_docs, num_features, binary, hash_variant, value_dtype, *m);
     *out = m.release();
@@ -1382,6 +1389,7 @@ int stc_tokenize_hashing_tf_dev(stc_ctx* ctx, const uint8_t* text, int64_t n_byt
     run_tokenizer(*ctx, t, text, n_bytes, text_off, n_docs);
     auto m = std::make_unique<stc_dcsr>();
     m->ctx = ctx;
+    m->device = ctx->device;
     hashing::build_csr(*ctx, t.utf8.as<uint8_t>(), t.tok_off.as<int64_t>(), t.n_tok, t.doc_off.as<int64_t>(),
                        n_docs, num_features, binary, hash_variant, value_dtype, *m);
     *out = m.release();
@@ -1393,6 +1401,7 @@ int stc_idf_fit(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, double* 
                 int64_t* df_out, int64_t* m_out) {
   return guard([&] {
     STC_REQUIRE(ctx && tf && idf_out, "ctx/tf/idf_out");
+    STC_REQUIRE(tf->ctx == ctx, "the matrix belongs to another stc_ctx");
     STC_REQUIRE(min_doc_freq >= 0, "minDocFreq must be >= 0");
     ctx->use();
     hipStream_t s = ctx->stream;
@@ -1423,6 +1432,7 @@ int stc_idf_fit(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, double* 
 int stc_idf_transform(stc_ctx* ctx, stc_dcsr* tf, const double* idf, double zero_floor) {
   return guard([&] {
     STC_REQUIRE(ctx && tf && idf, "ctx/tf/idf");
+    STC_REQUIRE(tf->ctx == ctx, "the matrix belongs to another stc_ctx");
     STC_REQUIRE(zero_floor >= 0.0, "zero_floor must be >= 0");
     ctx->use();
     DevBuf d;
@@ -1482,10 +1492,10 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->lds_rows = cfg->dtype == STC_F32 ? lda::estep_lds_rows<float>(L->k, L->kp, L->P)
                                         : lda::estep_lds_rows<double>(L->k, L->kp, L->P);
     const char* nw = std::getenv("STC_DISABLE_WAVE");
-    // docs with nnz <= wave_cap run the register-resident grid kernel (fp32: lda_grid.hip, fp64:
-    // lda_grid64.hip), the rest the workgroup kernel (lda.hip); −1: no slot is "short" (not even empty)
+    // docs with nnz <= wave_cap run the register-resident kernel (fp32: lda_grid.hip, fp64:
+    // lda_rows64.hip), the rest the workgroup kernel (lda.hip); −1: no slot is "short" (not even empty)
     const int cap = use_wide(L->k, L->dtype) ? lda::wide_row_cap(L->k)
-                    : cfg->dtype == STC_F32 ? lda::wave_row_cap(L->k) : lda::grid64_row_cap(L->k);
+                    : cfg->dtype == STC_F32 ? lda::grid_row_cap(L->k) : lda::rows64_row_cap(L->k);
     L->wave_cap = (!(nw && nw[0] == '1') && cap > 0) ? cap : -1;
     // α / η resolution ([U] OnlineLDAOptimizer.initialize)
     std::vector<double> alpha((size_t)L->k);
@@ -1547,6 +1557,7 @@ int stc_lda_destroy(stc_lda* lda) {
 int stc_lda_set_corpus(stc_lda* L, const stc_dcsr* corpus, int64_t corpus_size_total) {
   return guard([&] {
     STC_REQUIRE(L && corpus, "lda/corpus");
+    STC_REQUIRE(corpus->ctx == L->ctx, "the corpus belongs to another stc_ctx than the LDA handle");
     STC_REQUIRE(corpus->cols == L->V, "corpus must have vocab_size columns");
     STC_REQUIRE(corpus->dtype == L->dtype, "corpus value dtype must match the LDA dtype");
     STC_REQUIRE(corpus->rows < (int64_t(1) << 31), "at most 2^31-1 documents per rank");
@@ -1688,6 +1699,7 @@ int stc_lda_bound(stc_lda* L, const stc_dcsr* docs, uint64_t gamma_seed, int64_t
                   double* topics_part_out, double* token_count_out) {
   return guard([&] {
     STC_REQUIRE(L && docs, "lda/docs");
+    STC_REQUIRE(docs->ctx == L->ctx, "the documents belong to another stc_ctx than the LDA handle");
     L->ctx->use();
     double h[3] = {0, 0, 0};
     double norm = 0;
@@ -1714,6 +1726,7 @@ int stc_lda_topic_distribution(stc_lda* L, const stc_dcsr* docs, uint64_t gamma_
                                int64_t doc_id_base, const double* gamma0, double* out) {
   return guard([&] {
     STC_REQUIRE(L && docs && (out || docs->rows == 0), "lda/docs/out");
+    STC_REQUIRE(docs->ctx == L->ctx, "the documents belong to another stc_ctx than the LDA handle");
     L->ctx->use();
     if (L->dtype == STC_F32)
       infer_impl<float>(*L, *docs, gamma_seed, doc_id_base, gamma0, false, out, nullptr);

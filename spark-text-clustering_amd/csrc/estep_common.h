@@ -1,4 +1,4 @@
-// estep_common.h — pieces shared by the register-resident E-step kernels (lda_wave.hip,
+// estep_common.h — pieces shared by the register-resident E-step kernels (lda_grid.hip,
 // lda_grid.hip): Spark's φ epsilon in log space, packed-FMA operand type, reduce-scatter helpers
 // and the diagnostic s_memtime stamps.
 #pragma once

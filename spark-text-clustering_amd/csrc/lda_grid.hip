@@ -12,7 +12,7 @@
 //     barrier and every wave sums them in the same order ⇒ bit-identical φ and r everywhere.
 //   s = Bᵀr : lane-local packed FMAs, reduce-scattered over the 32 row lanes only (permlane32 and
 //     permlane16 swaps, then row_half_mirror / quad_perm involutions, all of which keep bit 3):
-//     KL values per lane instead of the 52 of the topic-split kernel (lda_wave.hip).
+//     KL values per lane instead of the 52 a topic-split layout (two waves of 52 topics) would hold.
 //   γ, ψ(γ), exp on the owned topic (one per lane); eθ' of the group slice back through LDS.
 //   ψ(Σγ') from Σγ' = Σα + Σ_n cts_n − Σ_n cts_n·ε'_n/φ_n: a per-document constant unless a ballot
 //   finds a row whose ε' is visible at fp32 resolution.

@@ -86,12 +86,7 @@ int estep_lds_rows(int k, int kp, int P);
 template <typename T>
 void launch_estep(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound);
 
-// Wave-per-document E-step (lda_wave.hip): fp32, k <= 128, nnz <= wave_row_cap(k).
-int wave_kmax(int k);                  // 0 when the wave kernel does not apply
-int wave_row_cap(int k);               // max nnz a wave keeps in VGPRs (0 if n/a)
-void launch_estep_wave(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound);
-// Row-lane × topic-group grid E-step (lda_grid.hip), the default behind the two entry points above
-// (STC_WAVE_KERNEL=split selects the topic-split kernel of lda_wave.hip instead).
+// fp32 row-lane × topic-group grid E-step (lda_grid.hip): k <= 128, nnz <= grid_row_cap(k) (0 if n/a)
 int grid_row_cap(int k);
 void launch_estep_grid(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound);
 // fp64 grid E-step (lda_grid64.hip): k <= 104, nnz <= grid64_row_cap(k) (0 if n/a).

@@ -112,7 +112,8 @@ struct Ctx {
 };
 
 struct DCsr {
-  Ctx* ctx = nullptr;
+  Ctx* ctx = nullptr;  // the context that made it; only it may read the buffers (checked at the ABI)
+  int device = -1;     // for stc_dcsr_free, which may run after that context is gone
   int64_t rows = 0, cols = 0, nnz = 0;
   int64_t max_row = -1;  // longest row's nnz when known (host uploads), −1 otherwise
   int dtype = STC_F64;

@@ -78,11 +78,13 @@ def test_two_ranks_lda_next_idf_bound(tmp_path, oracle):
     st = oracle.OnlineLDAState(lam=lam0.T.copy(), alpha=alpha, eta=eta, corpus_size=total,
                                mini_batch_fraction=W.FRACTION, optimize_doc_concentration=True)
     empty_rank1 = 0
-    for _ in range(W.STEPS):
+    # next_impl (api.hip): the membership is keyed by the DRAW counter, which advances on every call
+    # (Spark's generator advances on empty batches too); γ₀ by the iteration the batch would make
+    for draw in range(1, W.STEPS + 1):
         it = st.iteration + 1
         docs, g0 = [], []
         for r, c in enumerate((c0, c1)):
-            mem = _members(c.indptr, W.FRACTION, W.SEED, it, r, oracle)
+            mem = _members(c.indptr, W.FRACTION, W.SEED, draw, r, oracle)
             empty_rank1 += (r == 1 and not mem)
             for pos, d in enumerate(mem):
                 docs.append(c.row(d))

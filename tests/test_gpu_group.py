@@ -87,6 +87,61 @@ def test_group_next_trains_every_member(ctx):
         assert np.all(np.isfinite(g.topics())) and np.all(g.alpha() > 0)
 
 
+def _shard_rows(indptr, n):
+    """stc_group's document split (api.hip shard_rows): contiguous rows, nnz-balanced."""
+    rows, nnz = indptr.size - 1, int(indptr[-1])
+    r0, r = [0], 0
+    for q in range(1, n):
+        target = (nnz * q + n - 1) // n
+        while r < rows and indptr[r] < target:
+            r += 1
+        r0.append(max(r, r0[-1]))
+    return r0 + [rows]
+
+
+@pytest.mark.parametrize("members", [2, 3])
+def test_group_next_matches_the_oracle_replay(ctx, oracle, members):
+    """The multi-rank sharded path end to end (per-member Poisson draws keyed by (draw, rank, local row),
+    the global-empty rule, the sliced λ update and its all-gathers) against the single-process oracle
+    replaying the same membership (test_gpu_comm._members restates k_sample).  fp64, 1e-9 on λ and α."""
+    import stc
+    from test_gpu_comm import _members
+
+    rng = np.random.default_rng(70 + members)
+    D, V, k, seed, frac, steps = 90, 700, 6, 77, 0.05, 8
+    corpus = random_corpus(rng, D, V, 1, 30, empty_every=11)
+    lam0 = rng.gamma(100.0, 0.01, size=(V, k))
+    r0 = _shard_rows(corpus.indptr, members)
+    with stc.LdaGroup([0] * members, k, V, dtype="f64", mini_batch_fraction=frac, seed=seed,
+                      optimize_doc_concentration=True) as g:
+        g.set_corpus(corpus)
+        g.set_topics(lam0)
+        for _ in range(steps):
+            g.next()
+        lam, alpha, iters = g.topics(), g.alpha(), g.iteration()
+    alpha0, eta = oracle.resolve_alpha_eta(k)
+    st = oracle.OnlineLDAState(lam=lam0.T.copy(), alpha=alpha0, eta=eta, corpus_size=D, mini_batch_fraction=frac,
+                               optimize_doc_concentration=True)
+    empty = 0
+    for draw in range(1, steps + 1):
+        it = st.iteration + 1
+        docs, g0 = [], []
+        for r in range(members):
+            lo, hi = r0[r], r0[r + 1]
+            ip = corpus.indptr[lo:hi + 1] - corpus.indptr[lo]
+            for pos, dl in enumerate(_members(ip, frac, seed, draw, r, oracle)):
+                docs.append(corpus.row(lo + dl))
+                g0.append(oracle.gamma_init(seed, oracle.train_doc_key(it, r, pos), k))
+        if not docs:
+            empty += 1
+            continue
+        oracle.submit_minibatch(st, docs, g0)
+    assert iters == st.iteration and st.iteration > 0
+    rel = np.max(np.abs(lam - st.lam.T) / st.lam.T)
+    assert rel < 1e-9, rel
+    np.testing.assert_allclose(alpha, st.alpha, rtol=1e-9)
+
+
 def test_group_argument_errors(ctx):
     import stc
 

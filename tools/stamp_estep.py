@@ -40,9 +40,7 @@ def main():
 
     ctx = stc.Context(0)
     lib = stc._lib.load()
-    # the grid kernel's reader (lda_grid.hip) unless STC_WAVE_KERNEL=split (lda_wave.hip)
-    split = os.environ.get("STC_WAVE_KERNEL") == "split"
-    reader = getattr(lib, "stc_debug_stamps" if split else "stc_debug_stamps_grid")
+    reader = lib.stc_debug_stamps_grid  # the fp32 grid kernel (lda_grid.hip)
     reader.restype = C.c_int
     reader.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
     buf = (C.c_ulonglong * 12)()
