@@ -576,14 +576,6 @@ bool launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamCh
   return ok;
 }
 
-// development switch: STC_G64=grid runs lda_grid64.hip's topic-split kernel instead of the rows split
-bool use_old_grid64() {
-  static const bool v = [] {
-    const char* e = getenv("STC_G64");
-    return e && std::string(e) == "grid";
-  }();
-  return v;
-}
 
 // fast kernel on slots [0, n_short), workgroup kernel on [n_short, n); mean_rows = the launch's mean
 // entries per document (the many-topic kernel's team size)
@@ -601,7 +593,6 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
       // launched (a refused cooperative grid falls through to the one-CU kernel)
     } else if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
     else if constexpr (std::is_same<T, float>::value) lda::launch_estep_grid(s, w, stats, bound);
-    else if (use_old_grid64()) lda::launch_estep_grid64(s, w, stats, bound, m.max_row < 0 || m.max_row > lda::grid64_onchip_rows(L.k));
     else lda::launch_estep_rows64(s, w, stats, bound, m.max_row < 0 || m.max_row > lda::rows64_onchip_rows(L.k));
   }
   if (n > n_short) {

@@ -28,7 +28,7 @@ __device__ __forceinline__ float rs_dpp(float x, float y, bool hi) {
 constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141, DPP_ROW_ROR8 = 0x128,
               DPP_QP_3210 = 0x1B, DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E;
 
-// ---- fp64 cross-lane helpers (lda_grid64.hip, lda_wide.hip): a double moves as two dwords
+// ---- fp64 cross-lane helpers (lda_rows64.hip, lda_wide.hip): a double moves as two dwords
 typedef unsigned long long u64;
 
 __device__ __forceinline__ unsigned lo32(double v) { return (unsigned)__builtin_bit_cast(u64, v); }

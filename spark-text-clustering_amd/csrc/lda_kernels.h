@@ -89,11 +89,8 @@ void launch_estep(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound);
 // fp32 row-lane × topic-group grid E-step (lda_grid.hip): k <= 128, nnz <= grid_row_cap(k) (0 if n/a)
 int grid_row_cap(int k);
 void launch_estep_grid(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound);
-// fp64 grid E-step (lda_grid64.hip): k <= 104, nnz <= grid64_row_cap(k) (0 if n/a).
-int grid64_row_cap(int k);
-int grid64_onchip_rows(int k);  // rows past this are streamed (a second launch, `long_docs`)
-void launch_estep_grid64(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs);
-// fp64 rows-split E-step (lda_rows64.hip): same k / row caps as the grid kernel
+// fp64 rows-split E-step (lda_rows64.hip): k <= 104, nnz <= rows64_row_cap(k) (0 if n/a); documents
+// past rows64_onchip_rows(k) run in a second launch (`long_docs`)
 int rows64_row_cap(int k);
 int rows64_onchip_rows(int k);
 void launch_estep_rows64(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs);

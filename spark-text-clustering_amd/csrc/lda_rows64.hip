@@ -19,8 +19,9 @@
 //     constant unless some row's ε' is visible at fp64 resolution (ε' ≥ 2^-53·φ).
 //   Spark's stop rule Σ|Δγ|/k ≤ 1e-3 is one comparison against EStepArgs::stop_thr; the ψ waves'
 //     Σ|Δγ| partials ride the second barrier.
-// Against lda_grid64.hip's topic split (each wave a 26-topic slice, the s reduction a 32-lane DPP /
-// permlane reduce-scatter of 13 values in every wave, ψ/exp in all four waves) this removes ≈ 75
+// Against the round-2 topic split (lda_grid64.hip, since removed: each wave a 26-topic slice, the s
+// reduction a 32-lane DPP / permlane reduce-scatter of 13 values in every wave, ψ/exp in all four
+// waves) this removes ≈ 75
 // cross-lane and ≈ 200 transcendental VALU instructions per document-iteration and the scratch
 // reload the old loop carried; the cost is LDS traffic (13 8-byte stores per lane and iteration),
 // which the LDS array absorbs beside the VALU (MI355X_MICROARCH.md §LDS).

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of an E-step change: the LDA parity tests, the headline (and planted) bench lines with the new
-# kernel (and, with OLD=1, with STC_G64=grid — the previous one), then the stamp build's phase split
+# kernel (and, with OLD_LIB=path, with that earlier build of the library), then the stamp build's phase split
 # (STAMP=1).  One time limit per step; stops at the first failure.
 mkdir -p gpurun_out; : > gpurun_out/status.log
 step() {  # step NAME SECONDS CMD...
@@ -18,9 +18,9 @@ if [ "${TESTS:-default}" != "none" ]; then
 fi
 step b_new 240 $B
 step p_new 240 $B $P
-if [ -n "$OLD" ]; then
-  step b_old 240 env STC_G64=grid $B
-  step p_old 240 env STC_G64=grid $B $P
+if [ -n "$OLD_LIB" ]; then  # a previous build of libstc.so, e.g. saved before an E-step change
+  step b_old 240 env STC_LIB=$OLD_LIB $B
+  step p_old 240 env STC_LIB=$OLD_LIB $B $P
 fi
 if [ -n "$STAMP" ]; then
   step stamp 200 env STC_LIB=spark-text-clustering_amd/stc/libstc_stamp.so python tools/stamp_rows64.py

@@ -32,7 +32,7 @@ PHASE = re.compile(r"k_estep|k_sstats|k_fixup|rocprim|fillBuffer|k_part_|k_fill_
 # same launches the bench's HIP-event "estep" phase brackets
 # (STATS = true, BOUND = false): k_estep / k_estep_grid / k_estep_wave / k_estep_wide <..., true, false>;
 # k_estep_grid64 / k_estep_rows64 <shape, true, false, LONG>; k_estep_wide_mc / _tc <T, Q, NR, true>
-ESTEP = re.compile(r"k_estep_grid64<DShape<[^>]*>, true, false, (true|false)>$"
+ESTEP = re.compile(r"k_estep_grid64<DShape<[^>]*>, true, false, (true|false)>$"  # round-2 profiles
                    r"|k_estep_rows64<RShape<[^>]*>, true, false, (true|false)>$"
                    r"|k_estep_wide_(mc|tc)<\w+, \d+, \d+, true>$"
                    r"|k_estep(_grid|_wave|_wide)?<(?!DShape).*, true, false>$")
