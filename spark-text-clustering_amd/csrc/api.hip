@@ -55,7 +55,7 @@ struct stc_lda {
   bool has_topics = false;
   int64_t nblocks_m = 0;
 
-  DevBuf lam, Bp, logscale, colsum, colpart, alpha, small, scal;
+  DevBuf lam, Bp, logscale, colsum, psic, colpart, alpha, small, scal;
   DevBuf batch_raw, batch, orig, flags, sincl, bptr, bnnz, nnzp, g0, gamma, eth, elogth, iters,
       nonempty, r, keys, vals, skeys, svals, stat, headbuf, tailbuf, sort_tmp, scan_tmp,
       stats4, cum2, bound, dtmp, lpart;
@@ -326,10 +326,10 @@ void relayout(stc_lda& L) {
 template <typename T>
 void refresh_model(stc_lda& L) {
   hipStream_t s = L.ctx->stream;
-  lda::launch_colsum_lambda(s, L.lam.as<double>(), L.V, L.k, L.colpart.as<double>(), L.nblocks_m);
-  lda::launch_colsum_reduce(s, L.colpart.as<double>(), L.nblocks_m, L.k, nullptr, L.colsum.as<double>());
-  lda::launch_expelogbeta<T>(s, L.lam.as<double>(), L.colsum.as<double>(), L.V, L.k, L.kp, nullptr,
-                             L.Bp.as<T>(), L.logscale.as<double>());
+  lda::launch_lambda_eeb<T>(s, false, L.lam.as<double>(), nullptr, L.Bp.as<T>(), L.logscale.as<double>(), L.V,
+                            L.k, L.kp, 0.0, 0.0, 0.0, nullptr, L.colpart.as<double>(), L.nblocks_m);
+  lda::launch_colsum_reduce(s, L.colpart.as<double>(), L.nblocks_m, L.k, nullptr, L.colsum.as<double>(),
+                            L.psic.as<double>());
   L.has_topics = true;
 }
 
@@ -418,6 +418,7 @@ lda::EStepArgs<T> estep_args(stc_lda& L) {
   a.lds_rows = L.lds_rows;
   a.Bp = L.Bp.as<T>();
   a.logscale = L.logscale.as<double>();
+  a.psic = L.psic.as<double>();
   a.alpha = L.alpha.as<double>();
   a.seed = L.cfg.seed;
   a.rank = L.ctx->rank;
@@ -667,30 +668,24 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   record(L, 3);
 }
 
-// the λ update, colsum and expElogβ' of one vocabulary slice r: rows [r·Vs, r·Vs + vn); its colsum
-// partials land at λ-update block r·Vs/RB, where the one-GPU reduction has them
+// the fused M-step pass over one vocabulary slice r, rows [r·Vs, r·Vs + vn): λ update, the next
+// expElogβ' rows + logscale, and colsum partials at λ-update block r·Vs/RB, where the one-GPU
+// reduction has them.  Nothing in it needs the new colsum (ψ(colsum) is the E-step's per-topic factor).
 template <typename T>
 void mstep_slice(stc_lda& L, int r, double rho, double scale, const double* gate) {
   const int64_t v0 = (int64_t)r * L.Vs, vn = std::max<int64_t>(0, std::min(L.V - v0, L.Vs));
   const int64_t nbs = L.Vs / lda::kRowsPerBlock;
-  lda::launch_lambda_update<T>(L.ctx->stream, L.lam.as<double>() + v0 * L.k, L.stat.as<T>() + v0 * L.kp,
-                               L.Bp.as<T>() + v0 * L.kp, vn, L.k, L.kp, rho, scale, L.eta, gate,
-                               L.colpart.as<double>() + (int64_t)r * nbs * L.k, nbs);
-}
-template <typename T>
-void eeb_slice(stc_lda& L, int r, const double* gate) {
-  const int64_t v0 = (int64_t)r * L.Vs, vn = std::max<int64_t>(0, std::min(L.V - v0, L.Vs));
-  if (vn > 0)
-    lda::launch_expelogbeta<T>(L.ctx->stream, L.lam.as<double>() + v0 * L.k, L.colsum.as<double>(), vn, L.k,
-                               L.kp, gate, L.Bp.as<T>() + v0 * L.kp, L.logscale.as<double>() + v0);
+  lda::launch_lambda_eeb<T>(L.ctx->stream, true, L.lam.as<double>() + v0 * L.k, L.stat.as<T>() + v0 * L.kp,
+                            L.Bp.as<T>() + v0 * L.kp, L.logscale.as<double>() + v0, vn, L.k, L.kp, rho, scale,
+                            L.eta, gate, L.colpart.as<double>() + (int64_t)r * nbs * L.k, nbs);
 }
 
 // [U] submitMiniBatch tail: the stats merge (treeReduce ≙ RCCL), updateLambda, updateAlpha.
-//  * one GPU: λ update over all rows, colsum, expElogβ'.
+//  * one GPU: the fused λ update + expElogβ' pass over all rows, then colsum and ψ(colsum).
 //  * N ranks: reduce-scatter of stat (each rank receives the summed rows of its vocabulary slice) and
-//    the logphat / count all-reduce in one group; the slice's λ update; an all-gather of the per-block
-//    colsum partials (k doubles per 64 rows), reduced in the one-GPU order, so colsum is identical on
-//    every rank; the slice's expElogβ'; an all-gather of expElogβ' and logscale for the next E-step.
+//    the logphat / count all-reduce in one group; the slice's fused λ update + expElogβ' pass; ONE
+//    group of all-gathers — the per-block colsum partials (k doubles per 64 rows), expElogβ' and
+//    logscale — then colsum reduced in the one-GPU block order, so it is identical on every rank.
 //    λ stays sharded (lam_stale) until a reader gathers it.  Per rank: stat (N−1)/N·V·kp·T bytes
 //    out, expElogβ' the same in, against 2(N−1)/N for an all-reduce, and 1/N of the M-step work.
 template <typename T>
@@ -725,19 +720,19 @@ void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
   if (ranks) {
     const size_t nbs = (size_t)(L.Vs / lda::kRowsPerBlock);
     mstep_slice<T>(L, c.rank, rho, scale, gate);
-    coll_all_gather(c, L.colpart.as<double>() + (size_t)c.rank * nbs * L.k, L.colpart.p, nbs * L.k, ncclFloat64, s);
-    lda::launch_colsum_reduce(s, L.colpart.as<double>(), nb_all, L.k, gate, L.colsum.as<double>());
-    eeb_slice<T>(L, c.rank, gate);
     const size_t cnt = (size_t)(L.Vs * L.kp);
     coll_group_start(c);
+    coll_all_gather(c, L.colpart.as<double>() + (size_t)c.rank * nbs * L.k, L.colpart.p, nbs * L.k, ncclFloat64, s);
     coll_all_gather(c, L.Bp.as<T>() + (size_t)c.rank * cnt, L.Bp.p, cnt, RcclType<T>::v, s);
     coll_all_gather(c, L.logscale.as<double>() + (size_t)c.rank * L.Vs, L.logscale.p, (size_t)L.Vs, ncclFloat64, s);
     coll_group_end(c);
+    lda::launch_colsum_reduce(s, L.colpart.as<double>(), nb_all, L.k, gate, L.colsum.as<double>(),
+                              L.psic.as<double>());
     L.lam_stale = true;
   } else {  // one GPU: all slices here (one unless STC_VIRTUAL_SHARDS)
     for (int r = 0; r < L.shards; ++r) mstep_slice<T>(L, r, rho, scale, gate);
-    lda::launch_colsum_reduce(s, L.colpart.as<double>(), nb_all, L.k, gate, L.colsum.as<double>());
-    for (int r = 0; r < L.shards; ++r) eeb_slice<T>(L, r, gate);
+    lda::launch_colsum_reduce(s, L.colpart.as<double>(), nb_all, L.k, gate, L.colsum.as<double>(),
+                              L.psic.as<double>());
   }
   if (L.cfg.optimize_doc_concentration)
     lda::launch_update_alpha(s, L.alpha.as<double>(), L.small.as<double>(), L.k, rho);
@@ -909,7 +904,8 @@ void estep_only(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0,
   }
   if (stat_out) {
     L.dtmp.reserve(sizeof(double) * L.V * L.k);
-    lda::launch_unscale_stat<T>(s, L.stat.as<T>(), L.logscale.as<double>(), L.V, L.k, L.kp, L.dtmp.as<double>());
+    lda::launch_unscale_stat<T>(s, L.stat.as<T>(), L.logscale.as<double>(), L.psic.as<double>(), L.V, L.k, L.kp,
+                                L.dtmp.as<double>());
     HIP_CHECK(hipMemcpyAsync(stat_out, L.dtmp.p, sizeof(double) * L.V * L.k, hipMemcpyDeviceToHost, s));
   }
   HIP_CHECK(hipStreamSynchronize(s));
@@ -1523,6 +1519,7 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->force_coll = fc && fc[0] == '1';
     ensure_layout(*L);  // λ, Bp, stat, logscale, colpart for the current shard count
     L->colsum.reserve(8 * L->k);
+    L->psic.reserve(16 * L->k);  // ψ(colsum), exp(−ψ(colsum))
     L->alpha.reserve(8 * L->k);
     L->small.reserve(8 * (L->k + 1));
     L->stats4.reserve(8 * 4);

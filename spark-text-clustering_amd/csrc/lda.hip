@@ -6,14 +6,15 @@
 //   k_estep          [U] OnlineLDAOptimizer.variationalTopicInference (+ LocalLDAModel
 //                    logLikelihoodBound corpusPart when BOUND)
 //   k_sstats/k_fixup [U] submitMiniBatch `stat(::, ids) += sstats` + treeReduce (per device)
-//   k_lambda_update  [U] submitMiniBatch `statsSum ⊙ expElogβᵀ` + updateLambda
-//   k_expelogbeta    [U] exp(LDAUtils.dirichletExpectation(λ)) (+ .t)
+//   k_lambda_eeb     [U] submitMiniBatch `statsSum ⊙ expElogβᵀ` + updateLambda, and in the same
+//                    pass the rows of exp(LDAUtils.dirichletExpectation(λ)) (+ .t)
 //   k_update_alpha   [U] updateAlpha (Newton step on α)
 //   k_topics_bound   [U] logLikelihoodBound topicsPart
 //
-// Numerics: expElogβ is stored ROW-SCALED, Bp[v][t] = exp(Elogβ[v][t] − m_v) with
-// m_v = max_t Elogβ[v][t], and the E-step iterates with eθ' = exp(ψ(γ_t) − ψ(max γ)).  Both
-// factors cancel exactly in γ ← eθ ⊙ Bᵀ(cts/(B·eθ)) + α and in batchResult = stat ⊙ expElogβ, so
+// Numerics: expElogβ is stored ROW-SCALED and without its per-topic factor,
+// Bp[v][t] = exp(ψ(λ_vt) − m_v) with m_v = max_t ψ(λ_vt); the E-step iterates with
+// eθ' = exp(ψ(γ_t) − ψ(max γ) − ψ(Σ_v λ_vt)).  Bp·eθ' = e^{-m_v}·expElogβ·exp(ψ(γ) − ψ(max γ)), so
+// both scales cancel exactly in γ ← eθ ⊙ Bᵀ(cts/(B·eθ)) + α and in batchResult = stat ⊙ expElogβ:
 // the recursion is Spark's, but nothing underflows in fp32 (Spark's unscaled exp(Elogβ) reaches
 // 1e-50 for rare terms).  The bound adds m_v and max E[log θ] back in fp64.
 #include "lda_kernels.h"
@@ -58,6 +59,14 @@ __device__ __forceinline__ float exp_t(float x) { return __expf(x); }
 __device__ __forceinline__ float psi_t(float x) { return digamma_fast(x); }
 __device__ __forceinline__ double psi_t(double x) { return digamma_t<double>(x); }
 __device__ __forceinline__ double exp_t(double x) { return exp(x); }
+// eθ' = exp(x − ψc_t): fp64 subtracts ψc_t in the argument, fp32 multiplies by exp(−ψc_t) (EStepArgs::psic)
+__device__ __forceinline__ double exp_minus_psic(double x, const double* psic, int k, int t) {
+  (void)k;
+  return exp(x - psic[t]);
+}
+__device__ __forceinline__ float exp_minus_psic(float x, const double* psic, int k, int t) {
+  return __expf(x) * (float)psic[k + t];
+}
 
 // ---------------------------------------------------------------------------------------
 // Block (256 threads = 4 waves) reduction of (sum, sum, max) in a fixed order: deterministic.
@@ -205,7 +214,7 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
   {
     const T psimax = psi_t((T)gmax);
     for (int t = tid; t < kp; t += kBlock)
-      s_eth[t] = t < k ? exp_t(psi_t(s_gam[t]) - psimax) : T(0);
+      s_eth[t] = t < k ? exp_minus_psic(psi_t(s_gam[t]) - psimax, a.psic, k, t) : T(0);
   }
   __syncthreads();
 
@@ -265,7 +274,7 @@ __device__ __forceinline__ void estep_doc(const EStepArgs<T>& a, unsigned char* 
     // Phase D: eθ' = exp(ψ(γ) − ψ(max γ)) ; meanGammaChange = Σ|Δγ| / k
     const T psimax = psi_t((T)gmax);
     lmax = psimax - psi_t((T)gsum);
-    for (int t = tid; t < k; t += kBlock) s_eth[t] = exp_t(psi_t(s_gam[t]) - psimax);
+    for (int t = tid; t < k; t += kBlock) s_eth[t] = exp_minus_psic(psi_t(s_gam[t]) - psimax, a.psic, k, t);
     ++it;
     done = dsum / (double)k <= 1e-3;
     __syncthreads();
@@ -537,92 +546,12 @@ void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, 
 // workgroup, lanes over topics, fixed-order per-topic partial sums (deterministic colsum).
 // ---------------------------------------------------------------------------------------
 
-template <typename T, bool UPDATE>
-__global__ __launch_bounds__(256) void k_lambda_update(double* __restrict__ lam, const T* __restrict__ stat,
-                                                       const T* __restrict__ Bp, int64_t V, int k, int kp,
-                                                       double rho, double scale, double eta,
-                                                       const double* __restrict__ gate,
-                                                       double* __restrict__ colpart) {
-  if (gate && !(gate[0] > 0.0)) return;  // Spark: no non-empty docs ⇒ no update (< 0: a team timed out)
-  __shared__ double s_acc[256];
-  const int tid = threadIdx.x;
-  const int TW = k < 256 ? k : 256;
-  const int nrl = 256 / TW;
-  const int ti = tid % TW, rl = tid / TW;
-  const int64_t v0 = (int64_t)blockIdx.x * kRowsPerBlock;
-  const int64_t v1 = (v0 + kRowsPerBlock < V) ? v0 + kRowsPerBlock : V;
-  for (int t0 = 0; t0 < k; t0 += TW) {
-    const int t = t0 + ti;
-    double acc = 0.0;
-    if (rl < nrl && t < k) {
-      for (int64_t v = v0 + rl; v < v1; v += nrl) {
-        const int64_t e = v * k + t;
-        double nl = lam[e];
-        if (UPDATE) {
-          const int64_t ev = v * kp + t;
-          nl = (1.0 - rho) * nl + rho * ((double)stat[ev] * (double)Bp[ev] * scale + eta);
-          lam[e] = nl;
-        }
-        acc += nl;
-      }
-    }
-    if (rl < nrl) s_acc[rl * TW + ti] = acc;
-    __syncthreads();
-    if (tid < TW && t0 + tid < k) {
-      double sum = 0.0;
-      for (int j = 0; j < nrl; ++j) sum += s_acc[j * TW + tid];
-      colpart[(int64_t)blockIdx.x * k + t0 + tid] = sum;
-    }
-    __syncthreads();
-  }
-}
-
-template <typename T>
-void launch_lambda_update(hipStream_t s, double* lam, const T* stat, const T* Bp, int64_t V, int k,
-                          int kp, double rho, double scale, double eta, const double* gate,
-                          double* colpart, int64_t nblocks) {
-  k_lambda_update<T, true><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, V, k, kp, rho, scale,
-                                                             eta, gate, colpart);
-  KERNEL_CHECK();
-}
-
-void launch_colsum_lambda(hipStream_t s, const double* lam, int64_t V, int k, double* colpart,
-                          int64_t nblocks) {
-  k_lambda_update<float, false><<<(unsigned)nblocks, 256, 0, s>>>(
-      const_cast<double*>(lam), nullptr, nullptr, V, k, k, 0.0, 0.0, 0.0, nullptr, colpart);
-  KERNEL_CHECK();
-}
-
-__global__ __launch_bounds__(256) void k_colsum_reduce(const double* __restrict__ colpart,
-                                                       int64_t nblocks, int k,
-                                                       const double* __restrict__ gate,
-                                                       double* __restrict__ colsum) {
-  if (gate && !(gate[0] > 0.0)) return;
-  __shared__ double s[256];
-  const int t = blockIdx.x;
-  double acc = 0.0;
-  for (int64_t b = threadIdx.x; b < nblocks; b += 256) acc += colpart[b * k + t];
-  s[threadIdx.x] = acc;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) colsum[t] = s[0];
-}
-
-void launch_colsum_reduce(hipStream_t s, const double* colpart, int64_t nblocks, int k,
-                          const double* gate, double* colsum) {
-  k_colsum_reduce<<<k, 256, 0, s>>>(colpart, nblocks, k, gate, colsum);
-  KERNEL_CHECK();
-}
-
-// expElogβ'[v][t] = exp(ψ(λ_vt) − ψ(colsum_t) − m_v), m_v ≈ max_t (ψ(λ_vt) − ψ(colsum_t)); one wave
-// per term (grid-stride over terms, so ψ(colsum) is staged once per block for many rows), each
-// lane's Q topics held in registers so ψ(λ) is evaluated once per element (branch-free fp64
-// digamma).  m_v only has to be common to the row and to logscale, not the exact maximum: the
-// fp32 build takes it from an fp32 DPP max, and evaluates the exponential as 2^n · 2^f with the
-// integer/fraction split done in fp64, so the fp32 argument never loses the bits of a large |Elogβ|.
+// expElogβ'[v][t] = exp(ψ(λ_vt) − m_v), m_v ≈ max_t ψ(λ_vt): the ROW-scaled part of Spark's
+// exp(dirichletExpectation(λ)) — the per-topic factor exp(−ψ(Σ_v λ_vt)) is applied to eθ by the
+// E-step (EStepArgs::psic), so a row needs only its own λ and the pass fuses with the λ update.
+// m_v only has to be common to the row and to logscale, not the exact maximum: the fp32 build takes
+// it from an fp32 DPP max and evaluates the exponential as 2^n · 2^f with the integer/fraction split
+// done in fp64, so the fp32 argument never loses the bits of a large |ψ(λ)|.
 __device__ __forceinline__ float exp_scaled(double x, float) {
   const double y = x * 1.4426950408889634;  // log2 e
   const double n = floor(y);
@@ -634,39 +563,58 @@ __device__ __forceinline__ double row_max(double m, float) {
 }
 __device__ __forceinline__ double row_max(double m, double) { return wave_max(m); }
 
-template <typename T, int Q>
-__global__ __launch_bounds__(256) void k_expelogbeta(const double* __restrict__ lam,
-                                                     const double* __restrict__ colsum, int64_t V,
-                                                     int k, int kp, const double* __restrict__ gate,
-                                                     T* __restrict__ Bp, double* __restrict__ logscale) {
-  if (gate && !(gate[0] > 0.0)) return;
-  extern __shared__ double s_psic[];
-  for (int t = threadIdx.x; t < k; t += 256) s_psic[t] = digamma_fast_d(colsum[t]);
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * 4;
-  int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  double nx[Q];  // the next row's λ, requested before this row's ψ work (hides the load latency)
+// The M-step in ONE pass over the vocabulary rows ([U] submitMiniBatch `statsSum ⊙ expElogβᵀ` +
+// updateLambda, then the next minibatch's expElogβ): per row v
+//   λ_v ← (1−ρ)λ_v + ρ(stat_v ⊙ Bp_v·D/|B| + η)     (UPDATE; stat ⊙ Bp = Spark's batchResult, §4)
+//   Bp_v ← exp(ψ(λ_v) − m_v), logscale_v = m_v      (the next E-step's rows)
+// and per block of kRowsPerBlock rows the per-topic partials of Σ_v λ_vt (colpart), reduced by
+// k_colsum_reduce in block order.  One wave per row (lane = topic mod 64, Q topics per lane), the
+// four waves of a block take rows w, w+4, …; the block's partials are added in wave order, so colsum
+// is identical for any vocabulary slicing that keeps the blocks (§6).  UPDATE = false: colsum
+// partials and Bp of the current λ (set_topics / init_random).
+template <typename T, int Q, bool UPDATE>
+__global__ __launch_bounds__(256) void k_lambda_eeb(double* __restrict__ lam, const T* __restrict__ stat,
+                                                    T* __restrict__ Bp, double* __restrict__ logscale,
+                                                    int64_t V, int k, int kp, double rho, double scale,
+                                                    double eta, const double* __restrict__ gate,
+                                                    double* __restrict__ colpart) {
+  if (gate && !(gate[0] > 0.0)) return;  // Spark: no non-empty docs ⇒ no update (< 0: a team timed out)
+  __shared__ double s_acc[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t v0 = (int64_t)blockIdx.x * kRowsPerBlock;
+  constexpr int QC = Q < 4 ? Q : 4;  // topics per lane whose loads are issued together
+  double acc[Q];
 #pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int t = lane + 64 * q;
-    nx[q] = (v < V && t < k) ? lam[v * k + t] : 1.0;
-  }
-  for (; v < V; v += stride) {
-    double lv[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int t = lane + 64 * q;
-      lv[q] = nx[q];
-      nx[q] = (v + stride < V && t < k) ? lam[(v + stride) * k + t] : 1.0;
-    }
+  for (int q = 0; q < Q; ++q) acc[q] = 0.0;
+  for (int i = w; i < kRowsPerBlock; i += 4) {
+    const int64_t v = v0 + i;
+    if (v >= V) break;
     double e[Q];
     double m = -INFINITY;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int t = lane + 64 * q;
-      e[q] = t < k ? digamma_fast_d(lv[q]) - s_psic[t] : -INFINITY;
-      m = fmax(m, e[q]);
+    for (int q0 = 0; q0 < Q; q0 += QC) {
+      double lv[QC], sv[QC], bv[QC];
+#pragma unroll
+      for (int j = 0; j < QC; ++j) {
+        const int t = lane + 64 * (q0 + j);
+        lv[j] = t < k ? lam[v * k + t] : 1.0;
+        if (UPDATE) {
+          sv[j] = t < k ? (double)stat[v * kp + t] : 0.0;
+          bv[j] = t < k ? (double)Bp[v * kp + t] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < QC; ++j) {
+        const int q = q0 + j, t = lane + 64 * q;
+        double nl = lv[j];
+        if (UPDATE) nl = (1.0 - rho) * nl + rho * (sv[j] * bv[j] * scale + eta);
+        if (t < k) {
+          if (UPDATE) lam[v * k + t] = nl;
+          acc[q] += nl;
+        }
+        e[q] = t < k ? digamma_fast_d(nl) : -INFINITY;
+        m = fmax(m, e[q]);
+      }
     }
     m = row_max(m, T());
     T* br = Bp + v * kp;
@@ -677,24 +625,159 @@ __global__ __launch_bounds__(256) void k_expelogbeta(const double* __restrict__ 
     }
     if (lane == 0) logscale[v] = m;
   }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    s_acc[w][lane] = acc[q];
+    __syncthreads();
+    const int t = lane + 64 * q;
+    if (w == 0 && t < k)
+      colpart[(int64_t)blockIdx.x * k + t] = ((s_acc[0][lane] + s_acc[1][lane]) + s_acc[2][lane]) + s_acc[3][lane];
+    __syncthreads();
+  }
+}
+
+// The same pass for many topics (kp > 256): a row per WORKGROUP — thread i owns topics i + 256·j — so
+// the loads of a row are spread over 256 lanes instead of one wave's Q·3 registers, and the next row's
+// loads are issued before this row's ψ/exp work (software pipelined).  The row max crosses the four
+// waves through LDS (double-buffered by row parity: one barrier per row).  Each topic's colsum partial
+// is one thread's running sum over the block's rows in row order.
+template <typename T, int Q, bool UPDATE>
+__global__ __launch_bounds__(256) void k_lambda_eeb_wide(double* __restrict__ lam, const T* __restrict__ stat,
+                                                         T* __restrict__ Bp, double* __restrict__ logscale,
+                                                         int64_t V, int k, int kp, double rho, double scale,
+                                                         double eta, const double* __restrict__ gate,
+                                                         double* __restrict__ colpart) {
+  if (gate && !(gate[0] > 0.0)) return;
+  __shared__ double s_max[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int64_t v0 = (int64_t)blockIdx.x * kRowsPerBlock;
+  const int nrow = (int)((V - v0) < kRowsPerBlock ? (V - v0 > 0 ? V - v0 : 0) : kRowsPerBlock);
+  double acc[Q], lv[Q], sv[Q], bv[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) acc[q] = 0.0;
+  auto load = [&](int64_t v) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int t = tid + 256 * q;
+      lv[q] = t < k ? lam[v * k + t] : 1.0;
+      if (UPDATE) {
+        sv[q] = t < k ? (double)stat[v * kp + t] : 0.0;
+        bv[q] = t < k ? (double)Bp[v * kp + t] : 0.0;
+      }
+    }
+  };
+  if (nrow > 0) load(v0);
+  for (int i = 0; i < nrow; ++i) {
+    const int64_t v = v0 + i;
+    double e[Q];
+    double m = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int t = tid + 256 * q;
+      double nl = lv[q];
+      if (UPDATE) nl = (1.0 - rho) * nl + rho * (sv[q] * bv[q] * scale + eta);
+      if (t < k) {
+        if (UPDATE) lam[v * k + t] = nl;
+        acc[q] += nl;
+      }
+      e[q] = nl;
+    }
+    if (i + 1 < nrow) load(v + 1);  // the next row's loads fly during this row's ψ / exp
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int t = tid + 256 * q;
+      e[q] = t < k ? digamma_fast_d(e[q]) : -INFINITY;
+      m = fmax(m, e[q]);
+    }
+    m = row_max(m, T());
+    if (lane == 0) s_max[i & 1][w] = m;
+    __syncthreads();
+    m = fmax(fmax(s_max[i & 1][0], s_max[i & 1][1]), fmax(s_max[i & 1][2], s_max[i & 1][3]));
+    T* br = Bp + v * kp;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int t = tid + 256 * q;
+      if (t < kp) br[t] = t < k ? exp_scaled(e[q] - m, T()) : T(0);
+    }
+    if (tid == 0) logscale[v] = m;
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int t = tid + 256 * q;
+    if (t < k) colpart[(int64_t)blockIdx.x * k + t] = acc[q];
+  }
 }
 
 template <typename T>
-void launch_expelogbeta(hipStream_t s, const double* lam, const double* colsum, int64_t V, int k,
-                        int kp, const double* gate, T* Bp, double* logscale) {
-  const unsigned grid = (unsigned)std::min<int64_t>(ceil_div(V, 4), 2048);  // ≈ 8 terms per wave at V = 2^18
-  const size_t sh = sizeof(double) * k;
+void launch_lambda_eeb(hipStream_t s, bool update, double* lam, const T* stat, T* Bp, double* logscale,
+                       int64_t V, int k, int kp, double rho, double scale, double eta, const double* gate,
+                       double* colpart, int64_t nblocks) {
+  if (nblocks <= 0) return;
+  if (kp > 256) {  // a row per workgroup
+    const int qw = (kp + 255) / 256;
+#define STC_LEEBW(QQ)                                                                                    \
+  do {                                                                                                   \
+    if (update)                                                                                          \
+      k_lambda_eeb_wide<T, QQ, true><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, logscale, V, k, kp, \
+                                                                        rho, scale, eta, gate, colpart);  \
+    else                                                                                                 \
+      k_lambda_eeb_wide<T, QQ, false><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, logscale, V, k,    \
+                                                                         kp, rho, scale, eta, gate, colpart); \
+  } while (0)
+    if (qw <= 2) STC_LEEBW(2);
+    else if (qw <= 4) STC_LEEBW(4);
+    else if (qw <= 8) STC_LEEBW(8);
+    else if (qw <= 16) STC_LEEBW(16);
+    else throw Error(STC_ERR_INVALID_ARG, "k > 4096 topics is not supported");
+#undef STC_LEEBW
+    KERNEL_CHECK();
+    return;
+  }
   const int q = (kp + 63) / 64;
-#define STC_EEB(QQ) k_expelogbeta<T, QQ><<<grid, 256, sh, s>>>(lam, colsum, V, k, kp, gate, Bp, logscale)
-  if (q <= 1) STC_EEB(1);
-  else if (q <= 2) STC_EEB(2);
-  else if (q <= 4) STC_EEB(4);
-  else if (q <= 8) STC_EEB(8);
-  else if (q <= 16) STC_EEB(16);
-  else if (q <= 32) STC_EEB(32);
-  else if (q <= 64) STC_EEB(64);
-  else throw Error(STC_ERR_INVALID_ARG, "k > 4096 topics is not supported");
-#undef STC_EEB
+#define STC_LEEB(QQ)                                                                                    \
+  do {                                                                                                  \
+    if (update)                                                                                         \
+      k_lambda_eeb<T, QQ, true><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, logscale, V, k, kp,   \
+                                                                   rho, scale, eta, gate, colpart);    \
+    else                                                                                                \
+      k_lambda_eeb<T, QQ, false><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, logscale, V, k, kp,  \
+                                                                    rho, scale, eta, gate, colpart);   \
+  } while (0)
+  if (q <= 1) STC_LEEB(1);
+  else if (q <= 2) STC_LEEB(2);
+  else STC_LEEB(4);
+#undef STC_LEEB
+  KERNEL_CHECK();
+}
+
+// colsum_t = Σ_b colpart[b][t] in block order, psic_t = ψ(colsum_t) (the E-step's per-topic factor of
+// expElogβ) and psic_{k+t} = exp(−ψ(colsum_t))
+__global__ __launch_bounds__(256) void k_colsum_reduce(const double* __restrict__ colpart,
+                                                       int64_t nblocks, int k,
+                                                       const double* __restrict__ gate,
+                                                       double* __restrict__ colsum, double* __restrict__ psic) {
+  if (gate && !(gate[0] > 0.0)) return;
+  __shared__ double s[256];
+  const int t = blockIdx.x;
+  double acc = 0.0;
+  for (int64_t b = threadIdx.x; b < nblocks; b += 256) acc += colpart[b * k + t];
+  s[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    colsum[t] = s[0];
+    const double pc = digamma_fast_d(s[0]);
+    psic[t] = pc;
+    psic[k + t] = exp(-pc);  // the fp32 kernels' multiplier (an fp32 exponent argument would lose its low bits)
+  }
+}
+
+void launch_colsum_reduce(hipStream_t s, const double* colpart, int64_t nblocks, int k,
+                          const double* gate, double* colsum, double* psic) {
+  k_colsum_reduce<<<k, 256, 0, s>>>(colpart, nblocks, k, gate, colsum, psic);
   KERNEL_CHECK();
 }
 
@@ -1125,22 +1208,25 @@ void launch_transpose_kv(hipStream_t s, const double* lam, int64_t V, int k, dou
   KERNEL_CHECK();
 }
 
+// Spark's sstats from the scaled stat: stat'_vt = stat_vt · e^{m_v} · e^{−ψc_t} (r carries e^{m_v},
+// eθ the per-topic e^{−ψ(colsum_t)}), so stat_vt = stat'_vt · exp(ψc_t − m_v)
 template <typename T>
 __global__ __launch_bounds__(256) void k_unscale_stat(const T* __restrict__ stat,
-                                                      const double* __restrict__ logscale, int64_t V,
+                                                      const double* __restrict__ logscale,
+                                                      const double* __restrict__ psic, int64_t V,
                                                       int k, int kp, double* __restrict__ out) {
   const int64_t total = V * k;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
     const int64_t v = e / k;
     const int t = (int)(e - v * k);
-    out[e] = (double)stat[v * kp + t] * exp(-logscale[v]);
+    out[e] = (double)stat[v * kp + t] * exp(psic[t] - logscale[v]);
   }
 }
 
 template <typename T>
-void launch_unscale_stat(hipStream_t s, const T* stat, const double* logscale, int64_t V, int k,
-                         int kp, double* out_vk) {
-  k_unscale_stat<T><<<4096, 256, 0, s>>>(stat, logscale, V, k, kp, out_vk);
+void launch_unscale_stat(hipStream_t s, const T* stat, const double* logscale, const double* psic, int64_t V,
+                         int k, int kp, double* out_vk) {
+  k_unscale_stat<T><<<4096, 256, 0, s>>>(stat, logscale, psic, V, k, kp, out_vk);
   KERNEL_CHECK();
 }
 
@@ -1150,15 +1236,14 @@ void launch_unscale_stat(hipStream_t s, const T* stat, const double* logscale, i
   template void launch_estep<T>(hipStream_t, const EStepArgs<T>&, bool, bool);                    \
   template void launch_sstats<T>(hipStream_t, const uint32_t*, const uint64_t*, int64_t, const T*, \
                                  const T*, int, T*, T*, T*);                                      \
-  template void launch_lambda_update<T>(hipStream_t, double*, const T*, const T*, int64_t, int, int, \
-                                        double, double, double, const double*, double*, int64_t); \
-  template void launch_expelogbeta<T>(hipStream_t, const double*, const double*, int64_t, int, int, \
-                                      const double*, T*, double*);                               \
+  template void launch_lambda_eeb<T>(hipStream_t, bool, double*, const T*, T*, double*, int64_t, int, \
+                                     int, double, double, double, const double*, double*, int64_t);    \
   template void launch_logphat<T>(hipStream_t, const T*, const int32_t*, int64_t, int, double*, double*);  \
   template void launch_topics_bound<T>(hipStream_t, const double*, const double*, int64_t, int,   \
                                        double, double*, int64_t);                                 \
   template void launch_sum_vals<T>(hipStream_t, const T*, int64_t, double*);                      \
-  template void launch_unscale_stat<T>(hipStream_t, const T*, const double*, int64_t, int, int, double*);
+  template void launch_unscale_stat<T>(hipStream_t, const T*, const double*, const double*, int64_t, int, \
+                                       int, double*);
 
 STC_INSTANTIATE(float)
 STC_INSTANTIATE(double)

@@ -100,7 +100,7 @@ struct GDoc {
   int lane, wave, g, rl, nnz, k, kp, t0, tl, t, it;
   bool ok, own;
   int64_t slot, row, mem, s0, e0;
-  float gam, alp, eth, cs, gsum, asum;
+  float gam, alp, pc, eth, cs, gsum, asum;  // pc = exp(−ψ(Σ_v λ_vt)) of the owned topic (EStepArgs::psic)
   double b_tok, c_tok;
 #ifdef STC_STAMP
   unsigned long long st0;  // kernel entry (stamp build): the preamble's cycles go to stamp slot 11
@@ -193,7 +193,7 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
     float gsum = d.gsum, asum = d.asum, dsum = 0.f, dummy = 0.f;
     xchg<S>(sm, 1, wave, lane, nullptr, 0, gsum, asum);
     d.asum = asum;
-    // eθ = exp(ψ(γ) − ψ(Σγ)): Spark's unscaled exp(E[log θ]); inside the loop ψ(Σγ') comes from
+    // eθ' = exp(ψ(γ) − ψ(Σγ) − ψc_t): Spark's exp(E[log θ]) times expElogβ's per-topic factor; inside the loop ψ(Σγ') comes from
     // the Σα + Σcts − Σ cts·ε'/φ identity, so without live ε' it is one constant per document
     float cs = digamma_fast(gsum);
     float ct = 0.f;
@@ -201,8 +201,8 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
     for (int j = 0; j < R; ++j) ct += cts[j];
     const float ctot = 0.5f * wave_sum_dpp(ct);  // Σ_n cts_n (each row is held by both groups)
     const float cs_flat = digamma_fast(asum + ctot);
-    float gam = d.gam, eth = d.own ? __expf(digamma_fast(gam) - cs) : 0.f;
-    const float alp = d.alp;
+    const float alp = d.alp, pc = d.pc;
+    float gam = d.gam, eth = d.own ? __expf(digamma_fast(gam) - cs) * pc : 0.f;
     if (d.own) my_eth[d.tl] = eth;
     __builtin_amdgcn_wave_barrier();  // the slices are read back only by this wave
     int it = 0;
@@ -311,10 +311,10 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
         gam = d.own ? gn : gam;
       }
       STAMP(7);
-      // Phase D: eθ = exp(ψ(γ) − ψ(Σγ)) into the group's LDS slice; computed in every lane (no
+      // Phase D: eθ' = exp(ψ(γ) − ψ(Σγ) − ψc) into the group's LDS slice; computed in every lane (no
       // exec-mask region), stored by the owners
       cs = cs_next;
-      eth = d.own ? __expf(digamma_fast(d.own ? gam : 1.f) - cs) : 0.f;
+      eth = d.own ? __expf(digamma_fast(d.own ? gam : 1.f) - cs) * pc : 0.f;
       if (d.own) my_eth[d.tl] = eth;
       __builtin_amdgcn_wave_barrier();
       ++it;
@@ -393,6 +393,7 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_grid(EStepArgs<floa
   }
   d.gam = d.own ? (a.gamma0 ? a.gamma0[mem * k + t] : (float)gamma_sample(stream, t, a.gamma_shape)) : 0.f;
   d.alp = d.own ? (float)a.alpha[t] : 0.f;
+  d.pc = d.own ? (float)a.psic[d.k + t] : 0.f;
   d.gsum = wave_sum_dpp(d.gam);
   d.asum = wave_sum_dpp(d.alp);
   for (int i = lane; i < 2 * S::KLP; i += 64) (&sm.eth[d.wave][0][0])[i] = 0.f;  // pads stay zero

@@ -44,7 +44,8 @@ struct EStepArgs {
   // rarest terms first, so the register / LDS rows are the cold ones and the streamed rows the hot
   // ones the MALL holds for every CU); nullptr: CSR order
   const int32_t* order = nullptr;
-  const T* Bp = nullptr;               // V×kp  row-scaled expElogβ'
+  const T* Bp = nullptr;               // V×kp  row-scaled expElogβ': exp(ψ(λ_vt) − m_v)
+  const double* psic = nullptr;        // 2k    ψ(Σ_v λ_vt), then exp(−ψ(Σ_v λ_vt)): eθ' = exp(ψ(γ_t) − ψ(Σγ) − psic_t)
   const double* logscale = nullptr;    // V     m_v (BOUND)
   const double* alpha = nullptr;       // k
   const T* gamma0 = nullptr;           // n×k or nullptr (counter RNG)
@@ -132,17 +133,14 @@ template <typename T>
 void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, int64_t E,
                    const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf);
 
+// the fused M-step pass (update = true: λ update; both: expElogβ' rows, logscale, colsum partials)
 template <typename T>
-void launch_lambda_update(hipStream_t s, double* lam, const T* stat, const T* Bp, int64_t V, int k,
-                          int kp, double rho, double scale, double eta, const double* gate,
-                          double* colpart, int64_t nblocks);
-void launch_colsum_lambda(hipStream_t s, const double* lam, int64_t V, int k, double* colpart,
-                          int64_t nblocks);
+void launch_lambda_eeb(hipStream_t s, bool update, double* lam, const T* stat, T* Bp, double* logscale,
+                       int64_t V, int k, int kp, double rho, double scale, double eta, const double* gate,
+                       double* colpart, int64_t nblocks);
+// colsum (block order), psic[0, k) = ψ(colsum), psic[k, 2k) = exp(−ψ(colsum))
 void launch_colsum_reduce(hipStream_t s, const double* colpart, int64_t nblocks, int k,
-                          const double* gate, double* colsum);
-template <typename T>
-void launch_expelogbeta(hipStream_t s, const double* lam, const double* colsum, int64_t V, int k,
-                        int kp, const double* gate, T* Bp, double* logscale);
+                          const double* gate, double* colsum, double* psic);
 template <typename T>
 void launch_logphat(hipStream_t s, const T* elogth, const int32_t* nonempty, int64_t n, int k,
                     double* small /* k+1 */, double* part /* kLogphatBlocks × (k+1) scratch */);
@@ -176,8 +174,8 @@ void launch_fill_batch(hipStream_t s, const int64_t* indptr, int64_t D, int64_t 
 void launch_transpose_kv(hipStream_t s, const double* lam, int64_t V, int k, double* out_kv,
                          int32_t* idx_kv);
 template <typename T>
-void launch_unscale_stat(hipStream_t s, const T* stat, const double* logscale, int64_t V, int k,
-                         int kp, double* out_vk);
+void launch_unscale_stat(hipStream_t s, const T* stat, const double* logscale, const double* psic, int64_t V,
+                         int k, int kp, double* out_vk);
 
 }  // namespace lda
 }  // namespace stc

@@ -31,6 +31,9 @@
 #ifndef R64_LOAD_BATCH
 #define R64_LOAD_BATCH 2  // row sets whose B loads are in flight together in the load phase
 #endif
+#ifndef R64_PRIO
+#define R64_PRIO 2  // wave priority raised over the latency-critical phases (1: ψ; 2: ψ + r): −2 % E-step (r03)
+#endif
 #ifndef R64_LONG_OCC
 #define R64_LONG_OCC 1  // long-document kernel workgroups per CU the register budget is cut for
 #endif
@@ -189,6 +192,7 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
   const bool town = lane < half && tt < k;   // a real topic
   const int ttl = tt / KL, ttp = tt - ttl * KL;
   const double alp = town ? a.alpha[tt] : 0.0;
+  const double pc = town ? a.psic[tt] : 0.0;  // ψ(Σ_v λ_vt): expElogβ's per-topic factor, carried by eθ
 
   // ---- worker lane: wave row q = lane (set q >> 3, row lane q & 7) → document row qn
   const int qn = 32 * (lane >> 3) + 8 * w + (lane & 7);
@@ -294,12 +298,12 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
     }
     return;
   }
-  // eθ = exp(ψ(γ) − ψ(Σγ)): Spark's unscaled exp(E[log θ]); inside the loop ψ(Σγ') comes from the
+  // eθ' = exp(ψ(γ) − ψ(Σγ) − ψc_t): Spark's exp(E[log θ]) times expElogβ's per-topic factor; inside the loop ψ(Σγ') comes from the
   // Σα + Σcts − Σ r·ε' identity, so without a visible ε' it is one constant per document
   const double cs_flat = digamma_fast_d(asum + ctot);
   {
     const double cs0 = digamma_fast_d(gsum0);
-    if (w < npsi && town) sm.eth[ttl][ttp] = exp_digamma_minus_s(g0, cs0);
+    if (w < npsi && town) sm.eth[ttl][ttp] = exp_digamma_minus_s(g0, cs0 + pc);
     if (threadIdx.x == 0) sm.cs = cs0;
   }
   __syncthreads();
@@ -332,6 +336,7 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
     }
     STAMP(1);  // eθ reads, φ FMAs, partial stores
     __builtin_amdgcn_wave_barrier();
+    if (R64_PRIO >= 2) __builtin_amdgcn_s_setprio(3);
     bool live = false;
     if (lane < 8 * R) {
       const double2* const pr = reinterpret_cast<const double2*>(pa + lane * kPaPitch);
@@ -351,6 +356,7 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int j = 0; j < R; ++j) rr[j] = sm.rrow[w][8 * j + rl];
+    if (R64_PRIO >= 2) __builtin_amdgcn_s_setprio(0);
     STAMP(2);  // worker sums, r, ε' ballot, r reads
     // Spark: while (meanGammaChange > 1e-3); dsum is block-uniform (every wave adds the same LDS
     // values in the same order)
@@ -369,6 +375,7 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
     STAMP(4);  // barrier 1
     const bool psi = npsi == 2 ? ((w >> 1) == (it & 1)) : (w == (it & 3));
     if (psi) {
+      if (R64_PRIO >= 1) __builtin_amdgcn_s_setprio(3);
       double dg = 0.0;
       if (town) {
         // every LDS read of the phase issued together: the 32 partials, γ, eθ, the four ε' sums
@@ -391,11 +398,12 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
         const double gn = fma(eo, s, alp);  // γ ← eθ ⊙ s + α
         dg = fabs(gn - g);
         sm.gam[tt] = gn;
-        sm.eth[ttl][ttp] = exp_digamma_minus_s(gn, csn);
+        sm.eth[ttl][ttp] = exp_digamma_minus_s(gn, csn + pc);
         if (tt == 0) sm.cs = csn;
       }
       const double d = wave_sum_d(dg);
       if (lane == 0) sm.dsum[pw] = d;
+      if (R64_PRIO >= 1) __builtin_amdgcn_s_setprio(0);
     }
     STAMP(psi ? 5 : 8);  // ψ phase (ψ waves; non-ψ waves: nothing)
     __syncthreads();  // (2) eθ, γ, Σ|Δγ| published

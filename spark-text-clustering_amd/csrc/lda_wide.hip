@@ -34,7 +34,9 @@ template <>
 struct WTr<float> {
   static __device__ __forceinline__ float wsum(float v) { return wave_sum_dpp(v); }
   static __device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
-  static __device__ __forceinline__ float eth(float g, float cs) { return __expf(digamma_fast(g) - cs); }
+  // eθ' = exp(ψ(g) − cs)·exp(−ψc): pc holds exp(−ψc) (an fp32 argument − ψc would lose its low bits)
+  static __device__ __forceinline__ float eth(float g, float cs, float pc) { return __expf(digamma_fast(g) - cs) * pc; }
+  static __device__ __forceinline__ float pcload(const double* psic, int k, int t) { return (float)psic[k + t]; }
   static __device__ __forceinline__ float psi(float x) { return digamma_fast(x); }
   static __device__ __forceinline__ float eps_floor() { return kTiny; }
   static __device__ __forceinline__ float eps_cap() { return 3.0e38f; }
@@ -66,7 +68,9 @@ template <>
 struct WTr<double> {
   static __device__ __forceinline__ double wsum(double v) { return wave_sum_d(v); }
   static __device__ __forceinline__ double rcp(double x) { return rcp_nr(x); }
-  static __device__ __forceinline__ double eth(double g, double cs) { return exp_digamma_minus_d(g, cs); }
+  // eθ' = exp(ψ(g) − cs − ψc): pc holds ψc
+  static __device__ __forceinline__ double eth(double g, double cs, double pc) { return exp_digamma_minus_d(g, cs + pc); }
+  static __device__ __forceinline__ double pcload(const double* psic, int k, int t) { (void)k; return psic[t]; }
   static __device__ __forceinline__ double psi(double x) { return digamma_fast_d(x); }
   static __device__ __forceinline__ double eps_floor() { return 0.0; }
   static __device__ __forceinline__ double eps_cap() { return 1e300; }
@@ -257,13 +261,14 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
     const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, mem) : (uint64_t)(a.doc_id_base + row);
     stream = doc_stream(a.seed, key);
   }
-  T gam[Q], alp[Q], eth[Q];
+  T gam[Q], alp[Q], pc[Q], eth[Q];  // pc: expElogβ's per-topic factor (WTr::pcload)
   T gs = T(0), as = T(0);
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     const int t = t0 + q;
     gam[q] = t < k ? (a.gamma0 ? a.gamma0[mem * k + t] : (T)gamma_sample(stream, t, a.gamma_shape)) : T(0);
     alp[q] = t < k ? (T)a.alpha[t] : T(0);
+    pc[q] = t < k ? Tr::pcload(a.psic, k, t) : T(0);
     gs += gam[q];
     as += alp[q];
   }
@@ -326,7 +331,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
   for (int n = nnz + tid; n < kWRows; n += kWThreads) sm.rr[n] = T(0);  // Phase B reads rows in 8s
   T cs = Tr::psi(gs);  // ψ(Σγ) of the current γ
 #pragma unroll
-  for (int q = 0; q < Q; ++q) eth[q] = (t0 + q < k) ? Tr::eth(gam[q], cs) : T(0);
+  for (int q = 0; q < Q; ++q) eth[q] = (t0 + q < k) ? Tr::eth(gam[q], cs, pc[q]) : T(0);
   T dg = T(0);  // Σ_q |Δγ| of this lane's topics in the last update
   int it = 0;
   double b_tok = 0.0, c_tok = 0.0;
@@ -432,7 +437,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
         const T gn = fma(eth[q], s[q], alp[q]);
         dg += fabs(gn - gam[q]);
         gam[q] = gn;
-        eth[q] = Tr::eth(gn, cs);
+        eth[q] = Tr::eth(gn, cs, pc[q]);
       }
     }
     ++it;
@@ -634,13 +639,14 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
       const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, mem) : (uint64_t)(a.doc_id_base + row);
       stream = doc_stream(a.seed, key);
     }
-    T gam[Q], alp[Q], eth[Q];
+    T gam[Q], alp[Q], pc[Q], eth[Q];  // pc: expElogβ's per-topic factor (WTr::pcload)
     T gs = T(0), as = T(0);
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int t = t0 + q;
       gam[q] = t < k ? (a.gamma0 ? a.gamma0[mem * k + t] : (T)gamma_sample(stream, t, a.gamma_shape)) : T(0);
       alp[q] = t < k ? (T)a.alpha[t] : T(0);
+      pc[q] = t < k ? Tr::pcload(a.psic, k, t) : T(0);
       gs += gam[q];
       as += alp[q];
     }
@@ -695,7 +701,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
     if (tid >= nloc) sm.rr[tid] = T(0);  // Phase B reads rows in 8s (published by barrier (1))
     T cs = Tr::psi(gs);
 #pragma unroll
-    for (int q = 0; q < Q; ++q) eth[q] = (t0 + q < k) ? Tr::eth(gam[q], cs) : T(0);
+    for (int q = 0; q < Q; ++q) eth[q] = (t0 + q < k) ? Tr::eth(gam[q], cs, pc[q]) : T(0);
     T dg = T(0);
     int it = 0;
     const T kd = (T)k;
@@ -847,7 +853,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
           const T gn = fma(eth[q], st[q], alp[q]);
           dg += fabs(gn - gam[q]);
           gam[q] = gn;
-          eth[q] = Tr::eth(gn, cs);
+          eth[q] = Tr::eth(gn, cs, pc[q]);
         }
       }
       ++it;
@@ -979,12 +985,13 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
       const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, mem) : (uint64_t)(a.doc_id_base + row);
       stream = doc_stream(a.seed, key);
     }
-    T gam[Q], alp[Q], eth[Q];
+    T gam[Q], alp[Q], pc[Q], eth[Q];  // pc: expElogβ's per-topic factor (WTr::pcload)
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int t = t0 + q;
       gam[q] = t < k ? (a.gamma0 ? a.gamma0[mem * k + t] : (T)gamma_sample(stream, t, a.gamma_shape)) : T(0);
       alp[q] = t < k ? (T)a.alpha[t] : T(0);
+      pc[q] = t < k ? Tr::pcload(a.psic, k, t) : T(0);
     }
     if (!nonempty) {
 #pragma unroll
@@ -1048,7 +1055,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
 
     T cs = Tr::psi(gs);
 #pragma unroll
-    for (int q = 0; q < Q; ++q) eth[q] = (t0 + q < k) ? Tr::eth(gam[q], cs) : T(0);
+    for (int q = 0; q < Q; ++q) eth[q] = (t0 + q < k) ? Tr::eth(gam[q], cs, pc[q]) : T(0);
     T dg = T(0);
     int it = 0;
     const T kd = (T)k;
@@ -1175,7 +1182,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
           const T gn = fma(eth[q], s[q], alp[q]);
           dg += fabs(gn - gam[q]);
           gam[q] = gn;
-          eth[q] = Tr::eth(gn, cs);
+          eth[q] = Tr::eth(gn, cs, pc[q]);
         }
       }
       ++it;

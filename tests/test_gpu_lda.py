@@ -1,9 +1,10 @@
 """GPU parity for the online-LDA path (K6–K12) through the C ABI vs the CPU oracle and the
 reference's known answers (tests/golden/en_topicdist.json, en_describe.json).
 
-Tolerances: f64 mode restates Spark's double arithmetic, so λ/γ/bound agree to ~1e-9 relative; f32
-mode (the default, the benchmarked path) is checked against the north-star bars: topicsMatrix
-within 1e-4 relative, logPerplexity within 1e-5 relative, identical top-10 terms per topic.
+Tolerances: f64 mode (the default and the benchmark headline) restates Spark's double arithmetic, so
+λ/γ/bound agree to ~1e-9 relative; f32 mode (the fast secondary) is checked against the north-star
+bars: topicsMatrix within 1e-4 relative, logPerplexity within 1e-5 relative, identical top-10 terms
+per topic.
 """
 import numpy as np
 import pytest
@@ -115,11 +116,12 @@ def test_estep_long_documents_global_path(ctx, oracle):
 
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
-@pytest.mark.parametrize("optimize_alpha", [True, False])
-def test_minibatch_steps_match_oracle(ctx, oracle, dtype, optimize_alpha):
-    """Injected λ₀, membership (with duplicates) and γ₀: λ and α after 3 submitMiniBatch calls."""
+@pytest.mark.parametrize("optimize_alpha,k", [(True, 12), (False, 12), (True, 300)])
+def test_minibatch_steps_match_oracle(ctx, oracle, dtype, optimize_alpha, k):
+    """Injected λ₀, membership (with duplicates) and γ₀: λ and α after 3 submitMiniBatch calls (k = 300:
+    the many-topic E-step and the row-per-workgroup M-step pass)."""
     rng = np.random.default_rng(12)
-    D, V, k = 80, 1024, 12
+    D, V = 80, 1024
     corpus = random_corpus(rng, D, V, 1, 60, empty_every=17)
     lam0 = rng.gamma(100.0, 0.01, size=(V, k))
     frac = 0.3
@@ -324,15 +326,14 @@ def _train(ctx, corpus, k, dtype, steps, reset_each=False, **kw):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "f64"])
-@pytest.mark.parametrize("V,shards", [(1000, 3), (100, 4), (4096, 2)])
-def test_sharded_mstep_slices_bit_identical(ctx, monkeypatch, dtype, V, shards):
+@pytest.mark.parametrize("V,shards,k", [(1000, 3, 12), (100, 4, 12), (4096, 2, 12), (1000, 3, 300)])
+def test_sharded_mstep_slices_bit_identical(ctx, monkeypatch, dtype, V, shards, k):
     """The multi-GPU M-step's vocabulary slices (ranks' λ / expElogβ rows, colsum partials placed
     where the one-GPU reduction has them), run on one GPU with STC_VIRTUAL_SHARDS: λ, α, the bound
     and topicDistribution are bit-identical to the unsliced M-step — including a ragged last slice
     and slices past V (V = 100 over 4 shards of 64 rows)."""
     rng = np.random.default_rng(40 + V)
     corpus = random_corpus(rng, 300, V, 1, 40, empty_every=17)
-    k = 12
     h1, d1 = _train(ctx, corpus, k, dtype, 6)
     monkeypatch.setenv("STC_VIRTUAL_SHARDS", str(shards))
     h2, d2 = _train(ctx, corpus, k, dtype, 6)

@@ -22,6 +22,14 @@ if [ -n "$OLD_LIB" ]; then  # a previous build of libstc.so, e.g. saved before a
   step b_old 240 env STC_LIB=$OLD_LIB $B
   step p_old 240 env STC_LIB=$OLD_LIB $B $P
 fi
+for lib in $LIBS; do  # experiment builds, e.g. LIBS="libstc_p1.so": headline (and planted) lines with each
+  n=${lib%.so}; n=${n#libstc_}
+  step b_$n 240 env STC_LIB=spark-text-clustering_amd/stc/$lib $B
+  if [ -n "$LIBS_PLANTED" ]; then step p_$n 240 env STC_LIB=spark-text-clustering_amd/stc/$lib $B $P; fi
+done
+if [ -n "$CONFIGS" ]; then  # e.g. CONFIGS="5 4": the many-topic shapes' headline lines
+  for c in $CONFIGS; do step c${c}_new 400 $B --config $c; done
+fi
 if [ -n "$STAMP" ]; then
   step stamp 200 env STC_LIB=spark-text-clustering_amd/stc/libstc_stamp.so python tools/stamp_rows64.py
   step stampp 200 env STC_LIB=spark-text-clustering_amd/stc/libstc_stamp.so python tools/stamp_rows64.py --corpus zipf-lda
