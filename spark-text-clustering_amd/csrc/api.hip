@@ -591,7 +591,7 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
     const TeamChoice tc = use_wide(L.k, L.dtype) && !bound ? team_choice<T>(L, mean_rows) : TeamChoice{};
     const bool team = tc.P > 1 && launch_wide_team<T>(L, w, stats, tc);
     if (team) {
-      // launched (a refused cooperative grid falls through to the one-CU kernel)
+      // launched (a grid that could not be resident falls through to the one-CU kernel)
     } else if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
     else if constexpr (std::is_same<T, float>::value) lda::launch_estep_grid(s, w, stats, bound);
     else lda::launch_estep_rows64(s, w, stats, bound, m.max_row < 0 || m.max_row > lda::rows64_onchip_rows(L.k));

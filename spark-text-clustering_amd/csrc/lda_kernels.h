@@ -113,7 +113,7 @@ struct WideTeam {
 void launch_gate_on_timeout(hipStream_t s, const unsigned* tmo, double* small, int k);
 template <typename T>
 int wide_resident_rows(int k);
-// false: the runtime refused the cooperative grid (nothing launched; the caller runs the one-CU kernel)
+// false: the grid could not be resident at once (nothing launched; the caller runs the one-CU kernel)
 template <typename T>
 bool launch_estep_wide_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt);
 // the same with the TOPICS split over the team (k > 512; lda_wide.hip k_estep_wide_tc)

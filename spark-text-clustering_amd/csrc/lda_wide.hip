@@ -525,7 +525,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
 //               identity); every member sums the P partials in member order, so γ, eθ and the stop
 //               rule are bit-identical in every member and the team leaves the loop together.
 // Persistent: G = 8·P·⌊CUs/(8P)⌋ blocks (one per CU: the kernel takes all 160 KB of LDS), launched
-// cooperatively (the runtime checks the grid is resident); team members share blockIdx % 8 (one XCD,
+// once the occupancy check says the grid is resident (launch_resident); team members share blockIdx % 8 (one XCD,
 // for L2 locality only).  Exchange (cdna_hip_programming.md Guideline 16, R2: the data is the flag):
 // every value travels in a 16-byte granule {epoch, value} written by ONE 16-B sc1 buffer store and
 // read by 16-B sc1 buffer loads (untorn on gfx950); each consumer wave re-reads its granules until
@@ -1283,6 +1283,24 @@ int wide_resident_rows(int k) {
   return rows(std::integral_constant<int, 4>{});
 }
 
+// The persistent team grid, launched only if every block can be resident at once: the kernel's
+// occupancy (blocks per CU at this LDS size) × the device's CUs must cover the grid (false: nothing
+// launched, the caller runs the one-CU kernel).  A plain launch, not hipLaunchCooperativeKernel: the
+// cooperative launch path made every profiled process (rocprofv3 --kernel-trace) fault at exit inside
+// the HSA runtime's teardown, after the profiler's finalisation (r03 exit probe: libamdhip64 exit
+// handler → libhsa-runtime64, on a /dev/dri mapping already released).  Residency is checked here; a
+// block that is nonetheless not co-resident (another process on the device) only delays its team, and
+// the bounded spins turn a delay past the limit into STC_ERR_HIP with λ untouched (launch_gate_on_timeout).
+inline bool launch_resident(const void* kern, int blocks, size_t lds, void** args, hipStream_t s) {
+  int dev = 0, cus = 0, per_cu = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kWThreads, lds));
+  if ((int64_t)per_cu * cus < blocks) return false;
+  HIP_CHECK(hipLaunchKernel(kern, dim3((unsigned)blocks), dim3(kWThreads), args, lds, s));
+  return true;
+}
+
 template <typename T, int Q>
 bool launch_q_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
   bool ok = true;
@@ -1296,13 +1314,7 @@ bool launch_q_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTea
     EStepArgs<T> aa = a;
     WideTeam ww = wt;
     void* args[] = {&aa, &nl, &ww};
-    // the runtime rejects a grid that could not be resident (hipErrorCooperativeLaunchTooLarge):
-    // reported to the caller, which runs the one-CU kernel instead
-    const hipError_t e = hipLaunchCooperativeKernel((const void*)kern, dim3((unsigned)wt.blocks), dim3(kWThreads), args, lds, s);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      ok = false;
-    }
+    ok = launch_resident((const void*)kern, wt.blocks, lds, args, s);
   };
   if (stats) go(k_estep_wide_mc<T, Q, NR, true>);
   else go(k_estep_wide_mc<T, Q, NR, false>);
@@ -1322,13 +1334,7 @@ bool launch_q_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTea
     EStepArgs<T> aa = a;
     WideTeam ww = wt;
     void* args[] = {&aa, &nl, &ww};
-    // the runtime rejects a grid that could not be resident (hipErrorCooperativeLaunchTooLarge):
-    // reported to the caller, which runs the one-CU kernel instead
-    const hipError_t e = hipLaunchCooperativeKernel((const void*)kern, dim3((unsigned)wt.blocks), dim3(kWThreads), args, lds, s);
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      ok = false;
-    }
+    ok = launch_resident((const void*)kern, wt.blocks, lds, args, s);
   };
   if (stats) go(k_estep_wide_tc<T, Q, NR, true>);
   else go(k_estep_wide_tc<T, Q, NR, false>);
