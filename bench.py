@@ -164,7 +164,11 @@ def cpu_baseline(h, corpus, a, budget_s=12.0):
 
     if not c_oracle.available():
         return None
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    # the host cores this process may use: the lease's share (OMP_NUM_THREADS, which the GPU box sets to
+    # its 16-core share per GPU), else every core in the affinity mask
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = omp or len(os.sched_getaffinity(0))
+    why = "OMP_NUM_THREADS (the lease's core share)" if omp else "the process's affinity mask"
     lam = np.ascontiguousarray(h.topics().T)  # k×V, Spark's internal orientation
     alpha = np.ascontiguousarray(h.alpha())
     eta = h.eta()
@@ -187,7 +191,7 @@ def cpu_baseline(h, corpus, a, budget_s=12.0):
     return {"value": done / dt, "unit": "docs/s", "cores": threads, "kind": "port",
             "sample": f"{steps} whole minibatch steps ({done} docs, Bernoulli({a.fraction}) of the same corpus; "
                       f"E-step + per-thread dense k×V stats + reduce + λ/α update, fp64) from the GPU model "
-                      f"after the timed steps; oracle/lda_oracle.c oracle_minibatch, OpenMP {threads} threads; "
+                      f"after the timed steps; oracle/lda_oracle.c oracle_minibatch, OpenMP {threads} threads = {why}; "
                       f"mean inner iters {iters / max(1, done):.1f}; {dt:.1f} s"}
 
 

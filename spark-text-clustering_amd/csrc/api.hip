@@ -60,6 +60,12 @@ struct stc_lda {
       nonempty, r, keys, vals, skeys, svals, stat, headbuf, tailbuf, sort_tmp, scan_tmp,
       stats4, cum2, bound, dtmp, lpart;
   DevBuf s_counts, s_weights, s_short, s_cincl, s_wincl, s_sincl;
+  // the next draw is sampled on a side stream, concurrently with this step's E-step (it reads only
+  // indptr and writes only the s_* buffers, which this step's fill_batch has consumed)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fill = nullptr, ev_samp = nullptr;
+  bool samp_pending = false;
+  DevBuf side_scan_tmp;
   DevBuf o_keys, o_keys2, o_idx, o_idx2, o_batch, o_orig, o_nnz, o_tmp;  // slot ordering (order_slots)
   bool sort_docs = true;  // STC_SORT_DOCS=0 keeps sampling order
   // many-topic kernel: per-entry row order, rarest terms first (lda_wide.hip), for `order_for`
@@ -111,6 +117,9 @@ struct stc_lda {
     if (hpre) (void)hipHostFree(hpre);
     if (htmo) (void)hipHostFree(htmo);
     if (ev_pre) (void)hipEventDestroy(ev_pre);
+    if (ev_fill) (void)hipEventDestroy(ev_fill);
+    if (ev_samp) (void)hipEventDestroy(ev_samp);
+    if (side) (void)hipStreamDestroy(side);
   }
 };
 
@@ -372,12 +381,14 @@ void ensure_batch(stc_lda& L, int64_t n, int64_t E) {
 }
 
 template <typename X>
-void incl_scan(stc_lda& L, const X* in, X* out, int64_t n) {
+void incl_scan(stc_lda& L, const X* in, X* out, int64_t n, hipStream_t s = nullptr, DevBuf* tmp = nullptr) {
   if (n <= 0) return;
+  if (!s) s = L.ctx->stream;
+  if (!tmp) tmp = &L.scan_tmp;
   size_t sb = 0;
-  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, sb, in, out, (int)n, L.ctx->stream));
-  L.scan_tmp.reserve(sb);
-  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(L.scan_tmp.p, sb, in, out, (int)n, L.ctx->stream));
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, sb, in, out, (int)n, s));
+  tmp->reserve(sb);
+  HIP_CHECK(hipcub::DeviceScan::InclusiveSum(tmp->p, sb, in, out, (int)n, s));
 }
 
 // bptr[0] = 0, bptr[i+1] = Σ_{j<=i} nnz_p[j]  (entry offsets of the partitioned slots)
@@ -693,6 +704,10 @@ void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
   Ctx& c = *L.ctx;
   hipStream_t s = c.stream;
   const bool ranks = c.coll() && (c.n_ranks > 1 || L.force_coll);
+  if (L.samp_pending) {  // the next draw's counts (side stream) feed this step's collective / readback
+    HIP_CHECK(hipStreamWaitEvent(s, L.ev_samp, 0));
+    L.samp_pending = false;
+  }
   if (c.coll()) {
     coll_group_start(c);
     if (ranks) {
@@ -798,17 +813,16 @@ void step_ids(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, s
 
 // sample draw `draw` on the device: per-doc counts (Poisson / Bernoulli), their scans, and (n, E,
 // n_short) into dcnt words 0–2, word 3 = n (all-reduced to the global n by the caller)
-void sample_draw(stc_lda& L, int64_t draw) {
+void sample_draw(stc_lda& L, int64_t draw, hipStream_t s, DevBuf* tmp) {
   Ctx& c = *L.ctx;
-  hipStream_t s = c.stream;
   const int64_t D = L.corpus->rows;
   if (D > 0) {
     lda::launch_sample(s, L.corpus->indptr.as<int64_t>(), D, L.cfg.mini_batch_fraction,
                        L.cfg.sample_with_replacement, L.cfg.seed, draw, c.rank, L.wave_cap,
                        L.s_counts.as<int32_t>(), L.s_weights.as<int64_t>(), L.s_short.as<int32_t>());
-    incl_scan<int32_t>(L, L.s_counts.as<int32_t>(), L.s_cincl.as<int32_t>(), D);
-    incl_scan<int64_t>(L, L.s_weights.as<int64_t>(), L.s_wincl.as<int64_t>(), D);
-    incl_scan<int32_t>(L, L.s_short.as<int32_t>(), L.s_sincl.as<int32_t>(), D);
+    incl_scan<int32_t>(L, L.s_counts.as<int32_t>(), L.s_cincl.as<int32_t>(), D, s, tmp);
+    incl_scan<int64_t>(L, L.s_weights.as<int64_t>(), L.s_wincl.as<int64_t>(), D, s, tmp);
+    incl_scan<int32_t>(L, L.s_short.as<int32_t>(), L.s_sincl.as<int32_t>(), D, s, tmp);
     // (n, E, n_short) from the scans' last elements: one kernel packs them, one copy to pinned memory
     lda::launch_last3(s, L.s_cincl.as<int32_t>() + (D - 1), L.s_wincl.as<int64_t>() + (D - 1),
                       L.s_sincl.as<int32_t>() + (D - 1), L.dcnt.as<int64_t>());
@@ -850,7 +864,7 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
     HIP_CHECK(hipEventSynchronize(L.ev_pre));
     std::copy(L.hpre, L.hpre + 4, cnt);
   } else {
-    sample_draw(L, draw);
+    sample_draw(L, draw, s, &L.scan_tmp);
     if (c.coll()) coll_all_reduce(c, L.dcnt.as<int64_t>() + 3, 1, ncclInt64, s);
     HIP_CHECK(hipMemcpyAsync(L.hcnt, L.dcnt.p, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
@@ -871,7 +885,17 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
                            L.orig.as<int32_t>(), L.nnzp.as<int64_t>());
   order_slots(L, ns32);
   slot_offsets(L, n);
-  sample_draw(L, draw + 1);  // the next draw, counted with this step's collective
+  // the next draw, on the side stream beside this step's E-step, counted with this step's collective
+  if (!L.side) {
+    HIP_CHECK(hipStreamCreateWithFlags(&L.side, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&L.ev_fill, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&L.ev_samp, hipEventDisableTiming));
+  }
+  HIP_CHECK(hipEventRecord(L.ev_fill, s));  // this draw's counts consumed (fill_batch, slot order)
+  HIP_CHECK(hipStreamWaitEvent(L.side, L.ev_fill, 0));
+  sample_draw(L, draw + 1, L.side, &L.side_scan_tmp);
+  HIP_CHECK(hipEventRecord(L.ev_samp, L.side));
+  L.samp_pending = true;
   L.pre_inflight = true;
   L.pre_draw = draw + 1;
   estep_and_stats<T>(L, n, ns32, E, nullptr, L.iteration + 1);

@@ -29,7 +29,7 @@
 #include "estep_common.h"
 
 #ifndef R64_LOAD_BATCH
-#define R64_LOAD_BATCH 2  // row sets whose B loads are in flight together in the load phase
+#define R64_LOAD_BATCH 3  // row sets whose B loads are in flight together in the load phase (r03: 2 → 3, −2 %)
 #endif
 #ifndef R64_PRIO
 #define R64_PRIO 2  // wave priority raised over the latency-critical phases (1: ψ; 2: ψ + r): −2 % E-step (r03)
@@ -159,10 +159,13 @@ struct RLds {
   double eth[8][S::KLP] __attribute__((aligned(16)));  // eθ, topic t at [t / KL][t % KL]
   double gam[S::KT];               // γ
   double rrow[kW][8 * S::RMAX];    // r = cts/φ per (wave, wave row)
+  int rid[kW][8 * S::RMAX];        // term id per (wave, wave row): the coalesced entry outputs
   double dsum[2];                  // Σ|Δγ| of the last update per ψ wave
   double esum[kW] __attribute__((aligned(16)));  // Σ r·ε' over a wave's rows (0 unless an ε' is visible)
   double part[kW][4];              // per-wave partial sums (init: Σγ₀, Σα, Σcts; end: Σγ, bound terms)
   double cs;                       // ψ(Σγ') of the current eθ (the bound's scale)
+  double apc[S::KT][2] __attribute__((aligned(16)));  // α_t, ψc_t of the ψ lanes' topics (not in VGPRs)
+  double ac[4] __attribute__((aligned(16)));  // Σα, Σcts, ψ(Σα + Σcts) (the flat ψ(Σγ'))
   union {
     struct {
       double pa[kW][8 * S::RMAX][kPaPitch];  // φ partials (wave, wave row, topic lane)
@@ -173,38 +176,135 @@ struct RLds {
   double ovf[S::NOVF > 0 ? S::NOVF * kW * S::KL * 64 : 1];  // row sets past RREG ([set][w][p][lane])
 };
 
-template <class S, int R, bool STATS, bool BOUND>
-__device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& sm, int64_t slot, int64_t row,
-                                           int64_t mem, int64_t s0, int64_t e0, int nnz) {
+// Per-lane document context: set up once per document by rows64_open, outside the row-set
+// specialisation, and read by the R-specialised loop (rows64_iterate) and by rows64_close.  Only the
+// block loads and the loop are instantiated per R: the prologue (γ₀ from the counter RNG — fp64 log,
+// sqrt, cos — and the first eθ) and the epilogue (digamma / lgamma of the outputs) exist once per
+// kernel.  Per R they made the common kernel 170 KB of code, past the 64 KB instruction cache a CU
+// pair shares, and documents that iterate a dozen times (the planted state) paid instruction-fetch
+// misses for the whole prologue of every document.
+struct RDoc {
+  int64_t slot, row, mem, s0, e0;
+  int nnz, rsets;
+  int lane, w, tl, rl;
+  int npsi, half, pw, tt, ttl, ttp;  // ψ-lane topic map
+  bool tval, town;                   // γ / eθ slot (the fp64 pad column included); a real topic
+  bool wv;                           // worker lane with a document row
+  int qid;                           // worker: term id, count, m_v, 2^53·ε'
+  double qc, qls, qe2;
+};
+
+// worker lanes, γ₀, α / ψc, Σγ₀ / Σα / Σcts, the first eθ; false (outputs written) for a document
+// without a nonzero count
+template <class S, bool STATS, bool BOUND>
+__device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>& sm, RDoc& d) {
+  constexpr int KL = S::KL, KLP = S::KLP;
+  const int k = a.k, kp = a.kp;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  d.lane = lane;
+  d.w = w;
+  d.tl = lane & 7;
+  d.rl = lane >> 3;
+  // ψ-lane topic map: k > 64 two ψ waves of `half` topics (t = (w & 1)·half + lane), else one
+  d.npsi = kp > 64 ? 2 : 1;
+  d.half = d.npsi == 2 ? (kp + 1) / 2 : kp;
+  d.pw = d.npsi == 2 ? (w & 1) : 0;
+  d.tt = d.pw * d.half + lane;
+  d.tval = lane < d.half && d.tt < kp;
+  d.town = lane < d.half && d.tt < k;
+  d.ttl = d.tt / KL;
+  d.ttp = d.tt - d.ttl * KL;
+  const int npsi = d.npsi, tt = d.tt;
+
+  // ---- worker lane: wave row q = lane (set q >> 3, row lane q & 7) → document row qn
+  const int qn = 32 * (lane >> 3) + 8 * w + (lane & 7);
+  d.wv = lane < 8 * d.rsets && qn < d.nnz;
+  const int64_t qe = d.wv ? d.s0 + qn : 0;
+  d.qid = d.wv ? a.indices[qe] : 0;
+  d.qc = d.wv ? a.values[qe] : 0.0;
+  d.qls = a.logscale[d.qid];
+  // ε'_q = 1e-100·e^{-m_v} held as 2^53·ε' (the test 2^53·ε' ≥ φ is then direct), capped at 1e300
+  // where e^{-m_v} overflows (Spark's unscaled row is 0 there; r ≈ cts·1e-284 reproduces that).
+  // Padding rows hold −2^53 (φ = −1, r = −0, never live).
+  d.qe2 = d.wv ? fmin(0x1p53 * exp(kLogEps - d.qls), 1e300) : -0x1p53;
+
+  // ---- γ₀ / α partials (the first npsi waves hold the topics), Σcts, eθ pads, α and ψc to LDS
+  double g0 = 0.0;
+  const double alp = d.town ? a.alpha[tt] : 0.0;
+  const double pc = d.town ? a.psic[tt] : 0.0;  // ψ(Σ_v λ_vt): expElogβ's per-topic factor, carried by eθ
+  if (w < npsi) {
+    if (d.tval) {
+      sm.apc[tt][0] = alp;
+      sm.apc[tt][1] = pc;
+    }
+    if (d.town) {
+      if (a.gamma0) {
+        g0 = a.gamma0[d.mem * k + tt];
+      } else {
+        const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, d.mem) : (uint64_t)(a.doc_id_base + d.row);
+        g0 = gamma_sample(doc_stream(a.seed, key), tt, a.gamma_shape);
+      }
+    }
+    if (d.tval) sm.gam[tt] = g0;
+  }
+  for (int i = threadIdx.x; i < 8 * KLP; i += 64 * kW) (&sm.eth[0][0])[i] = 0.0;
+  {
+    const double gs = wave_sum_d(g0), as = wave_sum_d(alp), cts = wave_sum_d(d.qc);
+    if (lane == 0) {
+      sm.part[w][0] = w < npsi ? gs : 0.0;
+      sm.part[w][1] = w < npsi ? as : 0.0;
+      sm.part[w][2] = cts;
+    }
+  }
+  const bool nonempty = __syncthreads_or(d.wv && d.qc != 0.0) != 0;  // (also publishes γ₀ and the partials)
+  const double gsum0 = (sm.part[0][0] + sm.part[1][0]) + (sm.part[2][0] + sm.part[3][0]);
+  if (threadIdx.x == 0) {  // read back by the ψ phase and the bound (published by the next barrier)
+    const double asum = (sm.part[0][1] + sm.part[1][1]) + (sm.part[2][1] + sm.part[3][1]);
+    const double ctot = (sm.part[0][2] + sm.part[1][2]) + (sm.part[2][2] + sm.part[3][2]);
+    sm.ac[0] = asum;
+    sm.ac[1] = ctot;
+    // inside the loop ψ(Σγ') comes from the Σα + Σcts − Σ r·ε' identity, so without a visible ε' it is
+    // one constant per document
+    sm.ac[2] = digamma_fast_d(asum + ctot);
+  }
+
+  if (!nonempty) {
+    if (w < npsi) {
+      if (d.town) {
+        if (a.gamma) a.gamma[d.mem * k + tt] = 0.0;
+        if (STATS) a.elogth[d.slot * k + tt] = 0.0;
+      }
+      if (STATS && d.tval) a.eth[d.slot * kp + tt] = 0.0;
+    }
+    if (threadIdx.x == 0) {
+      if (a.iters) a.iters[d.mem] = 0;
+      if (a.nonempty) a.nonempty[d.mem] = 0;
+      if (BOUND) a.bound[d.mem] = 0.0;
+    }
+    return false;
+  }
+  // eθ' = exp(ψ(γ) − ψ(Σγ) − ψc_t): Spark's exp(E[log θ]) times expElogβ's per-topic factor
+  {
+    const double cs0 = digamma_fast_d(gsum0);
+    if (w < npsi && d.town) sm.eth[d.ttl][d.ttp] = exp_digamma_minus_s(g0, cs0 + pc);
+    if (threadIdx.x == 0) sm.cs = cs0;
+  }
+  return true;  // (the block loads' barrier publishes eθ)
+}
+
+// the document block (R row sets) and the fixed point; returns the iteration count, the worker's φ
+// (without ε') in qdt; the final r sits in sm.rrow
+template <class S, int R>
+__device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S>& sm, const RDoc& d, double& qdt) {
   constexpr int KL = S::KL, KLP = S::KLP;
   constexpr int RG = R < S::RREG ? R : S::RREG;  // row sets in VGPRs; [RG, R) in sm.ovf
   static_assert(R >= 1 && R <= S::RMAX && R - RG <= S::NOVF, "row sets");
   STAMP_DECL
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int tl = lane & 7, rl = lane >> 3;
-  const int k = a.k, kp = a.kp;
-  // ψ-lane topic map: k > 64 two ψ waves of `half` topics (t = (w & 1)·half + lane), else one
-  const int npsi = kp > 64 ? 2 : 1;
-  const int half = npsi == 2 ? (kp + 1) / 2 : kp;
-  const int pw = npsi == 2 ? (w & 1) : 0;
-  const int tt = pw * half + lane;
-  const bool tval = lane < half && tt < kp;  // γ / eθ slot (the fp64 pad column included)
-  const bool town = lane < half && tt < k;   // a real topic
-  const int ttl = tt / KL, ttp = tt - ttl * KL;
-  const double alp = town ? a.alpha[tt] : 0.0;
-  const double pc = town ? a.psic[tt] : 0.0;  // ψ(Σ_v λ_vt): expElogβ's per-topic factor, carried by eθ
-
-  // ---- worker lane: wave row q = lane (set q >> 3, row lane q & 7) → document row qn
-  const int qn = 32 * (lane >> 3) + 8 * w + (lane & 7);
-  const bool wv = lane < 8 * R && qn < nnz;
-  const int64_t qe = wv ? s0 + qn : 0;
-  const int qid = wv ? a.indices[qe] : 0;
-  const double qc = wv ? a.values[qe] : 0.0;
-  const double qls = a.logscale[qid];
-  // ε'_q = 1e-100·e^{-m_v} held as 2^53·ε' (the test 2^53·ε' ≥ φ is then direct), capped at 1e300
-  // where e^{-m_v} overflows (Spark's unscaled row is 0 there; r ≈ cts·1e-284 reproduces that).
-  // Padding rows hold −2^53 (φ = −1, r = −0, never live).
-  const double qe2 = wv ? fmin(0x1p53 * exp(kLogEps - qls), 1e300) : -0x1p53;
+  const int lane = d.lane, w = d.w, tl = d.tl, rl = d.rl;
+  const int k = a.k, kp = a.kp, nnz = d.nnz, npsi = d.npsi, pw = d.pw, tt = d.tt, ttl = d.ttl, ttp = d.ttp;
+  const bool town = d.town;
+  const int qid = d.qid;
+  const double qc = d.qc, qe2 = d.qe2;
 
   // ---- B rows, coalesced: per row set the wave copies its eight rows (kp doubles each) with
   // 16-byte loads, stages them in LDS and every lane picks up its (row lane, topic lane) part
@@ -256,65 +356,16 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
     }
   }
 
-  // ---- γ₀ / α partials (the first npsi waves hold the topics), Σcts, eθ pads
-  double g0 = 0.0;
-  if (w < npsi) {
-    if (town) {
-      if (a.gamma0) {
-        g0 = a.gamma0[mem * k + tt];
-      } else {
-        const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, mem) : (uint64_t)(a.doc_id_base + row);
-        g0 = gamma_sample(doc_stream(a.seed, key), tt, a.gamma_shape);
-      }
-    }
-    if (tval) sm.gam[tt] = g0;
-  }
-  for (int i = threadIdx.x; i < 8 * KLP; i += 64 * kW) (&sm.eth[0][0])[i] = 0.0;
-  {
-    const double gs = wave_sum_d(g0), as = wave_sum_d(alp), cts = wave_sum_d(qc);
-    if (lane == 0) {
-      sm.part[w][0] = w < npsi ? gs : 0.0;
-      sm.part[w][1] = w < npsi ? as : 0.0;
-      sm.part[w][2] = cts;
-    }
-  }
-  const bool nonempty = __syncthreads_or(wv && qc != 0.0) != 0;  // (also publishes γ₀ and the partials)
-  const double gsum0 = (sm.part[0][0] + sm.part[1][0]) + (sm.part[2][0] + sm.part[3][0]);
-  const double asum = (sm.part[0][1] + sm.part[1][1]) + (sm.part[2][1] + sm.part[3][1]);
-  const double ctot = (sm.part[0][2] + sm.part[1][2]) + (sm.part[2][2] + sm.part[3][2]);
-
-  if (!nonempty) {
-    if (w < npsi) {
-      if (town) {
-        if (a.gamma) a.gamma[mem * k + tt] = 0.0;
-        if (STATS) a.elogth[slot * k + tt] = 0.0;
-      }
-      if (STATS && tval) a.eth[slot * kp + tt] = 0.0;
-    }
-    if (threadIdx.x == 0) {
-      if (a.iters) a.iters[mem] = 0;
-      if (a.nonempty) a.nonempty[mem] = 0;
-      if (BOUND) a.bound[mem] = 0.0;
-    }
-    return;
-  }
-  // eθ' = exp(ψ(γ) − ψ(Σγ) − ψc_t): Spark's exp(E[log θ]) times expElogβ's per-topic factor; inside the loop ψ(Σγ') comes from the
-  // Σα + Σcts − Σ r·ε' identity, so without a visible ε' it is one constant per document
-  const double cs_flat = digamma_fast_d(asum + ctot);
-  {
-    const double cs0 = digamma_fast_d(gsum0);
-    if (w < npsi && town) sm.eth[ttl][ttp] = exp_digamma_minus_s(g0, cs0 + pc);
-    if (threadIdx.x == 0) sm.cs = cs0;
-  }
-  __syncthreads();
+  __syncthreads();  // the staging area is the loop's partial arrays; (also publishes the first eθ)
 
   double* const pa = &sm.u.l.pa[w][0][0];
   double* const sb = &sm.u.l.sb[0][0];
   double rr[R];
-  double qdt = 0.0, qr = 0.0;  // worker: φ without ε', r of its row (final values are the outputs)
+  double qr = 0.0;  // worker: r of its row (φ without ε' in qdt)
+  qdt = 0.0;
   double dsum = 0.0;
   int it = 0;
-  STAMP(0);  // loads, γ₀, first eθ, two barriers
+  STAMP(0);  // block loads and their barrier
   while (true) {
     // Phase A: φ partials over the lane's KL topics; worker lane q (one per wave row) adds the eight
     // topic lanes' partials in a fixed order, forms r_q = cts/φ once and publishes it (wave-local LDS)
@@ -384,6 +435,7 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
 #pragma unroll
         for (int h = 0; h < 16; ++h) xs[h] = sp[h];
         const double g = sm.gam[tt], eo = sm.eth[ttl][ttp];
+        const double2 ap = *reinterpret_cast<const double2*>(&sm.apc[tt][0]);  // α_t, ψc_t
         const double2 e01 = *reinterpret_cast<const double2*>(&sm.esum[0]);
         const double2 e23 = *reinterpret_cast<const double2*>(&sm.esum[2]);
         double c4[4];
@@ -394,11 +446,11 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
         }
         const double s = (c4[0] + c4[1]) + (c4[2] + c4[3]);
         const double et = (e01.x + e01.y) + (e23.x + e23.y);
-        const double csn = et != 0.0 ? digamma_fast_d(asum + ctot - et) : cs_flat;
-        const double gn = fma(eo, s, alp);  // γ ← eθ ⊙ s + α
+        const double csn = et != 0.0 ? digamma_fast_d(sm.ac[0] + sm.ac[1] - et) : sm.ac[2];
+        const double gn = fma(eo, s, ap.x);  // γ ← eθ ⊙ s + α
         dg = fabs(gn - g);
         sm.gam[tt] = gn;
-        sm.eth[ttl][ttp] = exp_digamma_minus_s(gn, csn + pc);
+        sm.eth[ttl][ttp] = exp_digamma_minus_s(gn, csn + ap.y);
         if (tt == 0) sm.cs = csn;
       }
       const double d = wave_sum_d(dg);
@@ -412,7 +464,19 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
     ++it;
   }
 #undef BV
+  STAMP_FLUSH
+  return it;
+}
 
+// outputs: γ, E[log θ], eθ, the entries' r / keys / vals, iteration count, the bound
+template <class S, bool STATS, bool BOUND>
+__device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>& sm, const RDoc& d, int it, double qdt) {
+  const int lane = d.lane, w = d.w;
+  const int k = a.k, kp = a.kp, nnz = d.nnz, npsi = d.npsi, tt = d.tt, ttl = d.ttl, ttp = d.ttp;
+  const bool town = d.town, tval = d.tval, wv = d.wv;
+  const int64_t slot = d.slot, mem = d.mem, e0 = d.e0;
+  const int qid = d.qid;
+  const double qc = d.qc, qls = d.qls;
   // ---- outputs.  Exact Σγ of the final γ (ψ(Σγ) of E[log θ] and the bound)
   const double gfin = (w < npsi && town) ? sm.gam[tt] : 0.0;
   {
@@ -431,6 +495,7 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
       sm.part[w][1] = bt;
       sm.part[w][2] = bc;
     }
+    if (wv) sm.rid[w][lane] = qid;  // (rrow holds the final r since the last worker phase)
   }
   __syncthreads();
   const double gsum = (sm.part[0][0] + sm.part[1][0]) + (sm.part[2][0] + sm.part[3][0]);
@@ -441,23 +506,28 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
       const double el = digamma_t<double>(gfin) - psisum;
       if (a.gamma) a.gamma[mem * k + tt] = gfin;
       if (STATS) a.elogth[slot * k + tt] = el;
-      if (BOUND) topic = (alp - gfin) * el + (lgamma(gfin) - lgamma(alp));
+      if (BOUND) {
+        const double alp = sm.apc[tt][0];
+        topic = (alp - gfin) * el + (lgamma(gfin) - lgamma(alp));
+      }
     }
     if (STATS && tval) a.eth[slot * kp + tt] = sm.eth[ttl][ttp];  // the eθ the final φ used
   }
-  if (wv) {
-    a.r[e0 + qn] = qr;
+  // entry outputs in row order, consecutive threads on consecutive entries (whole cache lines: a
+  // wave's own eight rows per set would be 32–64-byte pieces of lines another wave also writes)
+  for (int n = threadIdx.x; n < nnz; n += 64 * kW) {
+    const int ws = (n >> 3) & 3, q = 8 * (n >> 5) + (n & 7);  // row n = 32·set + 8·wave + row lane
+    const double rv = sm.rrow[ws][q];
+    a.r[e0 + n] = rv;
     if (STATS) {
-      a.keys[e0 + qn] = (uint32_t)qid;
-      a.vals[e0 + qn] = entry_val<double>(slot, e0 + qn, qr);
+      a.keys[e0 + n] = (uint32_t)sm.rid[ws][q];
+      a.vals[e0 + n] = entry_val<double>(slot, e0 + n, rv);
     }
   }
   if (threadIdx.x == 0) {
     if (a.iters) a.iters[mem] = it;
     if (a.nonempty) a.nonempty[mem] = 1;
   }
-  STAMP(7);
-  STAMP_FLUSH
   if (BOUND) {
     topic = wave_sum_d(topic);
     if (lane == 0) sm.part[w][3] = topic;
@@ -471,7 +541,7 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
         tp += sm.part[v][3];
       }
       const double elog_max = sm.cs - psisum;  // log of the scale eθ carried (≈ 0)
-      a.bound[mem] = tok + ctk * elog_max + tp + (lgamma(asum) - lgamma(gsum));
+      a.bound[mem] = tok + ctk * elog_max + tp + (lgamma(sm.ac[0]) - lgamma(gsum));
     }
   }
 }
@@ -482,28 +552,31 @@ template <class S, bool STATS, bool BOUND, bool LONG>
 __global__ __launch_bounds__(64 * kW, LONG ? R64_LONG_OCC : 2) void k_estep_rows64(EStepArgs<double> a) {
   __shared__ RLds<S> sm;
   if ((int64_t)blockIdx.x >= a.n) return;
-  const int64_t slot = a.slot0 + blockIdx.x;
-  const int64_t row = a.batch ? (int64_t)a.batch[slot] : slot;
-  const int64_t mem = a.orig ? (int64_t)a.orig[slot] : slot;
-  const int64_t s0 = a.indptr[row];
-  const int nnz = (int)(a.indptr[row + 1] - s0);
-  const int rsets = (nnz + 31) >> 5;
-  if (LONG ? rsets <= kOnChipSets : rsets > kOnChipSets) return;  // the other kernel's document
-  const int64_t e0 = a.bptr ? a.bptr[slot] : s0;
+  RDoc d;
+  d.slot = a.slot0 + blockIdx.x;
+  d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
+  d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
+  d.s0 = a.indptr[d.row];
+  d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
+  d.rsets = (d.nnz + 31) >> 5;
+  if (LONG ? d.rsets <= kOnChipSets : d.rsets > kOnChipSets) return;  // the other kernel's document
+  d.e0 = a.bptr ? a.bptr[d.slot] : d.s0;
+  if (!rows64_open<S, STATS, BOUND>(a, sm, d)) return;
+  double qdt = 0.0;
+  int it;
   if constexpr (LONG) {
-    if (rsets == 7) rows64_doc<S, 7, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz);
-    else rows64_doc<S, 8, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz);
+    it = d.rsets == 7 ? rows64_iterate<S, 7>(a, sm, d, qdt) : rows64_iterate<S, 8>(a, sm, d, qdt);
   } else {
-    switch (rsets) {
-      case 0:
-      case 1: rows64_doc<S, 1, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz); break;
-      case 2: rows64_doc<S, 2, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz); break;
-      case 3: rows64_doc<S, 3, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz); break;
-      case 4: rows64_doc<S, 4, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz); break;
-      case 5: rows64_doc<S, 5, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz); break;
-      default: rows64_doc<S, 6, STATS, BOUND>(a, sm, slot, row, mem, s0, e0, nnz); break;
+    switch (d.rsets) {
+      case 1: it = rows64_iterate<S, 1>(a, sm, d, qdt); break;
+      case 2: it = rows64_iterate<S, 2>(a, sm, d, qdt); break;
+      case 3: it = rows64_iterate<S, 3>(a, sm, d, qdt); break;
+      case 4: it = rows64_iterate<S, 4>(a, sm, d, qdt); break;
+      case 5: it = rows64_iterate<S, 5>(a, sm, d, qdt); break;
+      default: it = rows64_iterate<S, 6>(a, sm, d, qdt); break;
     }
   }
+  rows64_close<S, STATS, BOUND>(a, sm, d, it, qdt);
 }
 
 template <class S, bool LONG>

@@ -37,6 +37,8 @@ fi
 if [ -n "$PROF" ]; then  # rocprofv3 passes of the bench (PROF_PASSES, BENCH_ARGS, PROF_OUT as tools/gpu_prof.sh)
   step prof 900 bash tools/gpu_prof.sh
 fi
+if [ -n "$ICACHE" ]; then step icache 700 bash tools/gpu_icache.sh; fi
+if [ -n "$COUNTERS" ]; then step counters 700 bash tools/gpu_counters.sh; fi
 if [ -n "$EXIT_PROBE" ]; then  # last: the team-kernel exit under rocprofv3 (EXIT_ARGS="--close": explicit teardown)
   rm -rf gpurun_out/exitp
   step exitp 180 env TMPDIR=/tmp rocprofv3 --kernel-trace --stats -d gpurun_out/exitp -o exitp --output-format csv -- python3 tools/exit_probe.py gpurun_out/exitp_maps.txt $EXIT_ARGS
