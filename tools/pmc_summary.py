@@ -12,7 +12,7 @@ FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB from the L2's fabr
 counters, measured in SEPARATE --pmc passes (they do not fit one pass on gfx950).  On gfx950
 FETCH_SIZE reports half the bytes of wide (16 B/lane) reads, so it is doubled
 (MI355X_MICROARCH.md, HBM section).  Infinity-Cache hits are counted as fabric traffic.
-One minibatch = one k_lambda_update<UPDATE=true> dispatch.
+One minibatch = one UPDATE=true dispatch of the fused M-step pass (k_lambda_eeb / k_lambda_eeb_wide).
 """
 import argparse
 import collections
@@ -78,8 +78,8 @@ def main():
         for kn, cs in load_counters(sq_path).items():
             sq[kn] = {c: sum(v) / len(v) for c, v in cs.items()}
 
-    steps = sum(len(v.get("FETCH_SIZE", [])) for kn, v in fetch.items() if "k_lambda_update<float, true>" in kn
-                or "k_lambda_update<double, true>" in kn)
+    steps = sum(len(v.get("FETCH_SIZE", [])) for kn, v in fetch.items()
+                if kn.startswith("k_lambda_eeb") and kn.endswith(", true>"))
     kernels = {}
     phase_total = 0.0
     for kn in sorted(set(fetch) | set(write)):
