@@ -118,3 +118,42 @@ def test_full_size_minibatch_properties(ctx, oracle, dtype):
     tot = float(np.sum(stat * eeb))
     assert abs(tot - tok.sum()) / tok.sum() < (1e-4 if dtype == "f32" else 1e-10), (tot, tok.sum())
     assert iters.min() >= 1
+
+
+@pytest.mark.parametrize("members", [2, 8])
+def test_config3_sharded_decomposition_full_size(ctx, members):
+    """BASELINE configs[2] (the configs[1] corpus sharded over 2 / 8 GPUs) at full size, on the one GPU
+    of this box: a device group repeating device 0 runs every member's shard of documents, the stat
+    reduce-scatter, the vocabulary-sliced fused M-step and the all-gathers — the multi-GPU call
+    sequence — and must train the same model as one handle on the unsharded corpus (same injected
+    minibatches and γ₀; fp64: only the summation order of sstats across shards differs)."""
+    import stc
+
+    D, L, V, k = 1_000_000, 200, 1 << 18, 100
+    corpus = _full_corpus(D, L, V, k)
+    rng = np.random.default_rng(77 + members)
+    lam = _tiled_topics(rng, V, k)
+    kw = dict(mini_batch_fraction=0.05, optimize_doc_concentration=True)
+    h = stc.LdaHandle(ctx, k, V, dtype="f64", **kw)
+    dc = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F64)
+    h.set_corpus(dc, D)
+    h.set_topics(lam)
+    with stc.LdaGroup([0] * members, k, V, dtype="f64", **kw) as g:
+        g.set_corpus(corpus)
+        g.set_topics(lam)
+        for it in range(2):
+            ids = rng.integers(0, D, size=50_000)  # with duplicates, as a Poisson draw has them
+            g0 = rng.gamma(100.0, 0.01, size=(ids.size, k))
+            sh = h.step(ids, g0)
+            sg = g.step(ids, g0)
+            assert sg["batch_docs"] == sh["batch_docs"] and sg["nonempty_docs"] == sh["nonempty_docs"]
+            # step 1 starts from the same λ: every document's E-step is identical; step 2 starts from λ
+            # that differs in the last bits, where documents on the stop rule's boundary may take one
+            # iteration more or fewer
+            assert abs(sg["inner_iters"] - sh["inner_iters"]) <= (0 if it == 0 else 1e-4 * sh["inner_iters"])
+        lg, lh = g.topics(), h.topics()
+        rel = np.abs(lg - lh) / lh
+        assert np.median(rel) < 1e-13 and rel.max() < 1e-6, (np.median(rel), rel.max())
+        np.testing.assert_allclose(g.alpha(), h.alpha(), rtol=1e-9)
+    dc.free()
+    h.close()
