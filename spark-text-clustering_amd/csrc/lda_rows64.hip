@@ -192,6 +192,9 @@ struct RDoc {
   bool wv;                           // worker lane with a document row
   int qid;                           // worker: term id, count, m_v, 2^53·ε'
   double qc, qls, qe2;
+#ifdef STC_STAMP
+  unsigned long long st0;            // kernel entry (diagnostic build: the per-document prologue)
+#endif
 };
 
 // worker lanes, γ₀, α / ψc, Σγ₀ / Σα / Σcts, the first eθ; false (outputs written) for a document
@@ -300,6 +303,9 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
   constexpr int RG = R < S::RREG ? R : S::RREG;  // row sets in VGPRs; [RG, R) in sm.ovf
   static_assert(R >= 1 && R <= S::RMAX && R - RG <= S::NOVF, "row sets");
   STAMP_DECL
+#ifdef STC_STAMP
+  st_acc[10] += st_last - d.st0;
+#endif
   const int lane = d.lane, w = d.w, tl = d.tl, rl = d.rl;
   const int k = a.k, kp = a.kp, nnz = d.nnz, npsi = d.npsi, pw = d.pw, tt = d.tt, ttl = d.ttl, ttp = d.ttp;
   const bool town = d.town;
@@ -477,6 +483,9 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
   const int64_t slot = d.slot, mem = d.mem, e0 = d.e0;
   const int qid = d.qid;
   const double qc = d.qc, qls = d.qls;
+#ifdef STC_STAMP
+  const unsigned long long st_close = stamp_now();
+#endif
   // ---- outputs.  Exact Σγ of the final γ (ψ(Σγ) of E[log θ] and the bound)
   const double gfin = (w < npsi && town) ? sm.gam[tt] : 0.0;
   {
@@ -544,6 +553,9 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
       a.bound[mem] = tok + ctk * elog_max + tp + (lgamma(sm.ac[0]) - lgamma(gsum));
     }
   }
+#ifdef STC_STAMP
+  if (lane == 0) atomicAdd(&g_stamps[7], stamp_now() - st_close);
+#endif
 }
 
 // LONG = false: documents with ≤ kOnChipSets row sets; LONG = true: 7–8 sets.  Both kernels run over
@@ -553,6 +565,9 @@ __global__ __launch_bounds__(64 * kW, LONG ? R64_LONG_OCC : 2) void k_estep_rows
   __shared__ RLds<S> sm;
   if ((int64_t)blockIdx.x >= a.n) return;
   RDoc d;
+#ifdef STC_STAMP
+  d.st0 = stamp_now();
+#endif
   d.slot = a.slot0 + blockIdx.x;
   d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
   d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;

@@ -21,7 +21,8 @@ sys.path.insert(0, os.path.join(ROOT, "spark-text-clustering_amd"))
 
 PHASES = ["init: loads, gamma0, first eth", "A: eth reads + phi FMAs + all-reduce", "r, eps ballot, sum|dgamma|",
           "B: s FMAs + stores", "barrier 1", "psi phase (psi waves)", "barrier 2 (psi waves)", "outputs",
-          "psi phase (other waves)", "barrier 2 (other waves)"]
+          "psi phase (other waves)", "barrier 2 (other waves)", "prologue: worker loads, gamma0, first eth"]
+PER_DOC = (0, 7, 10)  # once per document: block loads, outputs, prologue
 
 
 def main():
@@ -75,6 +76,8 @@ def main():
     for i, name in enumerate(PHASES):
         out["cycles_per_wave_iter"][name] = round(cyc[i] / (W * max(1, iters)), 1)
     out["cycles_per_wave_iter"]["total"] = round(cyc.sum() / (W * max(1, iters)), 1)
+    out["cycles_per_wave_doc"] = {PHASES[i]: round(cyc[i] / (W * max(1, docs)), 1) for i in PER_DOC}
+    out["cycles_per_wave_doc"]["loop"] = round(sum(cyc[i] for i in range(n) if i not in PER_DOC) / (W * max(1, docs)), 1)
     print(json.dumps(out, indent=1))
 
 
