@@ -49,6 +49,9 @@ struct EStepArgs {
   const double* logscale = nullptr;    // V     m_v (BOUND)
   const double* alpha = nullptr;       // k
   const T* gamma0 = nullptr;           // n×k or nullptr (counter RNG)
+  // fp64 rows kernel: scratch for the list of this launch's 7–8-row-set documents (capacity n slots +
+  // one count word), filled on the device before the long-document launch walks it
+  int32_t* long_list = nullptr;
   uint64_t seed = 0;
   int64_t iteration = 0;
   int rank = 0;

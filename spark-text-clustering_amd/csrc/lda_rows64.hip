@@ -186,6 +186,7 @@ struct RLds {
 struct RDoc {
   int64_t slot, row, mem, s0, e0;
   int nnz, rsets;
+  int tid;                           // threadIdx.x (laundered per document by the resident long kernel)
   int lane, w, tl, rl;
   int npsi, half, pw, tt, ttl, ttp;  // ψ-lane topic map
   bool tval, town;                   // γ / eθ slot (the fp64 pad column included); a real topic
@@ -203,7 +204,7 @@ template <class S, bool STATS, bool BOUND>
 __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>& sm, RDoc& d) {
   constexpr int KL = S::KL, KLP = S::KLP;
   const int k = a.k, kp = a.kp;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = d.tid & 63, w = d.tid >> 6;
   d.lane = lane;
   d.w = w;
   d.tl = lane & 7;
@@ -245,12 +246,16 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
         g0 = a.gamma0[d.mem * k + tt];
       } else {
         const uint64_t key = a.key_mode == 0 ? train_doc_key(a.iteration, a.rank, d.mem) : (uint64_t)(a.doc_id_base + d.row);
+#ifdef R64_DIAG_NORNG  // diagnostic build only (tools/iter_sweep.py): the prologue without γ₀'s RNG
+        g0 = 1.0 + 1e-3 * (double)(key & 1023) + 1e-4 * tt;
+#else
         g0 = gamma_sample(doc_stream(a.seed, key), tt, a.gamma_shape);
+#endif
       }
     }
     if (d.tval) sm.gam[tt] = g0;
   }
-  for (int i = threadIdx.x; i < 8 * KLP; i += 64 * kW) (&sm.eth[0][0])[i] = 0.0;
+  for (int i = d.tid; i < 8 * KLP; i += 64 * kW) (&sm.eth[0][0])[i] = 0.0;
   {
     const double gs = wave_sum_d(g0), as = wave_sum_d(alp), cts = wave_sum_d(d.qc);
     if (lane == 0) {
@@ -261,7 +266,7 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
   }
   const bool nonempty = __syncthreads_or(d.wv && d.qc != 0.0) != 0;  // (also publishes γ₀ and the partials)
   const double gsum0 = (sm.part[0][0] + sm.part[1][0]) + (sm.part[2][0] + sm.part[3][0]);
-  if (threadIdx.x == 0) {  // read back by the ψ phase and the bound (published by the next barrier)
+  if (d.tid == 0) {  // read back by the ψ phase and the bound (published by the next barrier)
     const double asum = (sm.part[0][1] + sm.part[1][1]) + (sm.part[2][1] + sm.part[3][1]);
     const double ctot = (sm.part[0][2] + sm.part[1][2]) + (sm.part[2][2] + sm.part[3][2]);
     sm.ac[0] = asum;
@@ -279,7 +284,7 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
       }
       if (STATS && d.tval) a.eth[d.slot * kp + tt] = 0.0;
     }
-    if (threadIdx.x == 0) {
+    if (d.tid == 0) {
       if (a.iters) a.iters[d.mem] = 0;
       if (a.nonempty) a.nonempty[d.mem] = 0;
       if (BOUND) a.bound[d.mem] = 0.0;
@@ -290,7 +295,7 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
   {
     const double cs0 = digamma_fast_d(gsum0);
     if (w < npsi && d.town) sm.eth[d.ttl][d.ttp] = exp_digamma_minus_s(g0, cs0 + pc);
-    if (threadIdx.x == 0) sm.cs = cs0;
+    if (d.tid == 0) sm.cs = cs0;
   }
   return true;  // (the block loads' barrier publishes eθ)
 }
@@ -335,7 +340,11 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
           const int srow = c / C2, q = c - srow * C2;
           const int id = __builtin_amdgcn_ds_bpermute((8 * j + (srow & 7)) << 2, qid);  // its worker lane
           const bool keep = c < 8 * C2 && 32 * j + 8 * w + srow < nnz;
+#ifdef R64_DIAG_NOGATHER  // diagnostic build only: the load phase without the B gather
+          const double2 x = make_double2(1e-3 * (id & 7), 1e-3 * (q & 7));
+#else
           const double2 x = *reinterpret_cast<const double2*>(a.Bp + (int64_t)(keep ? id : 0) * kp + 2 * (keep ? q : 0));
+#endif
           pc[jj][i] = keep ? x : make_double2(0.0, 0.0);
         }
       }
@@ -524,7 +533,7 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
   }
   // entry outputs in row order, consecutive threads on consecutive entries (whole cache lines: a
   // wave's own eight rows per set would be 32–64-byte pieces of lines another wave also writes)
-  for (int n = threadIdx.x; n < nnz; n += 64 * kW) {
+  for (int n = d.tid; n < nnz; n += 64 * kW) {
     const int ws = (n >> 3) & 3, q = 8 * (n >> 5) + (n & 7);  // row n = 32·set + 8·wave + row lane
     const double rv = sm.rrow[ws][q];
     a.r[e0 + n] = rv;
@@ -533,7 +542,7 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
       a.vals[e0 + n] = entry_val<double>(slot, e0 + n, rv);
     }
   }
-  if (threadIdx.x == 0) {
+  if (d.tid == 0) {
     if (a.iters) a.iters[mem] = it;
     if (a.nonempty) a.nonempty[mem] = 1;
   }
@@ -541,7 +550,7 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
     topic = wave_sum_d(topic);
     if (lane == 0) sm.part[w][3] = topic;
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (d.tid == 0) {
       double tok = 0.0, ctk = 0.0, tp = 0.0;
 #pragma unroll
       for (int v = 0; v < kW; ++v) {
@@ -558,23 +567,10 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
 #endif
 }
 
-// LONG = false: documents with ≤ kOnChipSets row sets; LONG = true: 7–8 sets.  Both kernels run over
-// the same slots and each skips the other's documents.
+// one document: slot → row / member / extent, then open → iterate<R> → close
 template <class S, bool STATS, bool BOUND, bool LONG>
-__global__ __launch_bounds__(64 * kW, LONG ? R64_LONG_OCC : 2) void k_estep_rows64(EStepArgs<double> a) {
-  __shared__ RLds<S> sm;
-  if ((int64_t)blockIdx.x >= a.n) return;
-  RDoc d;
-#ifdef STC_STAMP
-  d.st0 = stamp_now();
-#endif
-  d.slot = a.slot0 + blockIdx.x;
-  d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
+__device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& sm, RDoc& d) {
   d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
-  d.s0 = a.indptr[d.row];
-  d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
-  d.rsets = (d.nnz + 31) >> 5;
-  if (LONG ? d.rsets <= kOnChipSets : d.rsets > kOnChipSets) return;  // the other kernel's document
   d.e0 = a.bptr ? a.bptr[d.slot] : d.s0;
   if (!rows64_open<S, STATS, BOUND>(a, sm, d)) return;
   double qdt = 0.0;
@@ -594,20 +590,91 @@ __global__ __launch_bounds__(64 * kW, LONG ? R64_LONG_OCC : 2) void k_estep_rows
   rows64_close<S, STATS, BOUND>(a, sm, d, it, qdt);
 }
 
-template <class S, bool LONG>
-void launch_r1(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound) {
+// the documents with ≤ kOnChipSets row sets: one workgroup per slot (the long documents exit at once)
+template <class S, bool STATS, bool BOUND>
+__global__ __launch_bounds__(64 * kW, 2) void k_estep_rows64(EStepArgs<double> a) {
+  __shared__ RLds<S> sm;
+  if ((int64_t)blockIdx.x >= a.n) return;
+  RDoc d;
+#ifdef STC_STAMP
+  d.st0 = stamp_now();
+#endif
+  d.tid = threadIdx.x;
+  d.slot = a.slot0 + blockIdx.x;
+  d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
+  d.s0 = a.indptr[d.row];
+  d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
+  d.rsets = (d.nnz + 31) >> 5;
+  if (d.rsets > kOnChipSets) return;  // the long-document kernel's
+  rows64_doc<S, STATS, BOUND, false>(a, sm, d);
+}
+
+// the launch's 7–8-set documents into a.long_list: word 0 the count, then their slot offsets (in any
+// order: every document's outputs are its own)
+__global__ void k_rows64_long_list(EStepArgs<double> a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const int64_t slot = a.slot0 + i;
+  const int64_t row = a.batch ? (int64_t)a.batch[slot] : slot;
+  const int nnz = (int)(a.indptr[row + 1] - a.indptr[row]);
+  if (nnz > 32 * kOnChipSets) a.long_list[1 + atomicAdd(&a.long_list[0], 1)] = (int32_t)i;
+}
+
+// the 7–8-set documents at one workgroup per CU, a resident grid walking the list (a grid over every
+// slot would dispatch ~n workgroups at that occupancy only to have most exit after two dependent loads)
+template <class S, bool STATS, bool BOUND>
+__global__ __launch_bounds__(64 * kW, R64_LONG_OCC) void k_estep_rows64_long(EStepArgs<double> a) {
+  __shared__ RLds<S> sm;
+  const int cnt = a.long_list[0];
+  for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
+    RDoc d;
+#ifdef STC_STAMP
+    d.st0 = stamp_now();
+#endif
+    // every per-lane value derives from tid: laundered per document, so the compiler cannot hoist the
+    // lane maps and the α / ψc loads out of the document loop and hold them across the fixed point
+    d.tid = threadIdx.x;
+    asm volatile("" : "+v"(d.tid));
+    d.slot = a.slot0 + a.long_list[1 + j];
+    d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
+    d.s0 = a.indptr[d.row];
+    d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
+    d.rsets = (d.nnz + 31) >> 5;
+    rows64_doc<S, STATS, BOUND, true>(a, sm, d);
+    __syncthreads();  // LDS is the next document's
+  }
+}
+
+template <class S>
+void launch_common(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound) {
   const dim3 grid((unsigned)a.n);
   const int threads = 64 * kW;
-  if (stats) k_estep_rows64<S, true, false, LONG><<<grid, threads, 0, s>>>(a);
-  else if (bound) k_estep_rows64<S, false, true, LONG><<<grid, threads, 0, s>>>(a);
-  else k_estep_rows64<S, false, false, LONG><<<grid, threads, 0, s>>>(a);
+  if (stats) k_estep_rows64<S, true, false><<<grid, threads, 0, s>>>(a);
+  else if (bound) k_estep_rows64<S, false, true><<<grid, threads, 0, s>>>(a);
+  else k_estep_rows64<S, false, false><<<grid, threads, 0, s>>>(a);
+  KERNEL_CHECK();
+}
+template <class S>
+void launch_long(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound) {
+  if (!a.long_list) throw Error(STC_ERR_STATE, "fp64 rows E-step: no long-document list buffer");
+  HIP_CHECK(hipMemsetAsync(a.long_list, 0, sizeof(int32_t), s));
+  k_rows64_long_list<<<dim3((unsigned)((a.n + 255) / 256)), 256, 0, s>>>(a);
+  KERNEL_CHECK();
+  int dev = 0, cus = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(a.n, (int64_t)cus * R64_LONG_OCC)));
+  const int threads = 64 * kW;
+  if (stats) k_estep_rows64_long<S, true, false><<<grid, threads, 0, s>>>(a);
+  else if (bound) k_estep_rows64_long<S, false, true><<<grid, threads, 0, s>>>(a);
+  else k_estep_rows64_long<S, false, false><<<grid, threads, 0, s>>>(a);
   KERNEL_CHECK();
 }
 // the 7–8-set documents first (`long_docs` = false when the caller knows there are none), then the rest
 template <int KL>
 void launch_r(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound, bool long_docs) {
-  if (long_docs) launch_r1<RLong<KL>, true>(s, a, stats, bound);
-  launch_r1<RCommon<KL>, false>(s, a, stats, bound);
+  if (long_docs) launch_long<RLong<KL>>(s, a, stats, bound);
+  launch_common<RCommon<KL>>(s, a, stats, bound);
 }
 
 }  // namespace
