@@ -49,9 +49,6 @@ struct EStepArgs {
   const double* logscale = nullptr;    // V     m_v (BOUND)
   const double* alpha = nullptr;       // k
   const T* gamma0 = nullptr;           // n×k or nullptr (counter RNG)
-  // fp64 rows kernel: scratch for the list of this launch's 7–8-row-set documents (capacity n slots +
-  // one count word), filled on the device before the long-document launch walks it
-  int32_t* long_list = nullptr;
   uint64_t seed = 0;
   int64_t iteration = 0;
   int rank = 0;
@@ -72,6 +69,10 @@ struct EStepArgs {
   int32_t* iters = nullptr;            // n (optional)
   int32_t* nonempty = nullptr;         // n (optional)
   double* bound = nullptr;             // n (BOUND)
+  // fp64 rows kernel: scratch for the list of this launch's 7–8-row-set documents (capacity n slots +
+  // one count word), filled on the device before the long-document launch walks it (last, so the
+  // other kernels' argument layout is unchanged)
+  int32_t* long_list = nullptr;
 };
 
 // the largest double x with fl(x / k) ≤ 1e-3 (host; see EStepArgs::stop_thr)

@@ -186,7 +186,7 @@ struct RLds {
 struct RDoc {
   int64_t slot, row, mem, s0, e0;
   int nnz, rsets;
-  int tid;                           // threadIdx.x (laundered per document by the resident long kernel)
+  int tid;                           // the resident long kernel's threadIdx.x, laundered per document
   int lane, w, tl, rl;
   int npsi, half, pw, tt, ttl, ttp;  // ψ-lane topic map
   bool tval, town;                   // γ / eθ slot (the fp64 pad column included); a real topic
@@ -198,13 +198,18 @@ struct RDoc {
 #endif
 };
 
+// threadIdx.x, or its per-document laundered copy in the resident long-document kernel (RES)
+template <bool RES>
+__device__ __forceinline__ int rows64_tid(const RDoc& d) { return RES ? d.tid : (int)threadIdx.x; }
+
 // worker lanes, γ₀, α / ψc, Σγ₀ / Σα / Σcts, the first eθ; false (outputs written) for a document
 // without a nonzero count
-template <class S, bool STATS, bool BOUND>
+template <class S, bool STATS, bool BOUND, bool RES>
 __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>& sm, RDoc& d) {
+  const int tid = rows64_tid<RES>(d);
   constexpr int KL = S::KL, KLP = S::KLP;
   const int k = a.k, kp = a.kp;
-  const int lane = d.tid & 63, w = d.tid >> 6;
+  const int lane = tid & 63, w = tid >> 6;
   d.lane = lane;
   d.w = w;
   d.tl = lane & 7;
@@ -255,7 +260,7 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
     }
     if (d.tval) sm.gam[tt] = g0;
   }
-  for (int i = d.tid; i < 8 * KLP; i += 64 * kW) (&sm.eth[0][0])[i] = 0.0;
+  for (int i = tid; i < 8 * KLP; i += 64 * kW) (&sm.eth[0][0])[i] = 0.0;
   {
     const double gs = wave_sum_d(g0), as = wave_sum_d(alp), cts = wave_sum_d(d.qc);
     if (lane == 0) {
@@ -266,7 +271,7 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
   }
   const bool nonempty = __syncthreads_or(d.wv && d.qc != 0.0) != 0;  // (also publishes γ₀ and the partials)
   const double gsum0 = (sm.part[0][0] + sm.part[1][0]) + (sm.part[2][0] + sm.part[3][0]);
-  if (d.tid == 0) {  // read back by the ψ phase and the bound (published by the next barrier)
+  if (tid == 0) {  // read back by the ψ phase and the bound (published by the next barrier)
     const double asum = (sm.part[0][1] + sm.part[1][1]) + (sm.part[2][1] + sm.part[3][1]);
     const double ctot = (sm.part[0][2] + sm.part[1][2]) + (sm.part[2][2] + sm.part[3][2]);
     sm.ac[0] = asum;
@@ -284,7 +289,7 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
       }
       if (STATS && d.tval) a.eth[d.slot * kp + tt] = 0.0;
     }
-    if (d.tid == 0) {
+    if (tid == 0) {
       if (a.iters) a.iters[d.mem] = 0;
       if (a.nonempty) a.nonempty[d.mem] = 0;
       if (BOUND) a.bound[d.mem] = 0.0;
@@ -295,7 +300,7 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
   {
     const double cs0 = digamma_fast_d(gsum0);
     if (w < npsi && d.town) sm.eth[d.ttl][d.ttp] = exp_digamma_minus_s(g0, cs0 + pc);
-    if (d.tid == 0) sm.cs = cs0;
+    if (tid == 0) sm.cs = cs0;
   }
   return true;  // (the block loads' barrier publishes eθ)
 }
@@ -484,8 +489,9 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
 }
 
 // outputs: γ, E[log θ], eθ, the entries' r / keys / vals, iteration count, the bound
-template <class S, bool STATS, bool BOUND>
+template <class S, bool STATS, bool BOUND, bool RES>
 __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>& sm, const RDoc& d, int it, double qdt) {
+  const int tid = rows64_tid<RES>(d);
   const int lane = d.lane, w = d.w;
   const int k = a.k, kp = a.kp, nnz = d.nnz, npsi = d.npsi, tt = d.tt, ttl = d.ttl, ttp = d.ttp;
   const bool town = d.town, tval = d.tval, wv = d.wv;
@@ -533,7 +539,7 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
   }
   // entry outputs in row order, consecutive threads on consecutive entries (whole cache lines: a
   // wave's own eight rows per set would be 32–64-byte pieces of lines another wave also writes)
-  for (int n = d.tid; n < nnz; n += 64 * kW) {
+  for (int n = tid; n < nnz; n += 64 * kW) {
     const int ws = (n >> 3) & 3, q = 8 * (n >> 5) + (n & 7);  // row n = 32·set + 8·wave + row lane
     const double rv = sm.rrow[ws][q];
     a.r[e0 + n] = rv;
@@ -542,7 +548,7 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
       a.vals[e0 + n] = entry_val<double>(slot, e0 + n, rv);
     }
   }
-  if (d.tid == 0) {
+  if (tid == 0) {
     if (a.iters) a.iters[mem] = it;
     if (a.nonempty) a.nonempty[mem] = 1;
   }
@@ -550,7 +556,7 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
     topic = wave_sum_d(topic);
     if (lane == 0) sm.part[w][3] = topic;
     __syncthreads();
-    if (d.tid == 0) {
+    if (tid == 0) {
       double tok = 0.0, ctk = 0.0, tp = 0.0;
 #pragma unroll
       for (int v = 0; v < kW; ++v) {
@@ -567,12 +573,11 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
 #endif
 }
 
-// one document: slot → row / member / extent, then open → iterate<R> → close
+// one document (slot, row, member and extent set by the caller): open → iterate<R> → close
 template <class S, bool STATS, bool BOUND, bool LONG>
 __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& sm, RDoc& d) {
-  d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
   d.e0 = a.bptr ? a.bptr[d.slot] : d.s0;
-  if (!rows64_open<S, STATS, BOUND>(a, sm, d)) return;
+  if (!rows64_open<S, STATS, BOUND, LONG>(a, sm, d)) return;
   double qdt = 0.0;
   int it;
   if constexpr (LONG) {
@@ -587,7 +592,7 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
       default: it = rows64_iterate<S, 6>(a, sm, d, qdt); break;
     }
   }
-  rows64_close<S, STATS, BOUND>(a, sm, d, it, qdt);
+  rows64_close<S, STATS, BOUND, LONG>(a, sm, d, it, qdt);
 }
 
 // the documents with ≤ kOnChipSets row sets: one workgroup per slot (the long documents exit at once)
@@ -599,9 +604,9 @@ __global__ __launch_bounds__(64 * kW, 2) void k_estep_rows64(EStepArgs<double> a
 #ifdef STC_STAMP
   d.st0 = stamp_now();
 #endif
-  d.tid = threadIdx.x;
   d.slot = a.slot0 + blockIdx.x;
   d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
+  d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
   d.s0 = a.indptr[d.row];
   d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
   d.rsets = (d.nnz + 31) >> 5;
@@ -637,6 +642,7 @@ __global__ __launch_bounds__(64 * kW, R64_LONG_OCC) void k_estep_rows64_long(ESt
     asm volatile("" : "+v"(d.tid));
     d.slot = a.slot0 + a.long_list[1 + j];
     d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
+    d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
     d.s0 = a.indptr[d.row];
     d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
     d.rsets = (d.nnz + 31) >> 5;
