@@ -66,7 +66,7 @@ struct stc_lda {
   hipEvent_t ev_fill = nullptr, ev_samp = nullptr;
   bool samp_pending = false;
   DevBuf side_scan_tmp;
-  DevBuf long_list;  // fp64 rows kernel: the launch's 7–8-row-set documents (count word + slot offsets)
+  DevBuf long_list;  // rows / grid kernels: the launch's long documents (count word + slot offsets)
   DevBuf o_keys, o_keys2, o_idx, o_idx2, o_batch, o_orig, o_nnz, o_tmp;  // slot ordering (order_slots)
   bool sort_docs = true;  // STC_SORT_DOCS=0 keeps sampling order
   // many-topic kernel: per-entry row order, rarest terms first (lda_wide.hip), for `order_for`
@@ -605,8 +605,14 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
     if (team) {
       // launched (a grid that could not be resident falls through to the one-CU kernel)
     } else if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
-    else if constexpr (std::is_same<T, float>::value) lda::launch_estep_grid(s, w, stats, bound);
-    else {
+    else if constexpr (std::is_same<T, float>::value) {
+      const bool long_docs = m.max_row < 0 || m.max_row > lda::grid_onchip_rows(L.k);
+      if (long_docs) {
+        L.long_list.reserve(4 * (size_t)(n_short + 1));
+        w.long_list = L.long_list.as<int32_t>();
+      }
+      lda::launch_estep_grid(s, w, stats, bound, long_docs);
+    } else {
       const bool long_docs = m.max_row < 0 || m.max_row > lda::rows64_onchip_rows(L.k);
       if (long_docs) {
         L.long_list.reserve(4 * (size_t)(n_short + 1));

@@ -32,6 +32,7 @@ struct GShape {
 using G32 = GShape<1, 16, 8, 2>;   // k <= 32
 using G64 = GShape<2, 16, 8, 2>;   // k <= 64
 using G104 = GShape<2, 26, 6, 2>;  // k <= 104 (k = 100: 4 groups of 26 topics)
+using G104L = GShape<2, 26, 8, 1>; // k <= 104, documents of 193–256 rows (all eight row sets in VGPRs)
 using G128 = GShape<4, 16, 8, 2>;  // k <= 128
 
 template <class S>
@@ -344,25 +345,27 @@ __device__ __forceinline__ bool grid_core(const EStepArgs<float>& a, GLds<S>& sm
   return nonempty;
 }
 
-template <class S, bool STATS, bool BOUND>
-__global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_grid(EStepArgs<float> a) {
+// one document of slot `slot` with thread index `tid` (the resident long-document kernel passes a
+// per-document laundered copy, so nothing lane-dependent is hoisted out of its document loop);
+// SKIPLONG: leave documents past S::RMAX row sets to the long-document kernel
+template <class S, bool STATS, bool BOUND, bool SKIPLONG>
+__device__ __forceinline__ void grid_doc(const EStepArgs<float>& a, GLds<S>& sm, int64_t slot_, int tid) {
   constexpr int W = S::W, KL = S::KL;
   constexpr int N1 = hup(KL), N2 = hup(N1), N3 = hup(N2), N4 = hup(N3), N5 = hup(N4);
-  __shared__ GLds<S> sm;
-  if ((int64_t)blockIdx.x >= a.n) return;
   GDoc d;
 #ifdef STC_STAMP
   d.st0 = stamp_now();
 #endif
-  d.lane = threadIdx.x & 63;
-  d.wave = threadIdx.x >> 6;
+  d.lane = tid & 63;
+  d.wave = tid >> 6;
   d.g = (d.lane >> 3) & 1;
   d.rl = (d.lane & 7) | ((d.lane >> 4) << 3);
-  d.slot = a.slot0 + blockIdx.x;
+  d.slot = slot_;
   d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
   d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
   d.s0 = a.indptr[d.row];
   d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
+  if (SKIPLONG && ((d.nnz + 31) >> 5) > S::RMAX) return;
   d.e0 = a.bptr ? a.bptr[d.slot] : d.s0;
   d.k = a.k;
   d.kp = a.kp;
@@ -478,6 +481,36 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_grid(EStepArgs<floa
   }
 }
 
+// one workgroup per slot; SKIPLONG: the long-document kernel takes the documents past S::RMAX sets
+template <class S, bool STATS, bool BOUND, bool SKIPLONG>
+__global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_grid(EStepArgs<float> a) {
+  __shared__ GLds<S> sm;
+  if ((int64_t)blockIdx.x >= a.n) return;
+  grid_doc<S, STATS, BOUND, SKIPLONG>(a, sm, a.slot0 + blockIdx.x, (int)threadIdx.x);
+}
+
+// the launch's documents past `rows` rows into a.long_list (word 0 the count, then slot offsets)
+__global__ void k_grid_long_list(EStepArgs<float> a, int rows) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const int64_t slot = a.slot0 + i;
+  const int64_t row = a.batch ? (int64_t)a.batch[slot] : slot;
+  if ((int)(a.indptr[row + 1] - a.indptr[row]) > rows) a.long_list[1 + atomicAdd(&a.long_list[0], 1)] = (int32_t)i;
+}
+
+// the listed long documents on a resident grid (as lda_rows64.hip's long-document kernel)
+template <class S, bool STATS, bool BOUND>
+__global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_grid_long(EStepArgs<float> a) {
+  __shared__ GLds<S> sm;
+  const int cnt = a.long_list[0];
+  for (int j = blockIdx.x; j < cnt; j += gridDim.x) {
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    grid_doc<S, STATS, BOUND, false>(a, sm, a.slot0 + a.long_list[1 + j], tid);
+    __syncthreads();  // LDS is the next document's
+  }
+}
+
 // diagnostic: STC_GRID_LDS_PAD bytes of unused dynamic LDS per workgroup lower the occupancy
 // (e.g. 80000 → one wave per SIMD), to read the stamps' per-phase latencies without a partner wave
 size_t lds_pad() {
@@ -488,31 +521,59 @@ size_t lds_pad() {
   return v;
 }
 
-template <class S>
+template <class S, bool SKIPLONG = false>
 void launch_g(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound) {
   const dim3 grid((unsigned)a.n);
   const int threads = 64 * S::W;
   const size_t pad = lds_pad();
-  if (stats) k_estep_grid<S, true, false><<<grid, threads, pad, s>>>(a);
-  else if (bound) k_estep_grid<S, false, true><<<grid, threads, pad, s>>>(a);
-  else k_estep_grid<S, false, false><<<grid, threads, pad, s>>>(a);
+  if (stats) k_estep_grid<S, true, false, SKIPLONG><<<grid, threads, pad, s>>>(a);
+  else if (bound) k_estep_grid<S, false, true, SKIPLONG><<<grid, threads, pad, s>>>(a);
+  else k_estep_grid<S, false, false, SKIPLONG><<<grid, threads, pad, s>>>(a);
   KERNEL_CHECK();
+}
+// documents of S::RMAX < sets ≤ L::RMAX: listed on the device, run by L's kernel on a resident grid
+// (one workgroup per SIMD pair at one wave per SIMD), then the rest by S's kernel
+template <class S, class L>
+void launch_g_split(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound) {
+  if (!a.long_list) throw Error(STC_ERR_STATE, "grid E-step: no long-document list buffer");
+  HIP_CHECK(hipMemsetAsync(a.long_list, 0, sizeof(int32_t), s));
+  k_grid_long_list<<<dim3((unsigned)((a.n + 255) / 256)), 256, 0, s>>>(a, 32 * S::RMAX);
+  KERNEL_CHECK();
+  int dev = 0, cus = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int threads = 64 * L::W;
+  auto run = [&](auto kern) {
+    int per_cu = 0;  // workgroups resident per CU at this kernel's registers / LDS
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, 0));
+    const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(a.n, (int64_t)cus * std::max(1, per_cu))));
+    kern<<<grid, threads, 0, s>>>(a);
+  };
+  if (stats) run(k_estep_grid_long<L, true, false>);
+  else if (bound) run(k_estep_grid_long<L, false, true>);
+  else run(k_estep_grid_long<L, false, false>);
+  KERNEL_CHECK();
+  launch_g<S, true>(s, a, stats, bound);
 }
 
 }  // namespace
 
 int grid_row_cap(int k) {
   if (k <= 64) return 32 * G64::RMAX;
-  if (k <= 104) return 32 * G104::RMAX;
+  if (k <= 104) return 32 * G104L::RMAX;
   if (k <= 128) return 32 * G128::RMAX;
   return 0;
 }
+int grid_onchip_rows(int k) { return k > 64 && k <= 104 ? 32 * G104::RMAX : grid_row_cap(k); }
 
-void launch_estep_grid(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound) {
+void launch_estep_grid(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound, bool long_docs) {
   if (a.n == 0) return;
   if (a.k <= 32) launch_g<G32>(s, a, stats, bound);
   else if (a.k <= 64) launch_g<G64>(s, a, stats, bound);
-  else if (a.k <= 104) launch_g<G104>(s, a, stats, bound);
+  else if (a.k <= 104) {
+    if (long_docs) launch_g_split<G104, G104L>(s, a, stats, bound);
+    else launch_g<G104>(s, a, stats, bound);
+  }
   else if (a.k <= 128) launch_g<G128>(s, a, stats, bound);
   else throw Error(STC_ERR_INVALID_ARG, "grid E-step: k > 128");
 }

@@ -69,9 +69,9 @@ struct EStepArgs {
   int32_t* iters = nullptr;            // n (optional)
   int32_t* nonempty = nullptr;         // n (optional)
   double* bound = nullptr;             // n (BOUND)
-  // fp64 rows kernel: scratch for the list of this launch's 7–8-row-set documents (capacity n slots +
-  // one count word), filled on the device before the long-document launch walks it (last, so the
-  // other kernels' argument layout is unchanged)
+  // fp64 rows / fp32 grid kernels: scratch for the list of this launch's long documents (capacity n
+  // slots + one count word), filled on the device before the long-document launch walks it (last, so
+  // the other kernels' argument layout is unchanged)
   int32_t* long_list = nullptr;
 };
 
@@ -93,7 +93,9 @@ void launch_estep(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound);
 
 // fp32 row-lane × topic-group grid E-step (lda_grid.hip): k <= 128, nnz <= grid_row_cap(k) (0 if n/a)
 int grid_row_cap(int k);
-void launch_estep_grid(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound);
+// documents past grid_onchip_rows(k) run in a second, resident launch (`long_docs`; a.long_list set)
+int grid_onchip_rows(int k);
+void launch_estep_grid(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound, bool long_docs);
 // fp64 rows-split E-step (lda_rows64.hip): k <= 104, nnz <= rows64_row_cap(k) (0 if n/a); documents
 // past rows64_onchip_rows(k) run in a second launch (`long_docs`)
 int rows64_row_cap(int k);

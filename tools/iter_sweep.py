@@ -28,16 +28,17 @@ def main():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--caps", default="1,2,4,8,0")
     p.add_argument("--seed", type=int, default=20261015)
+    p.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     a = p.parse_args()
     import stc
     from stc import synth
 
     ctx = stc.Context(0)
     corpus = synth.make_corpus(a.corpus, a.docs, a.tokens, a.vocab, a.k, a.seed)
-    dc = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F64)
+    dc = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F64 if a.dtype == "f64" else stc.STC_F32)
     # the model state: planted topics, or 20 uncapped minibatches from λ₀
     h0 = stc.LdaHandle(ctx, a.k, a.vocab, mini_batch_fraction=a.fraction, optimize_doc_concentration=True,
-                       seed=a.seed, dtype="f64")
+                       seed=a.seed, dtype=a.dtype)
     h0.set_corpus(dc, a.docs)
     if a.corpus == "zipf-lda":
         h0.set_topics(synth.planted_topics(a.vocab, a.k, seed=a.seed))
@@ -50,7 +51,7 @@ def main():
     rows = []
     for cap in [int(c) for c in a.caps.split(",")]:
         h = stc.LdaHandle(ctx, a.k, a.vocab, mini_batch_fraction=a.fraction, optimize_doc_concentration=True,
-                          seed=a.seed, dtype="f64", max_inner_iter=cap)
+                          seed=a.seed, dtype=a.dtype, max_inner_iter=cap)
         h.set_corpus(dc, a.docs)
         h.set_topics(lam)
         h.next(stats=False)  # warm-up
@@ -71,7 +72,7 @@ def main():
     x = np.array([r["mean_inner_iters"] for r in rows])
     y = np.array([r["estep_ms"] for r in rows])
     b, c = np.polyfit(x, y, 1)
-    print(json.dumps({"corpus": a.corpus, "fit": {"fixed_ms": round(float(c), 4), "ms_per_iter": round(float(b), 4)},
+    print(json.dumps({"corpus": a.corpus, "dtype": a.dtype, "fit": {"fixed_ms": round(float(c), 4), "ms_per_iter": round(float(b), 4)},
                       "rows": rows}))
 
 
