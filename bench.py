@@ -99,6 +99,20 @@ def algorithmic_bytes(nnz, k, docs, dtype):
     return a + b + docs * c
 
 
+# the E-step kernels' sources: a PMC entry counts only if it was measured on these exact files
+ESTEP_SOURCES = ("lda_rows64.hip", "lda_grid.hip", "lda_wide.hip", "lda.hip", "estep_common.h", "lda_kernels.h")
+
+
+def estep_sources_sha():
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in ESTEP_SOURCES:
+        with open(os.path.join(ROOT, "spark-text-clustering_amd", "csrc", f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(a, dtype, corpus):
     """HBM bytes per launch of the training E-step kernel from the committed PMC summary
     (tools/pmc_summary.py over tools/gpu_prof.sh's separate FETCH_SIZE / WRITE_SIZE passes), if it
@@ -112,8 +126,16 @@ def pmc_traffic(a, dtype, corpus):
     for e in pm.get("entries", [pm]):
         w = e.get("workload", {})
         if (w.get("docs"), w.get("k"), w.get("vocab"), w.get("tokens"), w.get("fraction"), w.get("corpus"),
-                w.get("dtype", "f32")) == want and "estep_kernel_bytes_per_launch" in e:
-            return e["estep_kernel_bytes_per_launch"], f"{os.path.basename(PMC_SUMMARY)} ({e.get('note', '')})"
+                w.get("dtype", "f32")) != want:
+            continue
+        b = e.get("estep_kernel_bytes_per_launch")
+        if not e.get("estep_kernel") or not b:
+            return None, f"PMC entry {e.get('tag', '?')} names no E-step kernel (broken summary)"
+        sha = estep_sources_sha()
+        if e.get("estep_sources_sha") != sha:
+            return None, (f"PMC entry {e.get('tag', '?')} was measured on other E-step sources "
+                          f"({e.get('estep_sources_sha')} vs HEAD {sha}): not a measurement of this code")
+        return b, f"{os.path.basename(PMC_SUMMARY)} ({e.get('note', '')})"
     return None, "no PMC summary committed for this workload"
 
 
@@ -249,26 +271,65 @@ def featurization(stc, ctx, a, log, tokens, reps=3):
     }
 
 
-def run_state(stc, ctx, dcorp, a, dtype, total, lam0, barrier, log, steps, warmup):
-    """One training run: λ₀ (random Gamma, or the given topicsMatrix), 3 timed cold minibatches,
-    burn-in + warmup to the fixed state, then exactly `steps` timed minibatches."""
-    h = stc.LdaHandle(ctx, a.k, a.vocab, mini_batch_fraction=a.fraction, optimize_doc_concentration=True,
-                      seed=a.seed, dtype=dtype)
-    h.set_corpus(dcorp, total)
+class _Single:
+    """one stc_lda on this process's context (N = 1, or one rank per GPU under torchrun)"""
+
+    def __init__(self, stc, ctx, a, dtype, dcorp, total):
+        self.ctx = ctx
+        self.h = stc.LdaHandle(ctx, a.k, a.vocab, mini_batch_fraction=a.fraction, optimize_doc_concentration=True,
+                               seed=a.seed, dtype=dtype)
+        self.h.set_corpus(dcorp, total)
+
+    def sync(self):
+        self.ctx.synchronize()
+
+    def counters(self):  # (this process's view, the local view)
+        c = self.h.counters()
+        return c, c
+
+    def phases(self):
+        return self.h.phase_times(), None
+
+
+class _Group:
+    """one stc_group over N devices from this process (stc_group_*: the JVM drop-in's local[*] form)"""
+
+    def __init__(self, stc, a, dtype, corpus, devices):
+        self.h = stc.LdaGroup(devices, a.k, a.vocab, mini_batch_fraction=a.fraction, optimize_doc_concentration=True,
+                              seed=a.seed, dtype=dtype)
+        self.h.set_corpus(corpus)
+
+    def sync(self):
+        self.h.synchronize()
+
+    def counters(self):  # (Σ over the members, member 0)
+        cs = self.h.counters()
+        tot = {key: sum(c[key] for c in cs) for key in cs[0]}
+        return tot, cs[0]
+
+    def phases(self):  # member 0's phase times, and the slowest member's E-step
+        ps = self.h.phase_times()
+        return ps[0], max(p["estep"] for p in ps)
+
+
+def run_state(m, lam0, barrier, log, a, dtype, steps, warmup):
+    """One training run on model m (_Single / _Group): λ₀ (random Gamma, or the given topicsMatrix), 3
+    timed cold minibatches, burn-in + warmup to the fixed state, then exactly `steps` timed minibatches."""
+    h = m.h
     if lam0 is None:
         h.init_random(a.seed)
     else:
         h.set_topics(lam0)
-    ctx.synchronize()
-    cc0 = h.counters()
+    m.sync()
+    cc0, _ = m.counters()
     t0 = time.perf_counter()
     n_cold = 3
     for _ in range(n_cold):
         h.next(stats=False)
-    ctx.synchronize()
+    m.sync()
     cold_s = time.perf_counter() - t0
-    cc1 = h.counters()
-    cold = {"docs_per_s_rank": (cc1["docs"] - cc0["docs"]) / cold_s,
+    cc1, _ = m.counters()
+    cold = {"docs_per_s": (cc1["docs"] - cc0["docs"]) / cold_s,
             "mean_inner_iters": (cc1["inner_iters"] - cc0["inner_iters"]) / max(1, cc1["docs"] - cc0["docs"]),
             "minibatches": n_cold}
     burn = max(0, a.state_minibatches - n_cold - warmup)
@@ -276,10 +337,10 @@ def run_state(stc, ctx, dcorp, a, dtype, total, lam0, barrier, log, steps, warmu
     for i in range(burn + warmup):
         h.next(stats=False)
         if i % 4 == 3:  # progress (a profiler pass serialises kernels: keep the log moving)
-            ctx.synchronize()
+            m.sync()
             log(f"  minibatch {n_cold + i + 1}")
-    ctx.synchronize()
-    c0 = h.counters()
+    m.sync()
+    c0, l0 = m.counters()
     h.enable_timing(True)
     barrier()
     log(f"timing {steps} steps ({dtype})")
@@ -288,11 +349,13 @@ def run_state(stc, ctx, dcorp, a, dtype, total, lam0, barrier, log, steps, warmu
         h.next(stats=False)
     barrier()
     elapsed = time.perf_counter() - t_start
-    phases = h.phase_times()
-    c1 = h.counters()
-    return h, {"elapsed": elapsed, "phases": phases, "cold": cold, "docs": c1["docs"] - c0["docs"],
-               "entries": c1["entries"] - c0["entries"], "iters": c1["inner_iters"] - c0["inner_iters"],
-               "cap_hits": c1["cap_hits"] - c0["cap_hits"]}
+    phases, estep_max = m.phases()
+    c1, l1 = m.counters()
+    return {"elapsed": elapsed, "phases": phases, "estep_ms_slowest_member": estep_max, "cold": cold,
+            "docs": c1["docs"] - c0["docs"], "entries": c1["entries"] - c0["entries"],
+            "iters": c1["inner_iters"] - c0["inner_iters"], "cap_hits": c1["cap_hits"] - c0["cap_hits"],
+            "docs_local": l1["docs"] - l0["docs"], "entries_local": l1["entries"] - l0["entries"],
+            "iters_local": l1["inner_iters"] - l0["inner_iters"]}
 
 
 def summarize(r, a, dtype, world, steps, corpus_kind, kernel):
@@ -314,7 +377,9 @@ def summarize(r, a, dtype, world, steps, corpus_kind, kernel):
         "mean_nnz_per_doc": r["entries_all"] / max(1.0, r["docs_all"]),
         "mean_inner_iters": r["iters_all"] / max(1.0, r["docs_all"]),
         "cap_hits": r["cap_hits"],
-        "phase_ms": {k: round(v, 4) for k, v in r["phases"].items() if k != "steps"},
+        "phase_ms": dict({k: round(v, 4) for k, v in r["phases"].items() if k != "steps"},
+                         **({"estep_slowest_member": round(r["estep_ms_slowest_member"], 4)}
+                            if r.get("estep_ms_slowest_member") is not None else {})),
         "estep_only_docs_per_s": per_step_docs * world / (estep_ms * 1e-3),
         "cold": r["cold"],
         "roofline": {
@@ -344,13 +409,22 @@ def kernel_name(dtype, k):
     return "k_estep_grid (lda_grid.hip): the fp32 training E-step, one launch per minibatch"
 
 
+def launch_mode(gpus, env):
+    """How this process runs N GPUs: "ranks" — one process per GPU under torchrun (WORLD_SIZE set); "group"
+    — `python bench.py --gpus N` with no launcher: ONE process drives the N devices through stc_group (the
+    reference's own deployment, one JVM on Spark local[*], LDATraining.scala:7); "single" — N = 1."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if world > 1:
+        return "ranks", world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
+    if gpus > 1:
+        return "group", gpus, 0, 0
+    return "single", 1, 0, 0
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        a.gpus = world
+    mode, world, rank, local = launch_mode(a.gpus, os.environ)
+    a.gpus = world
     log = (lambda msg: print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True))  # progress on stderr
     from stc import synth  # no GPU touched yet: the corpus pool may fork
 
@@ -361,16 +435,28 @@ def main():
         print(json.dumps(featurization(stc, stc.Context(local), a, log, tokens, reps=max(1, a.steps))), flush=True)
         return
 
-    # corpus shard: strong = rows [r·D/N, (r+1)·D/N) of one corpus; weak = an own D-doc corpus per rank
-    if a.scaling == "strong":
-        lo, hi, seed, total = rank * a.docs // world, (rank + 1) * a.docs // world, a.seed, a.docs
-    else:
-        lo, hi, seed, total = 0, a.docs, a.seed + 7919 * rank, a.docs * world
-    workers = max(1, min(a.workers, (os.cpu_count() or 1)) // max(1, world))
+    # corpus: strong = rows [r·D/N, (r+1)·D/N) of one corpus; weak = an own D-doc corpus per rank / member.
+    # A group is given the whole corpus on the host and shards it itself (contiguous rows, balanced by entries).
     t0 = time.perf_counter()
-    corpus = synth.make_corpus(a.corpus, a.docs, a.tokens, a.vocab, a.k, seed, lo, hi, workers)
+    if mode == "group":
+        workers = max(1, min(a.workers, os.cpu_count() or 1))
+        if a.scaling == "strong":
+            corpus, total = synth.make_corpus(a.corpus, a.docs, a.tokens, a.vocab, a.k, a.seed, 0, a.docs, workers), a.docs
+        else:
+            parts = [synth.make_corpus(a.corpus, a.docs, a.tokens, a.vocab, a.k, a.seed + 7919 * r, 0, a.docs, workers)
+                     for r in range(world)]
+            corpus, total = synth.concat_rows(parts, a.vocab), a.docs * world
+            del parts
+        lo, hi = 0, corpus.num_rows
+    else:
+        if a.scaling == "strong":
+            lo, hi, seed, total = rank * a.docs // world, (rank + 1) * a.docs // world, a.seed, a.docs
+        else:
+            lo, hi, seed, total = 0, a.docs, a.seed + 7919 * rank, a.docs * world
+        workers = max(1, min(a.workers, (os.cpu_count() or 1)) // max(1, world))
+        corpus = synth.make_corpus(a.corpus, a.docs, a.tokens, a.vocab, a.k, seed, lo, hi, workers)
     gen_s = time.perf_counter() - t0
-    log(f"corpus rows [{lo}, {hi}) generated in {gen_s:.1f} s")
+    log(f"{mode}: corpus rows [{lo}, {hi}) generated in {gen_s:.1f} s")
     secondary = world == 1 and not a.no_secondary
     planted = None
     if secondary:
@@ -383,22 +469,44 @@ def main():
         log(f"token corpus generated in {time.perf_counter() - t0:.1f} s")
 
     dist = None
-    if world > 1:
+    if mode == "ranks":
         import torch.distributed as dist  # control plane only (uid exchange, barrier, max time)
 
         dist.init_process_group("gloo")
     import stc
 
-    ctx = stc.Context(local)
-    if world > 1:
-        obj = [stc.Context.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        ctx.comm_init(obj[0], world, rank)
+    lam_head = None
+    if a.state == "planted":
+        if a.corpus != "zipf-lda":
+            raise SystemExit("--state planted needs --corpus zipf-lda")
+        lam_head = synth.planted_topics(a.vocab, a.k, seed=a.seed)
+    DT = {"f32": stc.STC_F32, "f64": stc.STC_F64}
+    if mode == "group":
+        n_dev = stc.Context.device_count()
+        if n_dev < world:
+            raise SystemExit(f"bench.py --gpus {world}: only {n_dev} device(s) visible; refusing to report "
+                             f"{world} GPUs")
+        devices = list(range(world))
+        log(f"stc_group over devices {devices}")
+        model = _Group(stc, a, a.dtype, corpus, devices)
+        ctx = None
 
-    def barrier():
-        ctx.synchronize()
-        if dist is not None:
-            dist.barrier()
+        def barrier():
+            model.sync()
+    else:
+        ctx = stc.Context(local)
+        if mode == "ranks":
+            obj = [stc.Context.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            ctx.comm_init(obj[0], world, rank)
+
+        def barrier():
+            ctx.synchronize()
+            if dist is not None:
+                dist.barrier()
+
+        dcorp = {a.dtype: stc.DeviceCsr.upload(ctx, corpus, DT[a.dtype])}
+        model = _Single(stc, ctx, a, a.dtype, dcorp[a.dtype], total)
 
     def reduce_run(r):
         el, d, e, it = r["elapsed"], float(r["docs"]), float(r["entries"]), float(r["iters"])
@@ -410,31 +518,24 @@ def main():
             s = torch.tensor([d, e, it], dtype=torch.float64)
             dist.all_reduce(s)
             el, (d, e, it) = float(t[0]), (float(x) for x in s)
-        r.update(elapsed=el, docs_local=r["docs"], entries_local=r["entries"], iters_local=r["iters"],
-                 docs_all=d, entries_all=e, iters_all=it)
+        r.update(elapsed=el, docs_all=d, entries_all=e, iters_all=it)
         return r
 
-    DT = {"f32": stc.STC_F32, "f64": stc.STC_F64}
-    dcorp = {a.dtype: stc.DeviceCsr.upload(ctx, corpus, DT[a.dtype])}
-    lam_head = None
-    if a.state == "planted":
-        if a.corpus != "zipf-lda":
-            raise SystemExit("--state planted needs --corpus zipf-lda")
-        lam_head = synth.planted_topics(a.vocab, a.k, seed=seed)
-    h, r = run_state(stc, ctx, dcorp[a.dtype], a, a.dtype, total, lam_head, barrier, log, a.steps, a.warmup)
+    r = run_state(model, lam_head, barrier, log, a, a.dtype, a.steps, a.warmup)
     head = summarize(reduce_run(r), a, a.dtype, world, a.steps, a.corpus, kernel_name(a.dtype, a.k))
+    h = model.h
 
     lines = []
     if secondary:
         other = "f32" if a.dtype == "f64" else "f64"
         dcorp[other] = stc.DeviceCsr.upload(ctx, corpus, DT[other])
-        _, r2 = run_state(stc, ctx, dcorp[other], a, other, total, None, barrier, log, a.steps, a.warmup)
+        r2 = run_state(_Single(stc, ctx, a, other, dcorp[other], total), None, barrier, log, a, other, a.steps, a.warmup)
         s2 = summarize(reduce_run(r2), a, other, world, a.steps, a.corpus, kernel_name(other, a.k))
         lines.append(dict(label=f"{other} E-step, same corpus and model state", dtype=other, corpus=a.corpus, **s2))
         pc, lam_p = planted
         for dt in (a.dtype, other):
             dp = stc.DeviceCsr.upload(ctx, pc, DT[dt])
-            _, r3 = run_state(stc, ctx, dp, a, dt, a.docs, lam_p, barrier, log, a.steps, a.warmup)
+            r3 = run_state(_Single(stc, ctx, a, dt, dp, a.docs), lam_p, barrier, log, a, dt, a.steps, a.warmup)
             s3 = summarize(reduce_run(r3), a, dt, world, a.steps, "zipf-lda", kernel_name(dt, a.k))
             lines.append(dict(label=f"{dt} E-step, planted-topic corpus at the planted model (SURVEY §8(d) state B)",
                               dtype=dt, corpus="zipf-lda", **s3))
@@ -457,6 +558,7 @@ def main():
                 note="the E-step iterates a register-resident block (~150 fixed-point iterations per doc at this "
                      "state), so it is VALU-bound and the HBM fraction is small by construction; see "
                      "roofline_compute and the planted-state secondary line")
+    parallelism = {"single": "dp1", "ranks": f"dp{world}", "group": f"group{world}"}[mode]
     line = {
         "metric": METRIC,
         "value": head["value"],
@@ -471,12 +573,16 @@ def main():
         "dtype": a.dtype,
         "data": f"synthetic {a.corpus} corpus (seeded, generated in {gen_s:.0f} s), resident in HBM",
         "config": {
-            "baseline_config": f"configs[{a.config - 1}]",
+            "baseline_config": f"configs[{a.config - 1}]" if world == 1 or a.config != 2 else "configs[2]",
             "workload": f"online LDA minibatch steps: {a.docs} docs x {a.tokens} tokens"
                         f"{' per GPU' if a.scaling == 'weak' else ' sharded over the GPUs'}, V={a.vocab}, k={a.k}, "
                         f"subsamplingRate={a.fraction}",
             "docs": a.docs, "tokens_per_doc": a.tokens, "vocab": a.vocab, "k": a.k,
-            "subsampling_rate": a.fraction, "corpus": a.corpus, "parallelism": f"dp{world}",
+            "subsampling_rate": a.fraction, "corpus": a.corpus, "parallelism": parallelism,
+            "launch": {"single": "one process, one GPU",
+                       "ranks": f"{world} processes (torchrun), one GPU each, RCCL communicator via stc_comm_init",
+                       "group": f"one process, {world} GPUs through stc_group (one host thread per device, "
+                                f"ncclCommInitAll)"}[mode],
             "mean_nnz_per_doc": head["mean_nnz_per_doc"], "mean_inner_iters": head["mean_inner_iters"],
             "model_state": (f"after {a.state_minibatches} minibatches from lambda0 (Gamma(100,1/100))"
                             if a.state == "burn-in" else

@@ -33,8 +33,10 @@
  *     the calling thread is returned by stc_last_error().  The library never aborts.
  *   - The caller owns every host array; output arrays are caller-allocated with the sizes given
  *     in each comment.  The library owns all device memory behind the opaque handles.
- *   - A handle is not thread-safe: serialise calls per handle.  One stc_ctx = one GPU; for
- *     several GPUs run one process (or thread) per GPU and connect them with stc_comm_init.
+ *   - A handle is not thread-safe: serialise calls per handle.  One stc_ctx = one GPU.  Several
+ *     GPUs are driven either from ONE process through an stc_group (one handle, N devices, one
+ *     host thread per member inside each group call — the JVM drop-in's form, Spark local[*]), or
+ *     by one process per GPU whose contexts are connected with stc_comm_init.
  *   - Matrices are row-major.  The topics matrix crosses the boundary as V×k (Spark's
  *     topicsMatrix orientation, element (v, t) at [v*k + t]) unless a KV layout flag is given.
  */
@@ -276,6 +278,8 @@ int stc_group_set_topics(stc_group* g, const double* topics, int layout);
 int stc_group_get_topics(stc_group* g, double* topics_out, int layout);
 int stc_group_get_alpha(stc_group* g, double* alpha_out /* k */);
 int stc_group_get_iteration(stc_group* g, int64_t* iteration_out);
+/* waits until every member's queued work (the last next / step included) has finished */
+int stc_group_synchronize(stc_group* g);
 /* OnlineLDAOptimizer.next() over every member's documents; stats summed over the members */
 int stc_group_next(stc_group* g, stc_step_stats* stats);
 /* submitMiniBatch over injected GLOBAL document ids (gamma0 n×k in the same order, may be NULL) */

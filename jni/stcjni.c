@@ -625,6 +625,8 @@ JNIEXPORT void JNICALL FN(groupSetCorpus)(JNIEnv* env, jclass c, jlong g, jlong 
   check(env, st);
 }
 
+JNIEXPORT void JNICALL FN(groupSynchronize)(JNIEnv* env, jclass c, jlong g) { check(env, stc_group_synchronize(GRP(g))); }
+
 JNIEXPORT void JNICALL FN(groupInitRandom)(JNIEnv* env, jclass c, jlong g, jlong seed) {
   check(env, stc_group_init_random(GRP(g), (uint64_t)seed));
 }

@@ -127,6 +127,7 @@ public final class StcNative {
   public static native void groupSetCorpus(long group, long rows, long cols, long[] indptr, int[] indices,
                                            double[] values);
   public static native void groupInitRandom(long group, long seed);
+  public static native void groupSynchronize(long group);
   public static native void groupSetTopics(long group, double[] topics, int layout);
   public static native void groupGetTopics(long group, double[] out, int layout);
   public static native void groupGetAlpha(long group, double[] out);

@@ -79,7 +79,7 @@ struct stc_lda {
   int team_force = 0;
   DevBuf team_words, team_x;
   unsigned* htmo = nullptr;  // pinned copy of the team kernel's timeout word
-  bool team_ran = false;     // the current call launched a team kernel (its timeout word is checked)
+  int64_t team_fallbacks = 0;  // team launches re-run on the one-CU kernel after a timeout
 
   // M-step sharding over the vocabulary (multi-GPU): rank r owns λ / expElogβ rows [r·Vs, (r+1)·Vs);
   // Vs is a multiple of the λ-update block so the per-block colsum partials (and hence colsum) are
@@ -520,32 +520,11 @@ TeamChoice team_choice(const stc_lda& L, double mean_rows) {
   return {std::max(2, std::min(4, (L.k + 1023) / 1024)), true};
 }
 
-// The team kernel's timeout word: a team whose partner never arrived gave up instead of hanging.  The
-// word gates the same call's M-step on the device (launch_gate_on_timeout poisons the non-empty count,
-// so λ, expElogβ', colsum and α stay as they were) and is copied to pinned memory after the launch;
-// finish_team() waits for the stream at the end of the call and raises the failure there — from the
-// call that failed, never from a later one.  `rollback`: undo the host-side step bookkeeping.
-void finish_team(stc_lda& L, bool rollback, int64_t n, int64_t E) {
-  if (!L.team_ran) return;
-  L.team_ran = false;
-  HIP_CHECK(hipStreamSynchronize(L.ctx->stream));
-  bool failed = L.htmo && *L.htmo;
-  if (rollback && !failed) {  // another rank's team timed out: its poisoned count reached this rank too
-    double gate = 0.0;
-    HIP_CHECK(hipMemcpy(&gate, L.small.as<double>() + L.k, sizeof(double), hipMemcpyDeviceToHost));
-    failed = gate < 0.0;
-  }
-  if (failed) {
-    if (L.htmo) *L.htmo = 0;
-    if (rollback) {
-      L.iteration -= 1;
-      L.cum_docs -= n;
-      L.cum_entries -= E;
-    }
-    throw Error(STC_ERR_HIP, "many-topic team E-step: a team member did not arrive (timed out); the model "
-                             "was left unchanged");
-  }
-}
+// The team kernel's timeout word: a member whose partner never arrived (a block that was not
+// co-resident after all, e.g. another process holding CUs) gave up instead of hanging, and so did its
+// team.  launch_split() reads the word right after the launch and, when it is set, runs the same slots
+// again on the one-CU kernel inside the same call: the step completes with the one-CU kernel's results
+// (which every member of a group or every rank gets on its own, so no rank's state can diverge).
 // debug knob STC_TEAM_FAULT=m: member m of team 0 never publishes (its partners time out quickly)
 int team_fault_member() {
   const char* e = getenv("STC_TEAM_FAULT");
@@ -582,10 +561,7 @@ bool launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamCh
   HIP_CHECK(hipMemsetAsync(L.team_words.p, 0, 16, s));
   HIP_CHECK(hipMemsetAsync(L.team_x.p, 0, xbytes, s));
   const bool ok = tc.topics ? lda::launch_estep_wide_tc<T>(s, w, stats, wt) : lda::launch_estep_wide_mc<T>(s, w, stats, wt);
-  if (ok) {
-    HIP_CHECK(hipMemcpyAsync(L.htmo, wt.tmo, sizeof(unsigned), hipMemcpyDeviceToHost, s));
-    L.team_ran = true;
-  }
+  if (ok) HIP_CHECK(hipMemcpyAsync(L.htmo, wt.tmo, sizeof(unsigned), hipMemcpyDeviceToHost, s));
   return ok;
 }
 
@@ -602,8 +578,13 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
     w.n = n_short;
     const TeamChoice tc = use_wide(L.k, L.dtype) && !bound ? team_choice<T>(L, mean_rows) : TeamChoice{};
     const bool team = tc.P > 1 && launch_wide_team<T>(L, w, stats, tc);
-    if (team) {
-      // launched (a grid that could not be resident falls through to the one-CU kernel)
+    if (team) {  // launched (a grid that could not be resident falls through to the one-CU kernel)
+      HIP_CHECK(hipStreamSynchronize(s));
+      if (*L.htmo) {  // a team gave up: the same slots on the one-CU kernel (it rewrites every output)
+        *L.htmo = 0;
+        L.team_fallbacks += 1;
+        lda::launch_estep_wide<T>(s, w, stats, bound);
+      }
     } else if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
     else if constexpr (std::is_same<T, float>::value) {
       const bool long_docs = m.max_row < 0 || m.max_row > lda::grid_onchip_rows(L.k);
@@ -667,7 +648,6 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   a.iters = L.iters.as<int32_t>();
   a.nonempty = L.nonempty.as<int32_t>();
   record(L, 1);
-  L.team_ran = false;
   launch_split<T>(L, *L.corpus, a, n, n_short, true, false, n > 0 ? (double)E / (double)n : 0.0);
   record(L, 2);
   HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.vpad * L.kp, s));  // padded rows stay zero
@@ -689,7 +669,6 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
     HIP_CHECK(hipMemsetAsync(L.small.p, 0, sizeof(double) * (L.k + 1), s));
     HIP_CHECK(hipMemsetAsync(L.stats4.p, 0, sizeof(int64_t) * 4, s));
   }
-  if (L.team_ran) lda::launch_gate_on_timeout(s, L.team_words.as<unsigned>(), L.small.as<double>(), L.k);
   record(L, 3);
 }
 
@@ -822,7 +801,18 @@ void step_ids(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, s
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
   estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1);
   train_tail<T>(L, n, p.E, st);
-  finish_team(L, true, n, p.E);
+}
+
+// A call that failed after queuing the next draw on the side stream (before train_tail ordered the main
+// stream behind it) leaves that draw in flight: wait for it and drop it, so nothing samples into the same
+// count buffers concurrently and the next call draws synchronously.
+void settle_side(stc_lda& L) {
+  if (!L.samp_pending) return;
+  L.ctx->use();
+  HIP_CHECK(hipStreamSynchronize(L.side));
+  L.samp_pending = false;
+  L.pre_inflight = false;
+  L.pre_valid = false;
 }
 
 // sample draw `draw` on the device: per-doc counts (Poisson / Bernoulli), their scans, and (n, E,
@@ -855,6 +845,7 @@ void sample_draw(stc_lda& L, int64_t draw, hipStream_t s, DevBuf* tmp) {
 template <typename T>
 void next_impl(stc_lda& L, stc_step_stats* st) {
   require_ready(L);
+  settle_side(L);
   relayout(L);
   ensure_order(L);
   Ctx& c = *L.ctx;
@@ -914,7 +905,6 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
   L.pre_draw = draw + 1;
   estep_and_stats<T>(L, n, ns32, E, nullptr, L.iteration + 1);
   train_tail<T>(L, n, E, st);
-  finish_team(L, true, n, E);
 }
 
 template <typename T>
@@ -930,7 +920,6 @@ void estep_only(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0,
   L.timing = false;
   estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1);
   L.timing = t;
-  finish_team(L, false, n, p.E);
   if (gamma_out && n > 0) {
     std::vector<T> g((size_t)(n * L.k));
     HIP_CHECK(hipMemcpyAsync(g.data(), L.gamma.p, sizeof(T) * g.size(), hipMemcpyDeviceToHost, s));
@@ -978,9 +967,7 @@ void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const
   a.gamma = gamma_out ? L.gamma.as<T>() : nullptr;
   a.iters = L.iters.as<int32_t>();
   a.bound = bound ? L.bound.as<double>() : nullptr;
-  L.team_ran = false;
   launch_split<T>(L, docs, a, n, p.n_short, false, bound, n > 0 ? (double)docs.nnz / (double)n : 0.0);
-  finish_team(L, false, 0, 0);
   if (gamma_out && n > 0) {
     std::vector<T> g((size_t)(n * L.k));
     HIP_CHECK(hipMemcpyAsync(g.data(), L.gamma.p, sizeof(T) * g.size(), hipMemcpyDeviceToHost, s));
@@ -1576,6 +1563,7 @@ int stc_lda_destroy(stc_lda* lda) {
     if (!lda) return;
     (void)hipSetDevice(lda->ctx->device);
     (void)hipStreamSynchronize(lda->ctx->stream);
+    if (lda->side) (void)hipStreamSynchronize(lda->side);
     delete lda;
   });
 }
@@ -1589,6 +1577,7 @@ int stc_lda_set_corpus(stc_lda* L, const stc_dcsr* corpus, int64_t corpus_size_t
     STC_REQUIRE(corpus->rows < (int64_t(1) << 31), "at most 2^31-1 documents per rank");
     STC_REQUIRE(corpus_size_total >= corpus->rows && corpus_size_total > 0,
                 "corpus_size_total must be >= this rank's rows and > 0");
+    settle_side(*L);  // a draw still being sampled reads the previous corpus
     L->corpus = corpus;
     L->corpus_total = corpus_size_total;
     L->pre_valid = false;  // a prefetched draw sampled the previous corpus
@@ -2029,12 +2018,24 @@ int stc_group_set_corpus(stc_group* g, int64_t n_rows, int64_t n_cols, const int
     const std::vector<int64_t> r0 = shard_rows(indptr, n_rows, g->n());
     std::vector<stc_dcsr*> shard((size_t)g->n(), nullptr);
     try {
+      // every shard uploaded before any member is switched to it: a failed upload (out of memory) leaves
+      // every member on its previous shard
+      const char* fe = getenv("STC_GROUP_UPLOAD_FAULT");  // debug knob: member i's upload fails (tests)
+      const int fault = fe ? atoi(fe) : -1;
       for_members(*g, [&](int i) {
+        if (i == fault) throw Error(STC_ERR_OOM, "injected shard upload failure (STC_GROUP_UPLOAD_FAULT)");
         shard[(size_t)i] = upload_rows(g->ctx[(size_t)i], r0[(size_t)i], r0[(size_t)i + 1], n_cols, indptr, indices,
                                        values, g->dtype);
-        member_ok(stc_lda_set_corpus(g->lda[(size_t)i], shard[(size_t)i], n_rows));
       });
+      for_members(*g, [&](int i) { member_ok(stc_lda_set_corpus(g->lda[(size_t)i], shard[(size_t)i], n_rows)); });
     } catch (...) {
+      // members already switched go back to their previous shard (or to none) before the new ones are freed
+      for (int i = 0; i < g->n(); ++i) {
+        stc_lda* l = g->lda[(size_t)i];
+        if (!shard[(size_t)i] || l->corpus != shard[(size_t)i]) continue;
+        stc_dcsr* old = (size_t)i < g->shard.size() ? g->shard[(size_t)i] : nullptr;
+        if (!old || stc_lda_set_corpus(l, old, g->rows) != STC_OK) l->corpus = nullptr;
+      }
       for (auto* d : shard) (void)stc_dcsr_free(d);
       throw;
     }
@@ -2083,6 +2084,17 @@ int stc_group_get_iteration(stc_group* g, int64_t* iteration_out) {
   return guard([&] {
     STC_REQUIRE(g && iteration_out, "group/iteration_out");
     *iteration_out = g->lda[0]->iteration;
+  });
+}
+
+int stc_group_synchronize(stc_group* g) {
+  return guard([&] {
+    STC_REQUIRE(g, "group");
+    for (int i = 0; i < g->n(); ++i) {
+      g->ctx[(size_t)i]->use();
+      HIP_CHECK(hipStreamSynchronize(g->ctx[(size_t)i]->stream));
+      if (g->lda[(size_t)i]->side) HIP_CHECK(hipStreamSynchronize(g->lda[(size_t)i]->side));  // the next draw
+    }
   });
 }
 

@@ -578,7 +578,7 @@ __global__ __launch_bounds__(256) void k_lambda_eeb(double* __restrict__ lam, co
                                                     int64_t V, int k, int kp, double rho, double scale,
                                                     double eta, const double* __restrict__ gate,
                                                     double* __restrict__ colpart) {
-  if (gate && !(gate[0] > 0.0)) return;  // Spark: no non-empty docs ⇒ no update (< 0: a team timed out)
+  if (gate && !(gate[0] > 0.0)) return;  // Spark: no non-empty docs ⇒ no update
   __shared__ double s_acc[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t v0 = (int64_t)blockIdx.x * kRowsPerBlock;
@@ -865,14 +865,6 @@ __global__ __launch_bounds__(256) void k_update_alpha(double* __restrict__ alpha
   block_reduce3(bad, z2, dz3, s_r);
   if (bad == 0.0)
     for (int t = threadIdx.x; t < k; t += 256) alpha[t] += rho * s_g[t];
-}
-
-__global__ void k_gate_on_timeout(const unsigned* __restrict__ tmo, double* __restrict__ small, int k) {
-  if (*tmo) small[k] = -1e300;
-}
-void launch_gate_on_timeout(hipStream_t s, const unsigned* tmo, double* small, int k) {
-  k_gate_on_timeout<<<1, 1, 0, s>>>(tmo, small, k);
-  KERNEL_CHECK();
 }
 
 void launch_update_alpha(hipStream_t s, double* alpha, const double* small, int k, double rho) {

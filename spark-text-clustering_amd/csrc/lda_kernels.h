@@ -116,7 +116,6 @@ struct WideTeam {
 };
 // after the E-step's logphat: a timed-out team poisons the non-empty count (small[k] = −1e300, negative
 // after any all-reduce over ranks), which gates the λ / colsum / expElogβ' / α updates off
-void launch_gate_on_timeout(hipStream_t s, const unsigned* tmo, double* small, int k);
 template <typename T>
 int wide_resident_rows(int k);
 // false: the grid could not be resident at once (nothing launched; the caller runs the one-CU kernel)

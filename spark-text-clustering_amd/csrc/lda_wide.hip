@@ -859,7 +859,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
       ++it;
       STAMP(5);  // γ, ψ/exp
     }
-    if (s_abort) return;  // a team timed out: every block leaves (the host raises)
+    if (s_abort) return;  // a team timed out: every block leaves (the host re-runs the one-CU kernel)
 
     // ---- outputs: this member's rows; the topic-level ones from member 0
     if (tid < nloc) {
@@ -1187,7 +1187,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
       }
       ++it;
     }
-    if (s_abort) return;  // a team timed out: every block leaves (the host raises)
+    if (s_abort) return;  // a team timed out: every block leaves (the host re-runs the one-CU kernel)
 
     // ---- outputs: rows from member 0 (identical in every member); this member's topics
     if (member == 0 && tid < nnz) {
@@ -1290,7 +1290,8 @@ int wide_resident_rows(int k) {
 // the HSA runtime's teardown, after the profiler's finalisation (r03 exit probe: libamdhip64 exit
 // handler → libhsa-runtime64, on a /dev/dri mapping already released).  Residency is checked here; a
 // block that is nonetheless not co-resident (another process on the device) only delays its team, and
-// the bounded spins turn a delay past the limit into STC_ERR_HIP with λ untouched (launch_gate_on_timeout).
+// the bounded spins turn a delay past the limit into a timeout word, on which the host re-runs the
+// same slots on the one-CU kernel (api.hip launch_split).
 inline bool launch_resident(const void* kern, int blocks, size_t lds, void** args, hipStream_t s) {
   int dev = 0, cus = 0, per_cu = 0;
   HIP_CHECK(hipGetDevice(&dev));

@@ -58,6 +58,22 @@ def _lda_config(lib, k, vocab_size, doc_concentration, topic_concentration, tau0
     return cfg, alpha_buf
 
 
+def _phase_times(lib, h):
+    """stc_lda_phase_times of one handle: mean device ms per step of each phase"""
+    ms = np.zeros(5, np.float64)
+    steps = C.c_int64()
+    L.check(lib.stc_lda_phase_times(h, L.ptr(ms, C.c_double), C.byref(steps)))
+    return {"sample": ms[0], "estep": ms[1], "sstats": ms[2], "allreduce": ms[3], "mstep": ms[4],
+            "steps": steps.value}
+
+
+def _counters(lib, h):
+    """stc_lda_counters of one handle (cumulative since creation)"""
+    out = np.zeros(4, np.int64)
+    L.check(lib.stc_lda_counters(h, L.ptr(out, C.c_int64)))
+    return {"docs": int(out[0]), "entries": int(out[1]), "inner_iters": int(out[2]), "cap_hits": int(out[3])}
+
+
 class LdaHandle:
     """Owns one stc_lda (optimizer state + LocalLDAModel parameters on the GPU)."""
 
@@ -170,16 +186,10 @@ class LdaHandle:
         L.check(self.ctx.lib.stc_lda_enable_timing(self.handle, int(bool(on))))
 
     def phase_times(self):
-        ms = np.zeros(5, np.float64)
-        steps = C.c_int64()
-        L.check(self.ctx.lib.stc_lda_phase_times(self.handle, L.ptr(ms, C.c_double), C.byref(steps)))
-        return {"sample": ms[0], "estep": ms[1], "sstats": ms[2], "allreduce": ms[3], "mstep": ms[4],
-                "steps": steps.value}
+        return _phase_times(self.ctx.lib, self.handle)
 
     def counters(self):
-        out = np.zeros(4, np.int64)
-        L.check(self.ctx.lib.stc_lda_counters(self.handle, L.ptr(out, C.c_int64)))
-        return {"docs": int(out[0]), "entries": int(out[1]), "inner_iters": int(out[2]), "cap_hits": int(out[3])}
+        return _counters(self.ctx.lib, self.handle)
 
     def close(self):
         if self.handle:
@@ -243,6 +253,31 @@ class LdaGroup:
         x = C.c_int64()
         L.check(self.lib.stc_group_get_iteration(self.handle, C.byref(x)))
         return x.value
+
+    def synchronize(self):
+        """waits for every member's queued work (stc_group_synchronize)"""
+        L.check(self.lib.stc_group_synchronize(self.handle))
+
+    def members(self):
+        """the member stc_lda handles, for counters and timing only (stc_group_member)"""
+        out = []
+        for i in range(len(self.devices)):
+            h = C.c_void_p()
+            L.check(self.lib.stc_group_member(self.handle, i, C.byref(h)))
+            out.append(h)
+        return out
+
+    def enable_timing(self, on=True):
+        for h in self.members():
+            L.check(self.lib.stc_lda_enable_timing(h, int(bool(on))))
+
+    def phase_times(self):
+        """per member: mean device ms per step of each phase"""
+        return [_phase_times(self.lib, h) for h in self.members()]
+
+    def counters(self):
+        """per member: cumulative docs / entries / inner iterations / cap hits"""
+        return [_counters(self.lib, h) for h in self.members()]
 
     def step(self, batch_ids, gamma0=None, stats=True):
         ids = L.as_i64(batch_ids)

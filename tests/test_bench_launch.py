@@ -1,0 +1,131 @@
+"""CPU: bench.py's launch modes.
+
+`python bench.py --gpus N` with no launcher must drive N devices from one process through stc_group
+(the reference's own deployment: one JVM on Spark local[*], LDATraining.scala:7) and report what ran;
+under torchrun (WORLD_SIZE set) every rank drives its own GPU.  No GPU here: the device count and the
+group are mocked, so only the bench's host logic runs.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "spark-text-clustering_amd"))
+
+import bench  # noqa: E402
+
+
+def test_launch_mode():
+    assert bench.launch_mode(1, {}) == ("single", 1, 0, 0)
+    assert bench.launch_mode(8, {}) == ("group", 8, 0, 0)
+    assert bench.launch_mode(2, {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1"}) == ("ranks", 2, 1, 1)
+    assert bench.launch_mode(1, {"WORLD_SIZE": "4", "RANK": "0", "LOCAL_RANK": "0"})[0] == "ranks"
+
+
+class FakeGroup:
+    """stands in for stc.LdaGroup: records the devices and the corpus split, counts next() calls"""
+    made = []
+
+    def __init__(self, devices, k, vocab_size, **kw):
+        self.devices, self.k, self.V = list(devices), k, vocab_size
+        self.steps = 0
+        self.rows = 0
+        FakeGroup.made.append(self)
+
+    def set_corpus(self, corpus):
+        self.rows = corpus.num_rows
+        self.nnz = corpus.nnz
+
+    def init_random(self, seed):
+        pass
+
+    def set_topics(self, t):
+        pass
+
+    def next(self, stats=True):
+        self.steps += 1
+
+    def synchronize(self):
+        pass
+
+    def enable_timing(self, on=True):
+        pass
+
+    def counters(self):
+        n = len(self.devices)
+        return [{"docs": 10 * self.steps, "entries": 1000 * self.steps, "inner_iters": 50 * self.steps,
+                 "cap_hits": 0} for _ in range(n)]
+
+    def phase_times(self):
+        return [{"sample": 0.1, "estep": 1.0 + i, "sstats": 0.2, "allreduce": 0.3, "mstep": 0.1, "steps": 5}
+                for i in range(len(self.devices))]
+
+
+def _run_bench(monkeypatch, capsys, argv, n_dev):
+    import stc
+
+    FakeGroup.made.clear()
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(stc.Context, "device_count", staticmethod(lambda: n_dev))
+    monkeypatch.setattr(stc, "LdaGroup", FakeGroup)
+    monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+    bench.main()
+    out = capsys.readouterr().out.strip().splitlines()
+    return json.loads(out[-1])
+
+
+def test_gpus_n_without_launcher_drives_a_group(monkeypatch, capsys):
+    line = _run_bench(monkeypatch, capsys, ["--gpus", "2", "--steps", "3", "--warmup", "1", "--docs", "2000",
+                                            "--tokens", "20", "--vocab", "4096", "--k", "8", "--workers", "1",
+                                            "--no-hbm-copy"], n_dev=2)
+    (g,) = FakeGroup.made
+    assert g.devices == [0, 1]
+    assert g.rows == 2000  # strong scaling: the whole corpus, sharded by the group
+    assert line["n_gpus"] == 2
+    assert line["config"]["parallelism"] == "group2"
+    assert line["config"]["baseline_config"] == "configs[2]"
+    assert line["cpu_baseline"] is None and line["secondary"] == []
+    # value = docs of all members / wall time; the roofline uses member 0's launch
+    assert line["value"] > 0
+    assert line["config"]["phase_ms"]["estep_slowest_member"] == 2.0
+    assert line["roofline"]["kernel_ms_per_launch"] == 1.0
+
+
+def test_gpus_n_fails_loudly_when_fewer_devices_are_visible(monkeypatch, capsys):
+    with pytest.raises(SystemExit, match="only 1 device"):
+        _run_bench(monkeypatch, capsys, ["--gpus", "4", "--steps", "1", "--warmup", "0", "--docs", "500",
+                                         "--tokens", "10", "--vocab", "1024", "--k", "4", "--workers", "1",
+                                         "--no-hbm-copy"], n_dev=1)
+
+
+def test_weak_group_corpus_is_one_shard_per_member(monkeypatch, capsys):
+    line = _run_bench(monkeypatch, capsys, ["--gpus", "2", "--scaling", "weak", "--steps", "1", "--warmup", "0",
+                                            "--docs", "600", "--tokens", "10", "--vocab", "1024", "--k", "4",
+                                            "--workers", "1", "--no-hbm-copy"], n_dev=3)
+    (g,) = FakeGroup.made
+    assert g.rows == 1200 and line["scaling"] == "weak" and line["n_gpus"] == 2
+
+
+def test_traffic_is_null_with_a_reason_unless_measured_on_these_sources(tmp_path, monkeypatch):
+    class A:
+        docs, k, vocab, tokens, fraction = 1000000, 100, 1 << 18, 200, 0.05
+
+    wl = {"docs": A.docs, "tokens": A.tokens, "vocab": A.vocab, "k": A.k, "fraction": A.fraction,
+          "corpus": "zipf", "dtype": "f64"}
+    p = tmp_path / "pmc.json"
+    monkeypatch.setattr(bench, "PMC_SUMMARY", str(p))
+    p.write_text(json.dumps({"entries": [{"workload": wl, "estep_kernel": [], "estep_kernel_bytes_per_launch": 0.0}]}))
+    b, why = bench.pmc_traffic(A, "f64", "zipf")
+    assert b is None and "no E-step kernel" in why
+    p.write_text(json.dumps({"entries": [{"workload": wl, "estep_kernel": ["k"], "estep_kernel_bytes_per_launch": 4.6e9,
+                                          "estep_sources_sha": "0" * 16}]}))
+    b, why = bench.pmc_traffic(A, "f64", "zipf")
+    assert b is None and "other E-step sources" in why
+    p.write_text(json.dumps({"entries": [{"workload": wl, "estep_kernel": ["k"], "estep_kernel_bytes_per_launch": 4.6e9,
+                                          "estep_sources_sha": bench.estep_sources_sha()}]}))
+    assert bench.pmc_traffic(A, "f64", "zipf")[0] == 4.6e9
+    assert np.isfinite(bench.pmc_traffic(A, "f64", "zipf")[0])

@@ -149,3 +149,42 @@ def test_group_argument_errors(ctx):
         stc.LdaGroup([0, 99], 8, 100)
     with pytest.raises(stc.StcIllegalArgument):
         stc.LdaGroup([], 8, 100)
+
+
+def test_failed_set_corpus_leaves_every_member_on_its_shard(ctx, monkeypatch):
+    """member 1's upload of a new corpus fails (debug knob STC_GROUP_UPLOAD_FAULT=1).  The
+    call raises, no member was switched to the new shards (freed again), and training continues on the
+    previous corpus exactly as a group that never saw the failed call; also timing / counters per member."""
+    import stc
+
+    rng = np.random.default_rng(77)
+    D, V, k = 200, 2500, 24
+    corpus = random_corpus(rng, D, V, 1, 140)
+    other = random_corpus(rng, 150, V, 1, 90)
+    lam = rng.gamma(100.0, 0.01, size=(V, k))
+    ids = [rng.integers(0, D, size=60) for _ in range(2)]
+    g0 = [rng.gamma(100.0, 0.01, size=(60, k)) for _ in range(2)]
+
+    def run(fail):
+        with stc.LdaGroup([0, 0], k, V, dtype="f64") as g:
+            g.set_corpus(corpus)
+            g.set_topics(lam)
+            g.step(ids[0], g0[0])
+            if fail:
+                monkeypatch.setenv("STC_GROUP_UPLOAD_FAULT", "1")
+                with pytest.raises(stc.StcError, match="injected shard upload failure"):
+                    g.set_corpus(other)
+                monkeypatch.delenv("STC_GROUP_UPLOAD_FAULT")
+            g.enable_timing(True)
+            g.step(ids[1], g0[1])
+            g.next(stats=False)
+            g.synchronize()
+            cs = g.counters()
+            assert len(cs) == 2 and sum(c["docs"] for c in cs) > 0
+            assert all(p["estep"] >= 0.0 for p in g.phase_times())
+            return g.topics(), g.alpha()
+
+    t0, a0 = run(False)
+    t1, a1 = run(True)
+    np.testing.assert_array_equal(t1, t0)
+    np.testing.assert_array_equal(a1, a0)

@@ -452,33 +452,38 @@ def test_team_estep_many_documents(ctx, dtype, k, monkeypatch):
 
 
 @pytest.mark.parametrize("k", [300, 700])
-def test_team_timeout_fails_the_same_call_and_keeps_the_model(ctx, k, monkeypatch):
+def test_team_timeout_falls_back_to_the_one_cu_kernel(ctx, k, monkeypatch):
     """A team member that never publishes (debug knob STC_TEAM_FAULT=1, team forced to P = 2; k = 300
-    splits rows, k = 700 topics) makes its partner give up.  The SAME step call raises (STC_ERR_HIP),
-    λ, α and the iteration count are bit-identical to before it (the timeout word gated the M-step on
-    the device), topicDistribution raises the same way, and without the knob training continues."""
-    import stc
-
-    monkeypatch.setenv("STC_WIDE_TEAM", "2")
+    splits rows, k = 700 topics) makes its partner give up.  The SAME call re-runs the slots on the one-CU
+    kernel and returns OK: λ, α and γ are bit-identical to a run that used the one-CU kernel from the start
+    (STC_WIDE_TEAM=1), for a training step and for topicDistribution (VERDICT r3 #8)."""
     rng = np.random.default_rng(31 + k)
     D, V = 48, 2048
     corpus = random_corpus(rng, D, V, 100, 300)
     lam = rng.gamma(100.0, 0.01, size=(V, k))
     g0 = rng.gamma(100.0, 0.01, size=(D, k))
-    h, d = _handle(ctx, corpus, k, "f64", lam)
     ids = np.arange(D)
-    h.step(ids, g0)
-    lam1, a1, it1 = h.topics(), h.alpha(), h.iteration()
-    monkeypatch.setenv("STC_TEAM_FAULT", "1")
-    with pytest.raises(stc.StcError) as e:
+
+    def run(team, fault):
+        monkeypatch.setenv("STC_WIDE_TEAM", str(team))
+        if fault:
+            monkeypatch.setenv("STC_TEAM_FAULT", "1")
+        else:
+            monkeypatch.delenv("STC_TEAM_FAULT", raising=False)
+        h, d = _handle(ctx, corpus, k, "f64", lam)
         h.step(ids, g0)
-    assert "did not arrive" in str(e.value)
-    np.testing.assert_array_equal(h.topics(), lam1)
-    np.testing.assert_array_equal(h.alpha(), a1)
-    assert h.iteration() == it1
-    with pytest.raises(stc.StcError):
-        h.topic_distribution(d)
-    monkeypatch.delenv("STC_TEAM_FAULT")
-    h.step(ids, g0)
-    assert h.iteration() == it1 + 1
-    assert not np.array_equal(h.topics(), lam1)
+        h.step(ids, g0)
+        td = h.topic_distribution(d, gamma0=g0)
+        out = (h.topics(), h.alpha(), h.iteration(), td)
+        h.close()
+        d.free()
+        return out
+
+    one = run(1, False)
+    fb = run(2, True)
+    np.testing.assert_array_equal(fb[0], one[0])
+    np.testing.assert_array_equal(fb[1], one[1])
+    assert fb[2] == one[2] == 2
+    np.testing.assert_array_equal(fb[3], one[3])
+    team = run(2, False)  # the healthy team agrees with the one-CU kernel to rounding
+    np.testing.assert_allclose(team[0], one[0], rtol=1e-9)

@@ -21,8 +21,10 @@ import json
 import os
 import re
 import shutil
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 # kernels of the E-step phase (the bench roofline's "kernel"): E-step, term sort, sstats SpMM,
 # the stat memset, and the partition scans (rocprim; tiny)
@@ -33,9 +35,10 @@ PHASE = re.compile(r"k_estep|k_sstats|k_fixup|rocprim|fillBuffer|k_part_|k_fill_
 # (STATS = true, BOUND = false): k_estep / k_estep_grid / k_estep_wave / k_estep_wide <..., true, false>;
 # k_estep_grid64 / k_estep_rows64 <shape, true, false, LONG>; k_estep_wide_mc / _tc <T, Q, NR, true>
 ESTEP = re.compile(r"k_estep_grid64<DShape<[^>]*>, true, false, (true|false)>$"  # round-2 profiles
-                   r"|k_estep_rows64<RShape<[^>]*>, true, false, (true|false)>$"
+                   r"|k_estep_rows64(_long)?<RShape<[^>]*>, true, false(, (true|false))?>$"
+                   r"|k_estep_grid(_long)?<GShape<[^>]*>, true, false>$"
                    r"|k_estep_wide_(mc|tc)<\w+, \d+, \d+, true>$"
-                   r"|k_estep(_grid|_wave|_wide)?<(?!DShape).*, true, false>$")
+                   r"|k_estep(_wave|_wide)?<(?!DShape|RShape|GShape).*, true, false>$")
 
 
 def short(name):
@@ -101,9 +104,15 @@ def main():
     est_launches = max((v["dispatches"] for v in est.values()), default=0)
     est_bytes = sum((v["fetch_bytes_x2_per_dispatch"] + v["write_bytes_per_dispatch"]) * v["dispatches"]
                     for v in est.values()) / max(1, est_launches)
+    if not est or est_bytes <= 0:
+        raise SystemExit(f"no training E-step kernel matched among {sorted(kernels)[:12]}: refusing to write "
+                         f"an empty traffic entry (fix ESTEP)")
+    from bench import estep_sources_sha
+
+    sha = estep_sources_sha()
     wl = {"docs": a.docs, "tokens": a.tokens, "vocab": a.vocab, "k": a.k, "fraction": a.fraction,
           "corpus": a.corpus, "dtype": a.dtype}
-    detail = {"workload": wl, "minibatches_in_run": steps, "kernels": kernels, "sq_per_dispatch": sq,
+    detail = {"workload": wl, "estep_sources_sha": sha, "minibatches_in_run": steps, "kernels": kernels, "sq_per_dispatch": sq,
               "estep_phase_bytes_per_step": per_step, "estep_kernel": sorted(est),
               "estep_kernel_bytes_per_launch": est_bytes}
     with open(os.path.join(out_dir, f"{a.tag}_pmc.json"), "w") as f:
@@ -117,7 +126,8 @@ def main():
     except (OSError, ValueError):
         entries = []
     entries = [e for e in entries if e.get("workload") != wl]
-    entries.append({"workload": wl, "estep_kernel": sorted(est), "estep_kernel_bytes_per_launch": est_bytes,
+    entries.append({"workload": wl, "tag": a.tag, "estep_sources_sha": sha,
+                    "estep_kernel": sorted(est), "estep_kernel_bytes_per_launch": est_bytes,
                     "estep_phase_bytes_per_step": per_step, "minibatches_in_run": steps,
                     "note": f"{a.tag}: FETCH_SIZE x2 + WRITE_SIZE per launch of the training E-step kernel "
                             f"(and of the whole E-step phase per minibatch), averaged over {steps} minibatches "
