@@ -27,6 +27,7 @@
 // which the LDS array absorbs beside the VALU (MI355X_MICROARCH.md §LDS).
 // Numerics as lda.hip: Bp row-scaled by e^{-m_v}, Spark's 1e-100 carried as ε'_n = 1e-100·e^{-m_v}.
 #include "estep_common.h"
+#include "psi64.h"
 
 #ifndef R64_LOAD_BATCH
 #define R64_LOAD_BATCH 3  // row sets whose B loads are in flight together in the load phase (r03: 2 → 3, −2 %)
@@ -62,97 +63,6 @@ template <int KL>
 using RCommon = RShape<KL, 5, kOnChipSets>;
 template <int KL>
 using RLong = RShape<KL, kMaxSets, kMaxSets>;
-
-// ---- the per-topic ψ/exp chain of the ψ phase, shaped for VALU count: every polynomial in Horner
-// form with its coefficient as the instruction's SGPR operand (a GFX9 VOP3 takes one constant-bus
-// operand), so no constant costs a v_mov pair; branch-free (the shift part is computed for every lane
-// and selected), so the compiler cannot sink it into a divergent branch.  Same Breeze series and
-// truncation fix as stc_internal.h exp_digamma_minus_d; exp() is Cody–Waite + a degree-13 Taylor
-// polynomial in even/odd halves (truncation 4e-18 relative).
-__device__ __forceinline__ double fma_s(double a, double b, double c) {  // a·b + c, c in an SGPR pair
-  double d;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
-  return d;
-}
-__device__ __forceinline__ double fma_sb(double a, double b, double c) {  // a·b + c, b in an SGPR pair
-  double d;
-  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b), "v"(c));
-  return d;
-}
-__device__ __forceinline__ double mul_s(double a, double b) {
-  double d;
-  asm("v_mul_f64 %0, %1, %2" : "=v"(d) : "v"(a), "s"(b));
-  return d;
-}
-__device__ __forceinline__ double add_s(double a, double b) {
-  double d;
-  asm("v_add_f64 %0, %1, %2" : "=v"(d) : "v"(a), "s"(b));
-  return d;
-}
-__device__ __forceinline__ double sub_s(double b, double a) {  // b − a, b in an SGPR pair
-  double d;
-  asm("v_add_f64 %0, -%1, %2" : "=v"(d) : "v"(a), "s"(b));
-  return d;
-}
-// Breeze's truncation term E(y) = f⁹·P(f), f = 1/y² (tools/fit_breeze_digamma.py)
-__device__ __forceinline__ double trunc_f(double f) {
-  double a = add_s(mul_s(f, -12318.55039822477), 2372.137971404805);
-  a = fma_s(a, f, -260.94994774566294);
-  a = fma_s(a, f, 26.284421368293753);
-  a = fma_s(a, f, -3.053401198888146);
-  const double f2 = f * f, f4 = f2 * f2;
-  return ((f4 * f4) * f) * a;
-}
-__device__ __forceinline__ double exp_digamma_minus_s(double x, double cst) {
-  const bool sh = x <= 5.0;
-  const double xs = sh ? x : 1.0;
-  // Σ_{i<6} 1/(xs+i) = p/q, q = xs(xs+1)…(xs+5)
-  double q = fma_s(add_s(xs, 15.0), xs, 85.0);
-  q = fma_s(q, xs, 225.0);
-  q = fma_s(q, xs, 274.0);
-  q = fma_s(q, xs, 120.0) * xs;
-  double p = fma_s(add_s(mul_s(xs, 6.0), 75.0), xs, 340.0);
-  p = fma_s(p, xs, 675.0);
-  p = fma_s(p, xs, 548.0);
-  p = fma_s(p, xs, 120.0);
-  const double iq = rcp_nr(q);
-  double c = p * iq;
-  c = fma(fma(-q, c, p), iq, c);
-  const double y = sh ? add_s(x, 6.0) : x;
-  const double iy = rcp_nr(y);
-  const double f = iy * iy;
-  double t = add_s(mul_s(f, 3617.0 / 8160.0), -1.0 / 12.0);
-  t = fma_s(t, f, 691.0 / 32760.0);
-  t = fma_s(t, f, -1.0 / 132.0);
-  t = fma_s(t, f, 1.0 / 240.0);
-  t = fma_s(t, f, -1.0 / 252.0);
-  t = fma_s(t, f, 1.0 / 120.0);
-  t = fma_s(t, f, -1.0 / 12.0) * f;
-  const double yb = xs + (floor(sub_s(5.0, xs)) + 1.0);  // Breeze's y ∈ (5, 6] (E needs ~1e-4 relative)
-  const double rb = __builtin_amdgcn_rcp(yb);
-  const double fix = trunc_f(f) - trunc_f(rb * rb);
-  const double shift = sh ? fix - c : 0.0;
-  const double z = ((shift - 0.5 * iy) + t) - cst;
-  // exp(z): n = rint(z / ln2), r = z − n·ln2 (hi/lo), e^r = E(r²) + r·O(r²)
-  const double n = __builtin_rint(mul_s(z, 1.4426950408889634));
-  double r = fma_sb(n, -6.93147180369123816490e-01, z);
-  r = fma_sb(n, -1.90821492927058770002e-10, r);
-  const double r2 = r * r;
-  double e = add_s(mul_s(r2, 1.0 / 479001600.0), 1.0 / 3628800.0);
-  e = fma_s(e, r2, 1.0 / 40320.0);
-  e = fma_s(e, r2, 1.0 / 720.0);
-  e = fma_s(e, r2, 1.0 / 24.0);
-  e = fma(e, r2, 0.5);
-  e = fma(e, r2, 1.0);
-  double o = add_s(mul_s(r2, 1.0 / 6227020800.0), 1.0 / 39916800.0);
-  o = fma_s(o, r2, 1.0 / 362880.0);
-  o = fma_s(o, r2, 1.0 / 5040.0);
-  o = fma_s(o, r2, 1.0 / 120.0);
-  o = fma_s(o, r2, 1.0 / 6.0);
-  o = fma(o, r2, 1.0);
-  const double ez = __builtin_ldexp(fma(r, o, e), (int)fmax(n, -1100.0));  // n < -1100: 0
-  return y * ez;
-}
 
 template <class S>
 struct RLds {

@@ -12,3 +12,5 @@ step() {  # step NAME SECONDS CMD...
 }
 step pytest_gpu ${PYTEST_SECS:-900} python -u -m pytest tests -x -v -m gpu --timeout 150 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+# one optional extra step: NAME SECONDS CMD...
+if [ $# -ge 3 ]; then step "$@"; fi

@@ -1,0 +1,154 @@
+// ubench_f64.hip — latency / issue microbenchmarks for the fp64 E-step's building blocks on gfx950
+// (MI355X): dependent and independent v_fma_f64, v_rcp_f64, the ψ/exp chain of the ψ phase
+// (psi64.h exp_digamma_minus_s, stc_internal.h exp_digamma_minus_fast), a dependent ds_read_b128, the
+// fp64 wave reduction, and a 4-wave s_barrier — each with 1, 2 and 3 waves per SIMD (one workgroup
+// of 4·W waves on one CU).  Prints one JSON line per case: cycles per operation per wave (s_memtime
+// around the loop, max over the waves).  Build: make -C tools ubench (hipcc, gfx950).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "psi64.h"
+
+using namespace stc;
+using namespace stc::lda;
+
+constexpr int kN = 256;  // operations per timed loop
+
+__device__ __forceinline__ unsigned long long now() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+enum Op { FMA_DEP, FMA_IND8, RCP_DEP, PSI_S, PSI_S_X2, PSI_FAST, LDS_DEP, WSUM, BARRIER, RCPNR_DEP };
+
+template <int OP>
+__global__ void k_bench(double* out, unsigned long long* cyc, double a, double b) {
+  __shared__ double lds[4096];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 4096; i += blockDim.x) lds[i] = 0.0;
+  __syncthreads();
+  double x = 1.0 + 1e-3 * (tid & 63), y = 2.0 + 1e-3 * (tid & 31);
+  double acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = x + j;
+  int idx = (tid & 63) * 2;
+  unsigned long long t0 = 0, t1 = 0;
+  for (int rep = 0; rep < 2; ++rep) {  // rep 0 warms the instruction cache
+    __syncthreads();
+    t0 = now();
+    if (OP == FMA_DEP) {
+#pragma unroll 16
+      for (int i = 0; i < kN; ++i) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(x) : "v"(a), "v"(b));
+    } else if (OP == FMA_IND8) {
+#pragma unroll 4
+      for (int i = 0; i < kN / 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(acc[j]) : "v"(a), "v"(b));
+    } else if (OP == RCP_DEP) {
+#pragma unroll 16
+      for (int i = 0; i < kN; ++i) asm volatile("v_rcp_f64 %0, %0" : "+v"(x));
+    } else if (OP == RCPNR_DEP) {
+#pragma unroll 8
+      for (int i = 0; i < kN; ++i) {
+        x = rcp_nr(x);
+        asm volatile("" : "+v"(x));
+      }
+    } else if (OP == PSI_S) {
+#pragma unroll 2
+      for (int i = 0; i < kN / 16; ++i) {
+        x = fma(exp_digamma_minus_s(x, a), 0.25, b);
+        asm volatile("" : "+v"(x));
+      }
+    } else if (OP == PSI_S_X2) {
+#pragma unroll 2
+      for (int i = 0; i < kN / 16; ++i) {
+        x = fma(exp_digamma_minus_s(x, a), 0.25, b);
+        y = fma(exp_digamma_minus_s(y, a), 0.25, b);
+        asm volatile("" : "+v"(x), "+v"(y));
+      }
+    } else if (OP == PSI_FAST) {
+#pragma unroll 2
+      for (int i = 0; i < kN / 16; ++i) {
+        x = fma(exp_digamma_minus_fast(x, a), 0.25, b);
+        asm volatile("" : "+v"(x));
+      }
+    } else if (OP == LDS_DEP) {
+#pragma unroll 8
+      for (int i = 0; i < kN; ++i) {
+        const double2 v = *reinterpret_cast<const double2*>(&lds[idx]);
+        idx = (idx + 2 + (int)v.x) & 4095 & ~1;
+      }
+      x += idx;
+    } else if (OP == WSUM) {
+#pragma unroll 4
+      for (int i = 0; i < kN / 8; ++i) {
+        x = wave_sum_d(x) * 1e-2;
+        asm volatile("" : "+v"(x));
+      }
+    } else if (OP == BARRIER) {
+#pragma unroll 8
+      for (int i = 0; i < kN; ++i) __syncthreads();
+    }
+    t1 = now();
+  }
+  double s = x + y;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += acc[j];
+  out[blockIdx.x * blockDim.x + tid] = s;
+  if ((tid & 63) == 0) cyc[blockIdx.x * 64 + (tid >> 6)] = t1 - t0;
+}
+
+// operations per timed loop, for the per-op figure
+static int ops(int op) {
+  switch (op) {
+    case PSI_S: case PSI_FAST: return kN / 16;
+    case PSI_S_X2: return kN / 16;  // pairs
+    case WSUM: return kN / 8;
+    default: return kN;
+  }
+}
+
+template <int OP>
+static void run(const char* name, int waves_per_simd, double* d_out, unsigned long long* d_cyc) {
+  const int threads = 64 * 4 * waves_per_simd;
+  hipLaunchKernelGGL(k_bench<OP>, dim3(1), dim3(threads), 0, 0, d_out, d_cyc, 0.999, 1e-3);
+  if (hipDeviceSynchronize() != hipSuccess) {
+    std::printf("{\"case\": \"%s\", \"error\": \"launch failed\"}\n", name);
+    std::exit(1);
+  }
+  std::vector<unsigned long long> c(64);
+  (void)hipMemcpy(c.data(), d_cyc, 64 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+  unsigned long long mx = 0;
+  for (int w = 0; w < threads / 64; ++w) mx = c[w] > mx ? c[w] : mx;
+  std::printf("{\"case\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_op\": %.2f}\n", name, waves_per_simd,
+              (double)mx / ops(OP));
+}
+
+int main() {
+  double* d_out = nullptr;
+  unsigned long long* d_cyc = nullptr;
+  if (hipMalloc(&d_out, 4096 * sizeof(double)) != hipSuccess || hipMalloc(&d_cyc, 64 * 8) != hipSuccess) {
+    std::printf("{\"error\": \"hipMalloc\"}\n");
+    return 1;
+  }
+  for (int w = 1; w <= 3; ++w) {
+    run<FMA_DEP>("fma_f64_dependent", w, d_out, d_cyc);
+    run<FMA_IND8>("fma_f64_8_independent", w, d_out, d_cyc);
+    run<RCP_DEP>("rcp_f64_dependent", w, d_out, d_cyc);
+    run<RCPNR_DEP>("rcp_nr_dependent", w, d_out, d_cyc);
+    run<PSI_S>("exp_digamma_minus_s_dependent", w, d_out, d_cyc);
+    run<PSI_S_X2>("exp_digamma_minus_s_2_chains", w, d_out, d_cyc);
+    run<PSI_FAST>("exp_digamma_minus_fast_dependent", w, d_out, d_cyc);
+    run<LDS_DEP>("ds_read_b128_dependent", w, d_out, d_cyc);
+    run<WSUM>("wave_sum_d_dependent", w, d_out, d_cyc);
+    run<BARRIER>("s_barrier", w, d_out, d_cyc);
+  }
+  (void)hipFree(d_out);
+  (void)hipFree(d_cyc);
+  return 0;
+}
