@@ -145,12 +145,13 @@ int stc_hash_tokens(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const in
  * Tokenizer result — lower-case, split on each Java \\s character ([ \t\n\x0B\f\r]), interior empty
  * tokens kept, trailing empty tokens dropped, a separator-free string is one token ("" → [""]) —
  * laid out as stc_hashing_tf's input: the separator-free lower-cased blob utf8_out (capacity
- * n_bytes), tok_off_out (capacity n_bytes + n_docs + 1) and doc_off_out[n_docs+1].
+ * n_bytes + n_bytes / 2: lower-casing can grow a 2-byte character to 3 bytes), tok_off_out (capacity
+ * n_bytes + n_docs + 1) and doc_off_out[n_docs+1].
  * Lower-casing is Java 8's String.toLowerCase (root locale, Unicode 6.2) for every code point: the BMP
- * through a generated table, Deseret inline, characters Java 8 does not case passed through.  The 18
- * code points whose mapping is not a same-length 1:1 map (U+0130 İ, U+03A3 Σ's Final_Sigma rule, and
- * capitals whose lower case changes UTF-8 length: U+023A, U+023E, U+1E9E, U+2126, U+212A, U+212B,
- * U+2C62, U+2C64, U+2C6D–U+2C70, U+2C7E, U+2C7F, U+A78D, U+A7AA) fail with STC_ERR_INVALID_ARG.   */
+ * through a generated table, Deseret inline, characters Java 8 does not case passed through, and the 18
+ * code points whose mapping is not a same-length 1:1 map by rule: U+0130 İ → "i̇" (2 → 3 bytes), U+03A3 Σ
+ * → ς / σ by its Final_Sigma context, and the capitals whose lower case changes UTF-8 length (U+023A,
+ * U+023E, U+1E9E, U+2126, U+212A, U+212B, U+2C62, U+2C64, U+2C6D–U+2C70, U+2C7E, U+2C7F, U+A78D, U+A7AA). */
 int stc_tokenize(stc_ctx* ctx, const uint8_t* text, int64_t n_bytes, const int64_t* text_off,
                  int64_t n_docs, uint8_t* utf8_out, int64_t* n_out_bytes, int64_t* tok_off_out,
                  int64_t* n_tok_out, int64_t* doc_off_out);
@@ -273,6 +274,9 @@ int stc_group_member(stc_group* g, int i, stc_lda** lda_out);
 /* the training corpus (rows = documents, values in the group's dtype on device) */
 int stc_group_set_corpus(stc_group* g, int64_t n_rows, int64_t n_cols, const int64_t* indptr,
                          const int32_t* indices, const double* values);
+/* frees the training corpus shards (inference — describe, bound, topicDistribution — needs none;
+ * next / step fail with STC_ERR_STATE until a new stc_group_set_corpus) */
+int stc_group_release_corpus(stc_group* g);
 int stc_group_init_random(stc_group* g, uint64_t seed);
 int stc_group_set_topics(stc_group* g, const double* topics, int layout);
 int stc_group_get_topics(stc_group* g, double* topics_out, int layout);

@@ -271,7 +271,7 @@ JNIEXPORT jlongArray JNICALL FN(tokenize)(JNIEnv* env, jclass c, jlong ctx, jbyt
                                           jbyteArray utf8_out, jlongArray tok_off_out, jlongArray doc_off_out) {
   int64_t nb = 0, nt = 0;
   const int64_t n_bytes = LEN(text), n_docs = LEN(text_off) - 1;
-  if (NEED(utf8_out, n_bytes, "tokenize utf8Out") || NEED(tok_off_out, n_bytes + n_docs + 1, "tokenize tokOffOut") ||
+  if (NEED(utf8_out, n_bytes + n_bytes / 2, "tokenize utf8Out") || NEED(tok_off_out, n_bytes + n_docs + 1, "tokenize tokOffOut") ||
       NEED(doc_off_out, n_docs + 1, "tokenize docOffOut"))
     return NULL;
   jbyte* t = PIN(jbyte, Byte, text);
@@ -626,6 +626,10 @@ JNIEXPORT void JNICALL FN(groupSetCorpus)(JNIEnv* env, jclass c, jlong g, jlong 
 }
 
 JNIEXPORT void JNICALL FN(groupSynchronize)(JNIEnv* env, jclass c, jlong g) { check(env, stc_group_synchronize(GRP(g))); }
+
+JNIEXPORT void JNICALL FN(groupReleaseCorpus)(JNIEnv* env, jclass c, jlong g) {
+  check(env, stc_group_release_corpus(GRP(g)));
+}
 
 JNIEXPORT void JNICALL FN(groupInitRandom)(JNIEnv* env, jclass c, jlong g, jlong seed) {
   check(env, stc_group_init_random(GRP(g), (uint64_t)seed));

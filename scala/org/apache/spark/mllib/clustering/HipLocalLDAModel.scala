@@ -20,7 +20,9 @@ import org.apache.spark.rdd.RDD
  * E-step's convergence tolerance, not bit for bit (DESIGN.md §3).
  *
  * The group handle is transient: a deserialised copy, or one after close(), has none and every method
- * falls back to Spark's CPU implementation.
+ * falls back to Spark's CPU implementation.  A group handle is not thread-safe, so every call on it is
+ * serialised by the model's lock (describeTopics / logLikelihood / topicDistribution may be called from
+ * several threads on a shared model); the finalizer releases the group of a model nobody closed.
  */
 final class HipLocalLDAModel private[clustering] (
     topicsM: Matrix,
@@ -30,23 +32,34 @@ final class HipLocalLDAModel private[clustering] (
     @transient private var group: Long)
   extends LocalLDAModel(topicsM, alphaV, etaV, shape) {
 
+  @transient private lazy val lock = new Object
+
   /** true while the model's λ is resident on the GPU group */
-  def onDevice: Boolean = group != 0L
+  def onDevice: Boolean = lock.synchronized(group != 0L)
 
   /** Releases the GPU group (the model keeps its host copy of λ and falls back to the CPU). */
-  def close(): Unit = {
+  def close(): Unit = lock.synchronized {
     if (group != 0L) StcNative.groupDestroy(group)
     group = 0L
   }
 
-  override def describeTopics(maxTermsPerTopic: Int): Array[(Array[Int], Array[Double])] = {
-    if (group == 0L) return super.describeTopics(maxTermsPerTopic)
-    val n = math.max(0, math.min(maxTermsPerTopic, vocabSize))
-    val idx = new Array[Int](k * n)
-    val w = new Array[Double](k * n)
-    StcNative.groupDescribe(group, maxTermsPerTopic, idx, w)
-    Array.tabulate(k)(t => (idx.slice(t * n, (t + 1) * n), w.slice(t * n, (t + 1) * n)))
+  override protected def finalize(): Unit = {
+    try close() finally super.finalize()
   }
+
+  /** f(group) under the lock, or the CPU fallback when the model holds no group */
+  private def onGroup[T](cpu: => T)(f: Long => T): T = lock.synchronized {
+    if (group == 0L) cpu else f(group)
+  }
+
+  override def describeTopics(maxTermsPerTopic: Int): Array[(Array[Int], Array[Double])] =
+    onGroup(super.describeTopics(maxTermsPerTopic)) { g =>
+      val n = math.max(0, math.min(maxTermsPerTopic, vocabSize))
+      val idx = new Array[Int](k * n)
+      val w = new Array[Double](k * n)
+      StcNative.groupDescribe(g, maxTermsPerTopic, idx, w)
+      Array.tabulate(k)(t => (idx.slice(t * n, (t + 1) * n), w.slice(t * n, (t + 1) * n)))
+    }
 
   private def collectCsr(documents: RDD[(Long, Vector)]): (Array[Long], Array[Vector], Array[AnyRef]) = {
     val docs = documents.collect()
@@ -55,41 +68,41 @@ final class HipLocalLDAModel private[clustering] (
     (docs.map(_._1), rows, StcNative.toCsr(rows))
   }
 
-  /** {bound, corpusPart, topicsPart, tokenCount} of the documents on the GPU */
-  private def deviceBound(documents: RDD[(Long, Vector)]): Array[Double] = {
+  /** {bound, corpusPart, topicsPart, tokenCount} of the documents on the GPU group g */
+  private def deviceBound(g: Long, documents: RDD[(Long, Vector)]): Array[Double] = {
     val (_, rows, csr) = collectCsr(documents)
-    StcNative.groupBound(group, rows.length, vocabSize, csr(0).asInstanceOf[Array[Long]],
+    StcNative.groupBound(g, rows.length, vocabSize, csr(0).asInstanceOf[Array[Long]],
       csr(1).asInstanceOf[Array[Int]], csr(2).asInstanceOf[Array[Double]], getSeed, 0L, null)
   }
 
   override def logLikelihood(documents: RDD[(Long, Vector)]): Double =
-    if (group == 0L) super.logLikelihood(documents) else deviceBound(documents)(0)
+    onGroup(super.logLikelihood(documents))(g => deviceBound(g, documents)(0))
 
-  override def logPerplexity(documents: RDD[(Long, Vector)]): Double = {
-    if (group == 0L) return super.logPerplexity(documents)
-    val r = deviceBound(documents)
-    -r(0) / r(3)
-  }
+  override def logPerplexity(documents: RDD[(Long, Vector)]): Double =
+    onGroup(super.logPerplexity(documents)) { g =>
+      val r = deviceBound(g, documents)
+      -r(0) / r(3)
+    }
 
-  override def topicDistributions(documents: RDD[(Long, Vector)]): RDD[(Long, Vector)] = {
-    if (group == 0L) return super.topicDistributions(documents)
-    val (ids, rows, csr) = collectCsr(documents)
-    val out = new Array[Double](rows.length * k)
-    StcNative.groupTopicDistribution(group, rows.length, vocabSize, csr(0).asInstanceOf[Array[Long]],
-      csr(1).asInstanceOf[Array[Int]], csr(2).asInstanceOf[Array[Double]], getSeed, 0L, null, out)
-    val theta = Array.tabulate(rows.length)(i => (ids(i), Vectors.dense(out.slice(i * k, (i + 1) * k))))
-    documents.sparkContext.parallelize(theta, math.max(1, documents.getNumPartitions))
-  }
+  override def topicDistributions(documents: RDD[(Long, Vector)]): RDD[(Long, Vector)] =
+    onGroup(super.topicDistributions(documents)) { g =>
+      val (ids, rows, csr) = collectCsr(documents)
+      val out = new Array[Double](rows.length * k)
+      StcNative.groupTopicDistribution(g, rows.length, vocabSize, csr(0).asInstanceOf[Array[Long]],
+        csr(1).asInstanceOf[Array[Int]], csr(2).asInstanceOf[Array[Double]], getSeed, 0L, null, out)
+      val theta = Array.tabulate(rows.length)(i => (ids(i), Vectors.dense(out.slice(i * k, (i + 1) * k))))
+      documents.sparkContext.parallelize(theta, math.max(1, documents.getNumPartitions))
+    }
 
-  override def topicDistribution(document: Vector): Vector = {
-    if (group == 0L) return super.topicDistribution(document)
-    require(document.size == vocabSize, s"document of size ${document.size}, the model has $vocabSize terms")
-    val csr = StcNative.toCsr(Array(document))
-    val out = new Array[Double](k)
-    StcNative.groupTopicDistribution(group, 1, vocabSize, csr(0).asInstanceOf[Array[Long]],
-      csr(1).asInstanceOf[Array[Int]], csr(2).asInstanceOf[Array[Double]], getSeed, 0L, null, out)
-    Vectors.dense(out)
-  }
+  override def topicDistribution(document: Vector): Vector =
+    onGroup(super.topicDistribution(document)) { g =>
+      require(document.size == vocabSize, s"document of size ${document.size}, the model has $vocabSize terms")
+      val csr = StcNative.toCsr(Array(document))
+      val out = new Array[Double](k)
+      StcNative.groupTopicDistribution(g, 1, vocabSize, csr(0).asInstanceOf[Array[Long]],
+        csr(1).asInstanceOf[Array[Int]], csr(2).asInstanceOf[Array[Double]], getSeed, 0L, null, out)
+      Vectors.dense(out)
+    }
 }
 
 object HipLocalLDAModel {

@@ -129,7 +129,9 @@ final class HipOnlineLDAOptimizer extends LDAOptimizer {
     val alpha = new Array[Double](k)
     StcNative.groupGetAlpha(group, alpha)
     val eta = StcNative.ldaGetEta(StcNative.groupMember(group, 0))
-    // the model owns the group from here on (HipLocalLDAModel.close releases it)
+    // the model owns the group from here on (HipLocalLDAModel.close or its finalizer releases it); it
+    // infers on the GPUs where λ is, and needs none of the training corpus shards
+    StcNative.groupReleaseCorpus(group)
     val model = new HipLocalLDAModel(Matrices.dense(vocabSize, k, topics), Vectors.dense(alpha), eta, gammaShape,
       group)
     group = 0L

@@ -54,7 +54,8 @@ public final class StcNative {
   public static native long hashingTfTokens(long ctx, long tokens, int numFeatures, boolean binary, int hashVariant,
                                             int valueDtype);
 
-  // ---- Tokenizer (ml.feature.Tokenizer: toLowerCase.split("\\s")); returns {nOutBytes, nTok}
+  // ---- Tokenizer (ml.feature.Tokenizer: toLowerCase.split("\\s")); returns {nOutBytes, nTok}.
+  // utf8Out holds text.length * 3 / 2 bytes (Java lower-cases a few 2-byte characters to 3 bytes)
   public static native long[] tokenize(long ctx, byte[] text, long[] textOff, byte[] utf8Out, long[] tokOffOut,
                                        long[] docOffOut);
   public static native long tokenizeHashingTfDev(long ctx, byte[] text, long[] textOff, int numFeatures,
@@ -126,6 +127,7 @@ public final class StcNative {
   public static native long groupMember(long group, int i);
   public static native void groupSetCorpus(long group, long rows, long cols, long[] indptr, int[] indices,
                                            double[] values);
+  public static native void groupReleaseCorpus(long group);
   public static native void groupInitRandom(long group, long seed);
   public static native void groupSynchronize(long group);
   public static native void groupSetTopics(long group, double[] topics, int layout);

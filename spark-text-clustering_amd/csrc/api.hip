@@ -1356,16 +1356,8 @@ void run_tokenizer(Ctx& c, Tokens& t, const uint8_t* text, int64_t n_bytes, cons
   d_off.reserve(8 * (n_docs + 1));
   if (n_bytes) HIP_CHECK(hipMemcpyAsync(d_text.p, text, n_bytes, hipMemcpyHostToDevice, c.stream));
   HIP_CHECK(hipMemcpyAsync(d_off.p, text_off, 8 * (n_docs + 1), hipMemcpyHostToDevice, c.stream));
-  int64_t bad = -1;
   tokenizer::tokenize(c, d_text.as<uint8_t>(), d_off.as<int64_t>(), n_docs, t.utf8, t.tok_off, t.doc_off,
-                      t.n_tok, t.n_bytes, bad);
-  if (bad >= 0) {
-    char msg[256];
-    snprintf(msg, sizeof msg, "Tokenizer: the GPU lower-casing covers U+0000-U+07FF (except U+0130, U+03A3, "
-             "U+023A, U+023E) and caseless blocks; unsupported character at byte %lld (lead byte 0x%02X)",
-             (long long)bad, (unsigned)text[bad]);
-    throw Error(STC_ERR_INVALID_ARG, msg);
-  }
+                      t.n_tok, t.n_bytes);
 }
 }  // namespace
 
@@ -1417,7 +1409,8 @@ int stc_idf_fit(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, double* 
     STC_REQUIRE(min_doc_freq >= 0, "minDocFreq must be >= 0");
     ctx->use();
     hipStream_t s = ctx->stream;
-    DevBuf df, idf;
+    DevBuf& df = ctx->scratch[9];  // grow-only on the context: no per-call allocation
+    DevBuf& idf = ctx->scratch[10];
     df.reserve(8 * tf->cols);
     idf.reserve(8 * tf->cols);
     idf::doc_freq(*ctx, *tf, df.as<int64_t>());
@@ -1447,7 +1440,7 @@ int stc_idf_transform(stc_ctx* ctx, stc_dcsr* tf, const double* idf, double zero
     STC_REQUIRE(tf->ctx == ctx, "the matrix belongs to another stc_ctx");
     STC_REQUIRE(zero_floor >= 0.0, "zero_floor must be >= 0");
     ctx->use();
-    DevBuf d;
+    DevBuf& d = ctx->scratch[11];
     d.reserve(8 * tf->cols);
     HIP_CHECK(hipMemcpyAsync(d.p, idf, 8 * tf->cols, hipMemcpyHostToDevice, ctx->stream));
     idf::transform(*ctx, *tf, d.as<double>(), zero_floor);
@@ -2044,6 +2037,24 @@ int stc_group_set_corpus(stc_group* g, int64_t n_rows, int64_t n_cols, const int
     g->row0 = r0;
     g->rows = n_rows;
     g->cols = n_cols;
+  });
+}
+
+int stc_group_release_corpus(stc_group* g) {
+  return guard([&] {
+    STC_REQUIRE(g, "group");
+    for (int i = 0; i < g->n(); ++i) {
+      stc_lda* l = g->lda[(size_t)i];
+      g->ctx[(size_t)i]->use();
+      settle_side(*l);
+      HIP_CHECK(hipStreamSynchronize(g->ctx[(size_t)i]->stream));
+      l->corpus = nullptr;
+      l->order_for = nullptr;
+      l->pre_valid = false;
+    }
+    for (auto* d : g->shard) (void)stc_dcsr_free(d);
+    g->shard.clear();
+    g->rows = 0;
   });
 }
 

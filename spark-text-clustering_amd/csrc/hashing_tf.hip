@@ -5,11 +5,10 @@
 // the reference's vocab-indexed counting slot LDAClustering.scala:154-167.  Bit-exact.
 //
 // Layout: the corpus arrives as ONE UTF-8 byte blob + int64 token offsets + int64 doc offsets
-// (plain arrays a JNI caller can hand over without per-string objects).  K1 is one lane per token
-// (byte-wise reads: tokens are 1–20 bytes, the blob is read once, HBM-bound).  K2 sorts each
-// document's bucket ids inside one wave (registers; hipcub's segmented sort only for documents past
-// 1024 tokens) and emits the sorted distinct ids + run lengths — no atomics on the CSR, so hot terms
-// ("the") cost nothing extra.
+// (plain arrays a JNI caller can hand over without per-string objects).  One wave per document hashes
+// its tokens (K1, aligned dword reads) straight into registers and sorts them there (K2 pass A; hipcub's
+// segmented sort only for documents past 1024 tokens, hashed to memory first); pass B emits the sorted
+// distinct ids + run lengths — no atomics on the CSR, so hot terms ("the") cost nothing extra.
 #include <hipcub/hipcub.hpp>
 
 #include "stc_internal.h"
@@ -116,11 +115,11 @@ void hash_tokens(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_
 
 // ---------------------------------------------------------------------------------------
 // K2: per-document sort + run-length count → CSR.  One wave per document.
-//  pass A (k_doc_sort): documents of ≤ kSortCap tokens are bitonic-sorted in registers (P = m/64
-//    keys per lane, m = the next power of two ≥ max(n, 64); partners j ≥ P across lanes by
-//    __shfl_xor, j < P inside the lane), written back sorted, and their distinct ids counted
-//    (ballot popcounts) into nnz[d].  Longer documents are appended to a list for the segmented
-//    radix sort (hipcub), then counted by k_doc_runs<COUNT>.
+//  pass A (k_doc_hash_sort, then k_doc_sort for 257–1024 tokens): documents of ≤ kSortCap tokens are
+//    bitonic-sorted in registers (≤ 256 tokens hashed straight into them) (P = m/64 keys per lane, m = the next power of two ≥ max(n, 64); partners
+//    j ≥ P across lanes by __shfl_xor, j < P inside the lane), written back sorted, and their distinct
+//    ids counted into nnz[d].  Longer documents are hashed to memory and appended to a list for the
+//    segmented radix sort (hipcub), then counted by k_doc_runs<COUNT>.
 //  scan nnz → indptr; pass B (k_doc_runs<EMIT>): each document's sorted keys in 64-key chunks; run
 //    heads by ballot, output slots by mbcnt, run lengths from the next head in the chunk, or, for a
 //    chunk's last run, when the next chunk's first head (or the document end) arrives.
@@ -188,27 +187,100 @@ __device__ __forceinline__ int64_t sort_doc(const int32_t* __restrict__ keys, in
 }
 
 constexpr int kDocWaves = 4;  // documents in flight per workgroup (one per wave)
+constexpr int kFusedCap = 256;  // documents up to this many tokens are hashed and sorted in one pass
 
-__global__ __launch_bounds__(64 * kDocWaves) void k_doc_sort(const int32_t* __restrict__ keys,
-                                                            const int64_t* __restrict__ doc_off, int64_t n_docs,
-                                                            int32_t* __restrict__ sorted, int64_t* __restrict__ nnz,
-                                                            int32_t* __restrict__ large,
-                                                            int32_t* __restrict__ n_large) {
+// K1 fused into K2's pass A: the document's bucket ids never round-trip through HBM.  Token p·64 + lane
+// of the document goes to register p of the lane (coalesced offset and byte loads; the bitonic network
+// sorts any starting order), is hashed there, and the P registers are sorted and their distinct ids
+// counted exactly as sort_doc does.
+template <bool SPARK24, int P>
+__device__ __forceinline__ int64_t hash_sort_doc(const uint8_t* __restrict__ utf8, const int64_t* __restrict__ tok_off,
+                                                 int64_t s, int n, int32_t nf, int32_t* __restrict__ sorted,
+                                                 int lane) {
+  int32_t x[P];
+  int64_t b[P], e[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int q = p * 64 + lane;
+    b[p] = q < n ? tok_off[s + q] : 0;
+    e[p] = q < n ? tok_off[s + q + 1] : 0;
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int q = p * 64 + lane;
+    if (q < n) {
+      const int32_t raw = murmur3<SPARK24>(utf8 + b[p], (uint32_t)(e[p] - b[p])) % nf;  // Utils.nonNegativeMod
+      x[p] = raw + (raw < 0 ? nf : 0);
+    } else {
+      x[p] = INT32_MAX;  // pads sort last
+    }
+  }
+  bitonic_regs<P>(x, lane);
+  const int32_t prev_last = __shfl_up(x[P - 1], 1, 64);
+  int heads = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int q = lane * P + p;
+    if (q < n) {
+      sorted[s + q] = x[p];
+      const int32_t prev = p == 0 ? prev_last : x[p - 1];
+      heads += (q == 0 || x[p] != prev) ? 1 : 0;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) heads += __shfl_xor(heads, o, 64);
+  return heads;
+}
+
+// one wave per document: ≤ kFusedCap tokens hashed, sorted and counted in registers (nnz[d]); longer
+// documents hashed into `keys` — ≤ kSortCap tokens for k_doc_sort (counted in *n_medium), the rest for the
+// segmented radix sort (appended to `large`).  Capping the fused path at 4 keys per lane keeps the kernel
+// at ~50 VGPRs: the hashing's dependent offset → byte loads need the occupancy (the P = 16 form held 132).
+template <bool SPARK24>
+__global__ __launch_bounds__(64 * kDocWaves) void k_doc_hash_sort(const uint8_t* __restrict__ utf8,
+                                                                 const int64_t* __restrict__ tok_off,
+                                                                 const int64_t* __restrict__ doc_off, int64_t n_docs,
+                                                                 int32_t nf, int32_t* __restrict__ keys,
+                                                                 int32_t* __restrict__ sorted,
+                                                                 int64_t* __restrict__ nnz, int32_t* __restrict__ large,
+                                                                 int32_t* __restrict__ n_large,
+                                                                 int32_t* __restrict__ n_medium) {
   const int lane = threadIdx.x & 63;
   for (int64_t d = (int64_t)blockIdx.x * kDocWaves + (threadIdx.x >> 6); d < n_docs;
        d += (int64_t)gridDim.x * kDocWaves) {
     const int64_t s = doc_off[d], n64 = doc_off[d + 1] - s;
-    if (n64 > kSortCap) {
-      if (lane == 0) large[atomicAdd(n_large, 1)] = (int32_t)d;
+    if (n64 > kFusedCap) {
+      for (int64_t q = lane; q < n64; q += 64) {
+        const int64_t t = s + q;
+        const int32_t raw = murmur3<SPARK24>(utf8 + tok_off[t], (uint32_t)(tok_off[t + 1] - tok_off[t])) % nf;
+        keys[t] = raw + (raw < 0 ? nf : 0);
+      }
+      if (lane == 0) {
+        if (n64 > kSortCap) large[atomicAdd(n_large, 1)] = (int32_t)d;
+        else atomicAdd(n_medium, 1);
+      }
       continue;
     }
     const int n = (int)n64;
     int64_t h = 0;
-    if (n <= 64) h = sort_doc<1>(keys, sorted, s, n, lane);
-    else if (n <= 128) h = sort_doc<2>(keys, sorted, s, n, lane);
-    else if (n <= 256) h = sort_doc<4>(keys, sorted, s, n, lane);
-    else if (n <= 512) h = sort_doc<8>(keys, sorted, s, n, lane);
-    else h = sort_doc<16>(keys, sorted, s, n, lane);
+    if (n <= 64) h = hash_sort_doc<SPARK24, 1>(utf8, tok_off, s, n, nf, sorted, lane);
+    else if (n <= 128) h = hash_sort_doc<SPARK24, 2>(utf8, tok_off, s, n, nf, sorted, lane);
+    else h = hash_sort_doc<SPARK24, 4>(utf8, tok_off, s, n, nf, sorted, lane);
+    if (lane == 0) nnz[d] = h;
+  }
+}
+
+// the documents of kFusedCap < n ≤ kSortCap tokens, hashed by k_doc_hash_sort: sorted in registers from
+// `keys` (8 or 16 keys per lane) and counted
+__global__ __launch_bounds__(64 * kDocWaves) void k_doc_sort(const int32_t* __restrict__ keys,
+                                                            const int64_t* __restrict__ doc_off, int64_t n_docs,
+                                                            int32_t* __restrict__ sorted, int64_t* __restrict__ nnz) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t d = (int64_t)blockIdx.x * kDocWaves + (threadIdx.x >> 6); d < n_docs;
+       d += (int64_t)gridDim.x * kDocWaves) {
+    const int64_t s = doc_off[d], n64 = doc_off[d + 1] - s;
+    if (n64 <= kFusedCap || n64 > kSortCap) continue;
+    const int n = (int)n64;
+    const int64_t h = n <= 512 ? sort_doc<8>(keys, sorted, s, n, lane) : sort_doc<16>(keys, sorted, s, n, lane);
     if (lane == 0) nnz[d] = h;
   }
 }
@@ -355,27 +427,43 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
     out.nnz = 0;
     return;
   }
-  // grow-only scratch kept on the context (the featurisation of one corpus reuses it)
+  // grow-only scratch kept on the context (the featurisation of one corpus reuses it): no allocation,
+  // and so no implicit device synchronisation of hipFree, per call
   DevBuf& keys = c.scratch[0];
   DevBuf& sorted = c.scratch[1];
   DevBuf& nnz = c.scratch[2];
   DevBuf& small = c.scratch[3];
-  keys.reserve(sizeof(int32_t) * n_tok);
-  sorted.reserve(sizeof(int32_t) * n_tok);
+  DevBuf& stmp = c.scratch[4];
   nnz.reserve(sizeof(int64_t) * (n_docs + 1));
   small.reserve(sizeof(int32_t) * (n_docs + 16));
-  int32_t* n_large_d = small.as<int32_t>();
+  sorted.reserve(sizeof(int32_t) * n_tok);
+  int32_t* n_large_d = small.as<int32_t>();  // word 0: long documents, word 1: medium ones
   int32_t* large = small.as<int32_t>() + 16;
-  hash_tokens(c, d_utf8, d_tok_off, n_tok, num_features, variant, keys.as<int32_t>());
-  HIP_CHECK(hipMemsetAsync(n_large_d, 0, sizeof(int32_t), st));
+  HIP_CHECK(hipMemsetAsync(n_large_d, 0, 2 * sizeof(int32_t), st));
   const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(ceil_div(n_docs, kDocWaves), 1), 1 << 14);
-  k_doc_sort<<<g, 64 * kDocWaves, 0, st>>>(keys.as<int32_t>(), d_doc_off, n_docs, sorted.as<int32_t>(),
-                               nnz.as<int64_t>() + 1, large, n_large_d);
+  keys.reserve(sizeof(int32_t) * n_tok);  // the long documents' bucket ids, at their token positions
+  if (variant == STC_HASH_SPARK24)
+    k_doc_hash_sort<true><<<g, 64 * kDocWaves, 0, st>>>(d_utf8, d_tok_off, d_doc_off, n_docs, num_features,
+                                                        keys.as<int32_t>(), sorted.as<int32_t>(), nnz.as<int64_t>() + 1,
+                                                        large, n_large_d, n_large_d + 1);
+  else
+    k_doc_hash_sort<false><<<g, 64 * kDocWaves, 0, st>>>(d_utf8, d_tok_off, d_doc_off, n_docs, num_features,
+                                                         keys.as<int32_t>(), sorted.as<int32_t>(), nnz.as<int64_t>() + 1,
+                                                         large, n_large_d, n_large_d + 1);
   KERNEL_CHECK();
-  int32_t n_large = 0;
-  HIP_CHECK(hipMemcpyAsync(&n_large, n_large_d, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  int32_t counts[2] = {0, 0};
+  HIP_CHECK(hipMemcpyAsync(counts, n_large_d, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
-  DevBuf sorted_l, seg, flags, tmp;
+  const int32_t n_large = counts[0];
+  if (counts[1] > 0) {
+    k_doc_sort<<<g, 64 * kDocWaves, 0, st>>>(keys.as<int32_t>(), d_doc_off, n_docs, sorted.as<int32_t>(),
+                                             nnz.as<int64_t>() + 1);
+    KERNEL_CHECK();
+  }
+  DevBuf& sorted_l = c.scratch[5];
+  DevBuf& seg = c.scratch[6];
+  DevBuf& flags = c.scratch[7];
+  DevBuf& tmp = c.scratch[8];
   if (n_large > 0) {  // long documents: hipcub segmented radix sort, then their run counts
     sorted_l.reserve(sizeof(int32_t) * n_tok);
     seg.reserve(sizeof(int64_t) * 2 * n_large);
@@ -404,7 +492,6 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
   size_t sb = 0;
   HIP_CHECK(hipcub::DeviceScan::InclusiveSum(nullptr, sb, nnz.as<int64_t>() + 1, out.indptr.as<int64_t>() + 1,
                                              (int)n_docs, st));
-  DevBuf stmp;
   stmp.reserve(sb);
   HIP_CHECK(hipcub::DeviceScan::InclusiveSum(stmp.p, sb, nnz.as<int64_t>() + 1, out.indptr.as<int64_t>() + 1,
                                              (int)n_docs, st));
@@ -412,6 +499,7 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
   HIP_CHECK(hipMemcpyAsync(&total, out.indptr.as<int64_t>() + n_docs, sizeof(int64_t), hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
   out.nnz = total;
+  out.positive = true;  // counts ≥ 1 (binary: 1)
   out.indices.reserve(sizeof(int32_t) * std::max<int64_t>(total, 1));
   out.values.reserve((value_dtype == STC_F32 ? 4 : 8) * std::max<int64_t>(total, 1));
   const uint8_t* fl = n_large > 0 ? flags.as<uint8_t>() : nullptr;
@@ -424,7 +512,6 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
                                                d_doc_off, n_docs, out.indptr.as<int64_t>(), binary,
                                                out.indices.as<int32_t>(), out.values.as<double>(), nullptr);
   KERNEL_CHECK();
-  if (n_large > 0) HIP_CHECK(hipStreamSynchronize(st));  // the long-document buffers die at scope exit
 }
 
 }  // namespace hashing

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kBinThreads) void k_df_bin(const int32_t* __restric
   for (int u = 0; u < kBinPer; ++u) {
     const int64_t e = e0 + u * kBinThreads + tid;
     uint32_t x = ~0u;
-    if (e < nnz && val[e] > V(0)) {
+    if (e < nnz && (val == nullptr || val[e] > V(0))) {  // val = nullptr: every value is known > 0
       const uint32_t id = (uint32_t)idx[e];
       x = ((id >> kTileBits) << 16) | (id & (kTile - 1));
     }
@@ -179,14 +179,17 @@ void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df) {
     bins.reserve(sizeof(uint16_t) * chunks * kBinChunk);
     tab.reserve(sizeof(int32_t) * chunks * 2 * kMaxTiles);
     part.reserve(sizeof(uint32_t) * groups * m.cols);
+    // a CSR whose values are all known > 0 (HashingTF output) is counted from its indices alone
     auto bin = [&](auto mt) {
       constexpr int MT = decltype(mt)::value;
       if (m.dtype == STC_F32)
-        k_df_bin<float, MT><<<(unsigned)chunks, kBinThreads, 0, s>>>(m.indices.as<int32_t>(), m.values.as<float>(),
-                                                                     m.nnz, T, bins.as<uint16_t>(), tab.as<int32_t>());
+        k_df_bin<float, MT><<<(unsigned)chunks, kBinThreads, 0, s>>>(
+            m.indices.as<int32_t>(), m.positive ? nullptr : m.values.as<float>(), m.nnz, T, bins.as<uint16_t>(),
+            tab.as<int32_t>());
       else
-        k_df_bin<double, MT><<<(unsigned)chunks, kBinThreads, 0, s>>>(m.indices.as<int32_t>(), m.values.as<double>(),
-                                                                      m.nnz, T, bins.as<uint16_t>(), tab.as<int32_t>());
+        k_df_bin<double, MT><<<(unsigned)chunks, kBinThreads, 0, s>>>(
+            m.indices.as<int32_t>(), m.positive ? nullptr : m.values.as<double>(), m.nnz, T, bins.as<uint16_t>(),
+            tab.as<int32_t>());
     };
     bin(std::integral_constant<int, kMaxTiles>{});
     KERNEL_CHECK();
@@ -267,6 +270,8 @@ __global__ __launch_bounds__(256) void k_transform(const int32_t* __restrict__ i
 }
 
 void transform(Ctx& c, DCsr& m, const double* d_idf, double zero_floor) {
+  // idf ≥ 0: values stay > 0 only when an idf of 0 is floored (the reference's 1e-4 mode)
+  m.positive = m.positive && zero_floor > 0.0;
   if (m.nnz == 0) return;
   const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(ceil_div(m.nnz / 4, 256), 1), 8192);
   if (m.dtype == STC_F32)

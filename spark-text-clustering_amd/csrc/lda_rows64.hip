@@ -35,6 +35,12 @@
 #ifndef R64_PRIO
 #define R64_PRIO 2  // wave priority raised over the latency-critical phases (1: ψ; 2: ψ + r): −2 % E-step (r03)
 #endif
+#ifndef R64_PSI_V2
+#define R64_PSI_V2 1  // the ψ phase's chain: psi64.h exp_digamma_minus_v2 (0: the round-3 form)
+#endif
+#ifndef R64_RCP_NR
+#define R64_RCP_NR 2  // Newton steps after v_rcp_f64 in that chain
+#endif
 #ifndef R64_LONG_OCC
 #define R64_LONG_OCC 1  // long-document kernel workgroups per CU the register budget is cut for
 #endif
@@ -63,6 +69,14 @@ template <int KL>
 using RCommon = RShape<KL, 5, kOnChipSets>;
 template <int KL>
 using RLong = RShape<KL, kMaxSets, kMaxSets>;
+
+__device__ __forceinline__ double exp_digamma_minus_r64(double x, double cst) {
+#if R64_PSI_V2
+  return exp_digamma_minus_v2<R64_RCP_NR>(x, cst);
+#else
+  return exp_digamma_minus_s(x, cst);
+#endif
+}
 
 template <class S>
 struct RLds {
@@ -119,7 +133,9 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
   const int tid = rows64_tid<RES>(d);
   constexpr int KL = S::KL, KLP = S::KLP;
   const int k = a.k, kp = a.kp;
-  const int lane = tid & 63, w = tid >> 6;
+  // the wave index is wave-uniform: held in an SGPR, every per-wave role test (ψ wave, worker sets) is
+  // scalar instead of a v_cmp / v_cndmask chain per iteration
+  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   d.lane = lane;
   d.w = w;
   d.tl = lane & 7;
@@ -209,7 +225,7 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
   // eθ' = exp(ψ(γ) − ψ(Σγ) − ψc_t): Spark's exp(E[log θ]) times expElogβ's per-topic factor
   {
     const double cs0 = digamma_fast_d(gsum0);
-    if (w < npsi && d.town) sm.eth[d.ttl][d.ttp] = exp_digamma_minus_s(g0, cs0 + pc);
+    if (w < npsi && d.town) sm.eth[d.ttl][d.ttp] = exp_digamma_minus_r64(g0, cs0 + pc);
     if (tid == 0) sm.cs = cs0;
   }
   return true;  // (the block loads' barrier publishes eθ)
@@ -380,7 +396,7 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
         const double gn = fma(eo, s, ap.x);  // γ ← eθ ⊙ s + α
         dg = fabs(gn - g);
         sm.gam[tt] = gn;
-        sm.eth[ttl][ttp] = exp_digamma_minus_s(gn, csn + ap.y);
+        sm.eth[ttl][ttp] = exp_digamma_minus_r64(gn, csn + ap.y);
         if (tt == 0) sm.cs = csn;
       }
       const double d = wave_sum_d(dg);

@@ -99,7 +99,79 @@ __device__ __forceinline__ double exp_digamma_minus_s(double x, double cst) {
   return y * ez;
 }
 
+
+// ---- round-4 form (exp_digamma_minus_v2): the same Breeze ψ and exp, fewer fp64 instructions.
+//  * Breeze's truncation fix E(x + 6) − E(y_B) (≤ 8e-13, needs ~1e-5 relative) in ONE packed-fp32
+//    stream for both arguments (v_pk_fma_f32 / v_pk_mul_f32): 1.1e-18 absolute against the fp64 form;
+//    Breeze's shift count ⌊5 − x⌋ + 1 stays fp64 (exact), only y_B's value is rounded to fp32.
+//  * the six recurrence terms as (2x+5)·(3u² + 20u + 24) / (u(u+4)(u+6)), u = x(x+5): the pairs
+//    1/(x+i) + 1/(x+5−i) share the numerator 2x+5 (two instructions and one level shorter than p/q).
+//  * RCP_STEPS Newton steps after v_rcp_f64 (tools/ubench_f64 measures the raw reciprocal's error).
+typedef float pkf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double trunc_fix_pk(double f6, double xs) {
+  const double nb = floor(sub_s(5.0, xs)) + 1.0;  // Breeze's shift count (exact)
+  const float rb = __builtin_amdgcn_rcpf((float)xs + (float)nb);
+  const pkf2 u = {(float)f6, rb * rb};
+  pkf2 a = u * (pkf2)(-12318.55039822477f) + (pkf2)(2372.137971404805f);
+  a = a * u + (pkf2)(-260.94994774566294f);
+  a = a * u + (pkf2)(26.284421368293753f);
+  a = a * u + (pkf2)(-3.053401198888146f);
+  const pkf2 u2 = u * u, u4 = u2 * u2, u8 = u4 * u4;
+  const pkf2 e = (u8 * u) * a;
+  return (double)(e.x - e.y);
+}
+template <int RCP_STEPS>
+__device__ __forceinline__ double rcp_n(double q) {
+  double r = __builtin_amdgcn_rcp(q);
+#pragma unroll
+  for (int i = 0; i < RCP_STEPS; ++i) r = fma(r, fma(-q, r, 1.0), r);
+  return r;
+}
+template <int RCP_STEPS>
+__device__ __forceinline__ double exp_digamma_minus_v2(double x, double cst) {
+  const bool sh = x <= 5.0;
+  const double xs = sh ? x : 1.0;
+  // Σ_{i<6} 1/(xs+i) = num/den
+  const double u = xs * add_s(xs, 5.0);
+  const double num = fma_s(add_s(mul_s(u, 3.0), 20.0), u, 24.0) * fma(xs, 2.0, 5.0);
+  const double den = u * fma_s(add_s(u, 10.0), u, 24.0);
+  const double iq = rcp_n<RCP_STEPS>(den);
+  double c = num * iq;
+  c = fma(fma(-den, c, num), iq, c);
+  const double y = sh ? add_s(x, 6.0) : x;
+  const double iy = rcp_n<RCP_STEPS>(y);
+  const double f = iy * iy;
+  double t = add_s(mul_s(f, 3617.0 / 8160.0), -1.0 / 12.0);
+  t = fma_s(t, f, 691.0 / 32760.0);
+  t = fma_s(t, f, -1.0 / 132.0);
+  t = fma_s(t, f, 1.0 / 240.0);
+  t = fma_s(t, f, -1.0 / 252.0);
+  t = fma_s(t, f, 1.0 / 120.0);
+  t = fma_s(t, f, -1.0 / 12.0) * f;
+  const double shift = sh ? trunc_fix_pk(f, xs) - c : 0.0;
+  const double z = (fma(-0.5, iy, shift) + t) - cst;
+  const double n = __builtin_rint(mul_s(z, 1.4426950408889634));
+  double r = fma_sb(n, -6.93147180369123816490e-01, z);
+  r = fma_sb(n, -1.90821492927058770002e-10, r);
+  const double r2 = r * r;
+  double e = add_s(mul_s(r2, 1.0 / 479001600.0), 1.0 / 3628800.0);
+  e = fma_s(e, r2, 1.0 / 40320.0);
+  e = fma_s(e, r2, 1.0 / 720.0);
+  e = fma_s(e, r2, 1.0 / 24.0);
+  e = fma(e, r2, 0.5);
+  e = fma(e, r2, 1.0);
+  double o = add_s(mul_s(r2, 1.0 / 6227020800.0), 1.0 / 39916800.0);
+  o = fma_s(o, r2, 1.0 / 362880.0);
+  o = fma_s(o, r2, 1.0 / 5040.0);
+  o = fma_s(o, r2, 1.0 / 120.0);
+  o = fma_s(o, r2, 1.0 / 6.0);
+  o = fma(o, r2, 1.0);
+  const double ez = __builtin_ldexp(fma(r, o, e), (int)fmax(n, -1100.0));  // n < -1100: 0
+  return y * ez;
+}
+
 }  // namespace psi64
 using psi64::exp_digamma_minus_s;
+using psi64::exp_digamma_minus_v2;
 }  // namespace lda
 }  // namespace stc

@@ -105,7 +105,7 @@ struct Ctx {
   LocalColl* local = nullptr;  // set instead of comm for same-device group members (owned by the group)
   int n_ranks = 1;
   int rank = 0;
-  DevBuf scratch[4];  // grow-only scratch of the featurisation kernels (hashing_tf.hip)
+  DevBuf scratch[12];  // grow-only scratch of the featurisation kernels (hashing_tf.hip, idf.hip, api.hip IDF)
   DevBuf coll_tmp;    // the in-process all-reduce's staging buffer
   void use() const { HIP_CHECK(hipSetDevice(device)); }
   bool coll() const { return comm != nullptr || local != nullptr; }
@@ -117,6 +117,9 @@ struct DCsr {
   int64_t rows = 0, cols = 0, nnz = 0;
   int64_t max_row = -1;  // longest row's nnz when known (host uploads), −1 otherwise
   int dtype = STC_F64;
+  // every value is > 0 (a HashingTF output: counts / binary 1; kept by a floored IDF transform), so a
+  // df count needs only the indices (cleared by anything that may write a value ≤ 0)
+  bool positive = false;
   DevBuf indptr;   // int64[rows+1]
   DevBuf indices;  // int32[nnz]
   DevBuf values;   // float/double[nnz]
@@ -482,11 +485,11 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
 }  // namespace hashing
 namespace tokenizer {
 // Spark ML Tokenizer on device: d_text/d_text_off (n_docs+1) in; lower-cased, separator-free blob,
-// token offsets (n_tok+1) and per-document token offsets (n_docs+1) out.  bad_pos >= 0 reports the
-// first byte whose character the kernel cannot lower-case (outputs then unset).
+// token offsets (n_tok+1) and per-document token offsets (n_docs+1) out (the blob may be up to half
+// as long again as the input: Java 8 lower-cases a few 2-byte characters to 3 bytes).
 void tokenize(Ctx& c, const uint8_t* d_text, const int64_t* d_text_off, int64_t n_docs,
               DevBuf& out_utf8, DevBuf& out_tok_off, DevBuf& out_doc_off, int64_t& n_tok,
-              int64_t& n_out_bytes, int64_t& bad_pos);
+              int64_t& n_out_bytes);
 }  // namespace tokenizer
 namespace idf {
 void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df /* cols */);

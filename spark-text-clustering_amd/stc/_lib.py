@@ -123,6 +123,7 @@ SIGNATURES = {
     "stc_group_get_alpha": (_int, [_p, _pdbl]),
     "stc_group_get_iteration": (_int, [_p, _pi64]),
     "stc_group_synchronize": (_int, [_p]),
+    "stc_group_release_corpus": (_int, [_p]),
     "stc_group_next": (_int, [_p, C.POINTER(StepStats)]),
     "stc_group_step": (_int, [_p, _pi64, _i64, _pdbl, C.POINTER(StepStats)]),
     "stc_group_describe": (_int, [_p, _i32, _pi32, _pdbl]),

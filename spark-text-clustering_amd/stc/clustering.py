@@ -254,6 +254,10 @@ class LdaGroup:
         L.check(self.lib.stc_group_get_iteration(self.handle, C.byref(x)))
         return x.value
 
+    def release_corpus(self):
+        """frees the training corpus shards (inference needs none; stc_group_release_corpus)"""
+        L.check(self.lib.stc_group_release_corpus(self.handle))
+
     def synchronize(self):
         """waits for every member's queued work (stc_group_synchronize)"""
         L.check(self.lib.stc_group_synchronize(self.handle))

@@ -90,7 +90,7 @@ class Tokenizer:
         """Tokens of every doc in HashingTF's input layout: (utf8 blob, tok_off, doc_off)."""
         text, off = encode_texts(texts)
         n_docs = off.size - 1
-        blob = np.zeros(max(text.size, 1), np.uint8)
+        blob = np.zeros(max(text.size + text.size // 2, 1), np.uint8)  # lower-casing may grow text by half (İ → "i̇")
         tok_off = np.zeros(text.size + n_docs + 1, np.int64)
         doc_off = np.zeros(n_docs + 1, np.int64)
         nb, nt = C.c_int64(), C.c_int64()

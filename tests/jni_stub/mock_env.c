@@ -94,9 +94,9 @@ int main(void) {
     jlongArray toff = arr(2, 8);
     jlong t2[2] = {0, 5};
     memcpy(toff->data, t2, sizeof t2);
-    FN(tokenize)(env, NULL, 0, text, toff, arr(5, 1), arr(6, 8), arr(2, 8));
+    FN(tokenize)(env, NULL, 0, text, toff, arr(7, 1), arr(6, 8), arr(2, 8));
     report("tokenize_short_tokoff");
-    FN(tokenize)(env, NULL, 0, text, toff, arr(4, 1), arr(7, 8), arr(2, 8));
+    FN(tokenize)(env, NULL, 0, text, toff, arr(6, 1), arr(7, 8), arr(2, 8));
     report("tokenize_short_utf8");
   }
   {

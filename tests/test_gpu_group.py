@@ -182,7 +182,14 @@ def test_failed_set_corpus_leaves_every_member_on_its_shard(ctx, monkeypatch):
             cs = g.counters()
             assert len(cs) == 2 and sum(c["docs"] for c in cs) > 0
             assert all(p["estep"] >= 0.0 for p in g.phase_times())
-            return g.topics(), g.alpha()
+            t, a = g.topics(), g.alpha()
+            # the model handed to inference drops its corpus shards: describe still works, training does not
+            g.release_corpus()
+            idx, _ = g.describe(5)
+            assert idx.shape == (k, 5)
+            with pytest.raises(stc.StcError, match="corpus"):
+                g.next(stats=False)
+            return t, a
 
     t0, a0 = run(False)
     t1, a1 = run(True)

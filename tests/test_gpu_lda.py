@@ -98,6 +98,34 @@ def test_estep_gamma_and_stat(ctx, oracle, dtype, k, kernel, monkeypatch):
         assert rel.max() < 1e-2, rel.max()
 
 
+@pytest.mark.parametrize("k,scale", [(100, 5e4), (100, 5e5), (300, 5e5)])
+def test_estep_fp32_at_production_scale_lambda(ctx, oracle, k, scale):
+    """the fp32 E-step carries expElogβ's per-topic factor exp(−ψ(colsum_t)) in eθ', so a λ of
+    a large corpus (colsum 1e8–1e9 here: λ scaled by 5e4–5e5 over V = 2048) scales eθ' and φ down by
+    that much.  γ still matches the fp64 oracle within the fp32 bounds of test_estep_gamma_and_stat."""
+    rng = np.random.default_rng(70 + k)
+    D, V = 40, 2048
+    corpus = random_corpus(rng, D, V, 1, 300, empty_every=11)
+    lam = rng.gamma(100.0, 0.01, size=(V, k)) * scale * rng.uniform(0.5, 2.0, size=(V, 1))
+    assert lam.sum(axis=0).min() > 1e8 * (scale / 5e5)
+    g0 = rng.gamma(100.0, 0.01, size=(D, k))
+    h, _ = _handle(ctx, corpus, k, "f32", lam)
+    gamma, _, iters = h.estep(np.arange(D), g0)
+    eeb = oracle.topics_exp_elog_beta(lam)
+    alpha = np.full(k, 1.0 / k)
+    for i in range(D):
+        cid, cts = corpus.row(i)
+        if cid.size == 0:
+            continue
+        g, _, it = oracle.variational_topic_inference(cid, cts, eeb, alpha, g0[i])
+        assert abs(int(iters[i]) - it) <= 3, (i, iters[i], it)
+        if iters[i] != it:
+            g, _, _ = oracle.variational_topic_inference(cid, cts, eeb, alpha, g0[i], n_iter=int(iters[i]))
+        assert np.abs(gamma[i] - g).sum() <= 1e-3 * k + 1e-4 * g.sum(), (i, np.abs(gamma[i] - g).sum())
+        big = g >= 1.0
+        np.testing.assert_allclose(gamma[i][big], g[big], rtol=TOL["f32"]["gamma"])
+
+
 def test_estep_long_documents_global_path(ctx, oracle):
     """Docs whose nnz×k block exceeds the LDS budget stream it from L2 instead (books-sized rows)."""
     rng = np.random.default_rng(11)

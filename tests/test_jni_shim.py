@@ -44,7 +44,7 @@ def test_short_java_arrays_throw_before_the_library_is_called(tmp_path):
     iae = "java/lang/IllegalArgumentException"
     short = {"hashingTf_short_indices": ("hashingTf indicesOut", 2, 3), "hashingTf_short_indptr": ("hashingTf indptrOut", 2, 3),
              "hashTokens_short": ("hashTokens idxOut", 2, 3), "tokenize_short_tokoff": ("tokenize tokOffOut", 6, 7),
-             "tokenize_short_utf8": ("tokenize utf8Out", 4, 5), "dcsrUpload_short_indices": ("dcsrUpload indices", 4, 5),
+             "tokenize_short_utf8": ("tokenize utf8Out", 6, 7), "dcsrUpload_short_indices": ("dcsrUpload indices", 4, 5),
              "dcsrUpload_short_indptr": ("dcsrUpload indptr", 3, 4), "ldaCounters_short": ("ldaCounters out", 3, 4),
              "ldaPhaseTimes_short": ("ldaPhaseTimes msOut", 4, 5)}
     for name, (what, have, need) in short.items():

@@ -51,6 +51,54 @@ def lower_entry(cp):
     return ord(lc)
 
 
+def special_maps():
+    """the length-changing 1:1 maps among the rejected entries: {cp: lower cp} (İ and Σ are handled by rule)"""
+    out = {}
+    for cp in range(0x80, 0x10000):
+        if 0xD800 <= cp <= 0xDFFF or java8_identity(cp) or cp in (0x130, 0x3A3):
+            continue
+        lc = chr(cp).lower()
+        if len(lc) == 1 and utf8_len(ord(lc)) != utf8_len(cp):
+            out[cp] = ord(lc)
+    return out
+
+
+# Final_Sigma (U+03A3 → ς when preceded by a cased letter, case-ignorables between, and not followed by
+# case-ignorables then a cased letter): the class of every code point the rule's two scans look at, as
+# Python's str.lower() — the oracle's lower-casing — applies it: 1 = case-ignorable (skipped), 2 = cased and
+# not case-ignorable (ends a scan, counts), 0 = anything else (ends a scan).  Read off str.lower() itself
+# ("AΣc" and "AΣcB"), so the table and the oracle cannot disagree.  Java 8's unassigned code points (the
+# identity ranges) are class 0, as the oracle's per-segment lowering treats them.
+SIG_OTHER, SIG_IGNORABLE, SIG_CASED = 0, 1, 2
+
+
+def sigma_class(cp):
+    if 0xD800 <= cp <= 0xDFFF or java8_identity(cp) or any(lo <= cp <= hi for lo, hi in SUPP_IDENTITY_RANGES):
+        return SIG_OTHER
+    c = chr(cp)
+    a, b = ("A\u03a3" + c).lower()[1], ("A\u03a3" + c + "B").lower()[1]
+    if a == "\u03c2" and b == "\u03c3":
+        return SIG_IGNORABLE
+    return SIG_CASED if a == "\u03c3" else SIG_OTHER
+
+
+SUPP_IDENTITY_RANGES = [(0x104B0, 0x104FF), (0x10C80, 0x10CFF), (0x118A0, 0x118FF), (0x16E40, 0x16E9F),
+                        (0x1E900, 0x1E95F)]
+
+
+def sigma_pages():
+    idx, data = [], []
+    for p in range(0x110000 >> 8):
+        cls = [sigma_class(cp) for cp in range(p << 8, (p + 1) << 8)]
+        if not any(cls):
+            idx.append(0)
+            continue
+        packed = [sum(cls[4 * i + j] << (2 * j) for j in range(4)) for i in range(64)]
+        data.append(packed)
+        idx.append(len(data))
+    return idx, data
+
+
 def pages():
     idx, data = [], []
     for p in range(256):
@@ -76,6 +124,20 @@ def main():
     n_rej = sum(1 for ent in data for e in ent if e == 0) - 1  # U+0000's entry (ASCII never looks it up)
     n_map = sum(1 for pi, ent in enumerate(data) for i, e in enumerate(ent)
                 if e and e != (idx.index(pi + 1) << 8) + i)
+    sp = special_maps()
+    sidx, sdata = sigma_pages()
+    assert len(sdata) < 256
+    srows = ["    {" + ", ".join(f"0x{x:02X}" for x in ent) + "}," for ent in sdata]
+    sirows = ["    " + ", ".join(f"{x:2d}" for x in sidx[i:i + 32]) + "," for i in range(0, len(sidx), 32)]
+    special = ("// the capitals whose lower case has another UTF-8 length (their kCasePages entry is 0): cp → lower\n"
+               f"constexpr int kSpecialN = {len(sp)};\n"
+               "__device__ const uint16_t kSpecialFrom[kSpecialN] = {" + ", ".join(f"0x{k:04X}" for k in sp) + "};\n"
+               "__device__ const uint16_t kSpecialTo[kSpecialN] = {" + ", ".join(f"0x{v:04X}" for v in sp.values()) + "};\n\n"
+               "// Final_Sigma classes (2 bits per code point, 0 other, 1 case-ignorable, 2 cased), two levels over\n"
+               "// U+0000–U+10FFFF: kSigPage[cp >> 8] = 0 (all other) or 1 + the page in kSigPages\n"
+               f"constexpr int kSigPagesN = {len(sdata)};\n"
+               "__device__ const uint8_t kSigPage[4352] = {\n" + "\n".join(sirows) + "\n};\n"
+               "__device__ const uint8_t kSigPages[kSigPagesN][64] = {\n" + "\n".join(srows) + "\n};\n\n")
     txt = ("// case_table.h — GENERATED by tools/gen_case_table.py (do not edit): Java 8 String.toLowerCase\n"
            "// (root locale) of every BMP code point, two levels: kCasePage[cp >> 8] = 0 (the page maps to itself)\n"
            "// or 1 + its page in kCasePages, whose entry cp & 0xFF = the lower-case code point, 0 = rejected (see\n"
@@ -84,6 +146,7 @@ def main():
            f"constexpr int kCasePagesN = {len(data)};\n"
            "__device__ const uint8_t kCasePage[256] = {\n" + "\n".join(irows) + "\n};\n"
            "__device__ const uint16_t kCasePages[kCasePagesN][256] = {\n" + "\n".join(rows) + "\n};\n\n"
+           + special +
            "}  // namespace tokenizer\n}  // namespace stc\n")
     open(OUT, "w").write(txt)
     print(f"wrote {OUT}: {len(data)} pages, {n_map} mapped, {n_rej} rejected")

@@ -24,7 +24,8 @@ __device__ __forceinline__ unsigned long long now() {
   return t;
 }
 
-enum Op { FMA_DEP, FMA_IND8, RCP_DEP, PSI_S, PSI_S_X2, PSI_FAST, LDS_DEP, WSUM, BARRIER, RCPNR_DEP };
+enum Op { FMA_DEP, FMA_IND8, RCP_DEP, PSI_S, PSI_S_X2, PSI_FAST, LDS_DEP, WSUM, BARRIER, RCPNR_DEP, PSI_V2_2, PSI_V2_1,
+          PKFMA_IND8 };
 
 template <int OP>
 __global__ void k_bench(double* out, unsigned long long* cyc, double a, double b) {
@@ -71,6 +72,24 @@ __global__ void k_bench(double* out, unsigned long long* cyc, double a, double b
         y = fma(exp_digamma_minus_s(y, a), 0.25, b);
         asm volatile("" : "+v"(x), "+v"(y));
       }
+    } else if (OP == PSI_V2_2 || OP == PSI_V2_1) {
+#pragma unroll 2
+      for (int i = 0; i < kN / 16; ++i) {
+        x = fma(OP == PSI_V2_2 ? exp_digamma_minus_v2<2>(x, a) : exp_digamma_minus_v2<1>(x, a), 0.25, b);
+        asm volatile("" : "+v"(x));
+      }
+    } else if (OP == PKFMA_IND8) {
+      typedef float f2_t __attribute__((ext_vector_type(2)));
+      f2_t p[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p[j] = (f2_t){(float)acc[j], (float)(acc[j] + 1.0)};
+      const f2_t fa = {(float)a, (float)a}, fb = {(float)b, (float)b};
+#pragma unroll 4
+      for (int i = 0; i < kN / 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p[j]) : "v"(fa), "v"(fb));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = p[j].x + p[j].y;
     } else if (OP == PSI_FAST) {
 #pragma unroll 2
       for (int i = 0; i < kN / 16; ++i) {
@@ -106,7 +125,7 @@ __global__ void k_bench(double* out, unsigned long long* cyc, double a, double b
 // operations per timed loop, for the per-op figure
 static int ops(int op) {
   switch (op) {
-    case PSI_S: case PSI_FAST: return kN / 16;
+    case PSI_S: case PSI_FAST: case PSI_V2_2: case PSI_V2_1: return kN / 16;
     case PSI_S_X2: return kN / 16;  // pairs
     case WSUM: return kN / 8;
     default: return kN;
@@ -129,12 +148,41 @@ static void run(const char* name, int waves_per_simd, double* d_out, unsigned lo
               (double)mx / ops(OP));
 }
 
+// accuracy of the raw v_rcp_f64 and of one / two Newton steps: max |r·q − 1| in units of 2^-52 over
+// q = 2^e · m, e ∈ [-20, 40), m ∈ [1, 2) on a fine grid
+__global__ void k_rcp_err(double* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const double q = ldexp(1.0 + (double)(i & 0xFFFFF) * 0x1p-20 + 0x1p-45 * (i >> 20), (i >> 20) - 20);
+  const double r0 = __builtin_amdgcn_rcp(q);
+  const double r1 = fma(r0, fma(-q, r0, 1.0), r0);
+  const double r2 = fma(r1, fma(-q, r1, 1.0), r1);
+  const double e0 = fabs(fma(r0, q, -1.0)) * 0x1p52, e1 = fabs(fma(r1, q, -1.0)) * 0x1p52,
+               e2 = fabs(fma(r2, q, -1.0)) * 0x1p52;
+  out[3 * i] = e0;
+  out[3 * i + 1] = e1;
+  out[3 * i + 2] = e2;
+}
+
 int main() {
   double* d_out = nullptr;
   unsigned long long* d_cyc = nullptr;
   if (hipMalloc(&d_out, 4096 * sizeof(double)) != hipSuccess || hipMalloc(&d_cyc, 64 * 8) != hipSuccess) {
     std::printf("{\"error\": \"hipMalloc\"}\n");
     return 1;
+  }
+  {
+    const int n = 60 << 20;
+    double* d_e = nullptr;
+    if (hipMalloc(&d_e, sizeof(double) * 3 * (size_t)n) == hipSuccess) {
+      hipLaunchKernelGGL(k_rcp_err, dim3(n / 256), dim3(256), 0, 0, d_e);
+      std::vector<double> e(3 * (size_t)n);
+      (void)hipMemcpy(e.data(), d_e, sizeof(double) * e.size(), hipMemcpyDeviceToHost);
+      double m[3] = {0, 0, 0};
+      for (size_t i = 0; i < e.size(); ++i) m[i % 3] = e[i] > m[i % 3] ? e[i] : m[i % 3];
+      std::printf("{\"case\": \"rcp_f64_error_ulp52\", \"raw\": %.4g, \"newton1\": %.4g, \"newton2\": %.4g}\n",
+                  m[0], m[1], m[2]);
+      (void)hipFree(d_e);
+    }
   }
   for (int w = 1; w <= 3; ++w) {
     run<FMA_DEP>("fma_f64_dependent", w, d_out, d_cyc);
@@ -144,6 +192,9 @@ int main() {
     run<PSI_S>("exp_digamma_minus_s_dependent", w, d_out, d_cyc);
     run<PSI_S_X2>("exp_digamma_minus_s_2_chains", w, d_out, d_cyc);
     run<PSI_FAST>("exp_digamma_minus_fast_dependent", w, d_out, d_cyc);
+    run<PSI_V2_2>("exp_digamma_minus_v2_nr2_dependent", w, d_out, d_cyc);
+    run<PSI_V2_1>("exp_digamma_minus_v2_nr1_dependent", w, d_out, d_cyc);
+    run<PKFMA_IND8>("pk_fma_f32_8_independent", w, d_out, d_cyc);
     run<LDS_DEP>("ds_read_b128_dependent", w, d_out, d_cyc);
     run<WSUM>("wave_sum_d_dependent", w, d_out, d_cyc);
     run<BARRIER>("s_barrier", w, d_out, d_cyc);
