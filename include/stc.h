@@ -170,6 +170,14 @@ int stc_idf_fit(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq,
  * zero_floor (the reference's LDAClustering.scala:184-187 quirk; 0 = stock Spark)          */
 int stc_idf_transform(stc_ctx* ctx, stc_dcsr* tf, const double* idf /* n_cols */,
                       double zero_floor);
+/* The same IDFModel kept on the device (the GPU-resident HashingTF → IDF → LDA pipeline: the idf
+ * vector need not cross PCIe between fit and transform); stc_idf_get copies it out (any may be NULL). */
+typedef struct stc_didf stc_didf;
+int stc_idf_fit_dev(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, stc_didf** out);
+int stc_idf_get(stc_ctx* ctx, const stc_didf* model, double* idf_out /* n_cols */,
+                int64_t* df_out /* n_cols */, int64_t* m_out);
+int stc_idf_transform_dev(stc_ctx* ctx, stc_dcsr* tf, const stc_didf* model, double zero_floor);
+int stc_didf_free(stc_didf* model);
 
 /* ---- online LDA ----------------------------------------------------------------------- */
 typedef struct stc_lda_config {

@@ -334,6 +334,35 @@ JNIEXPORT void JNICALL FN(idfTransform)(JNIEnv* env, jclass c, jlong ctx, jlong 
   check(env, st);
 }
 
+/* the IDF model kept on the device (GPU-resident pipeline); idfGet copies it out: returns m */
+JNIEXPORT jlong JNICALL FN(idfFitDev)(JNIEnv* env, jclass c, jlong ctx, jlong dcsr, jlong min_doc_freq) {
+  stc_didf* md = NULL;
+  if (check(env, stc_idf_fit_dev(CTX(ctx), CSR(dcsr), min_doc_freq, &md))) return 0;
+  return (jlong)(intptr_t)md;
+}
+
+JNIEXPORT jlong JNICALL FN(idfGet)(JNIEnv* env, jclass c, jlong ctx, jlong model, jlong cols, jdoubleArray idf_out,
+                                   jlongArray df_out) {
+  int64_t m = 0;
+  if ((idf_out && NEED(idf_out, cols, "idfGet idfOut")) || (df_out && NEED(df_out, cols, "idfGet dfOut"))) return 0;
+  jdouble* o = idf_out ? PIN(jdouble, Double, idf_out) : NULL;
+  jlong* df = df_out ? PIN(jlong, Long, df_out) : NULL;
+  int st = stc_idf_get(CTX(ctx), (const stc_didf*)(intptr_t)model, o, (int64_t*)df, &m);
+  if (df) UNPIN(Long, df_out, df, 0);
+  if (o) UNPIN(Double, idf_out, o, 0);
+  if (check(env, st)) return 0;
+  return m;
+}
+
+JNIEXPORT void JNICALL FN(idfTransformDev)(JNIEnv* env, jclass c, jlong ctx, jlong dcsr, jlong model,
+                                           jdouble zero_floor) {
+  check(env, stc_idf_transform_dev(CTX(ctx), CSR(dcsr), (const stc_didf*)(intptr_t)model, zero_floor));
+}
+
+JNIEXPORT void JNICALL FN(didfFree)(JNIEnv* env, jclass c, jlong model) {
+  check(env, stc_didf_free((stc_didf*)(intptr_t)model));
+}
+
 /* ---- online LDA ------------------------------------------------------------------------- */
 /* stc_lda_config_default + the given fields (alpha: length 1 or k, or null ⇒ −1 ⇒ 1/k) */
 JNIEXPORT jlong JNICALL FN(ldaCreate)(JNIEnv* env, jclass c, jlong ctx, jint k, jlong vocab, jdoubleArray alpha,

@@ -64,6 +64,11 @@ public final class StcNative {
   // ---- IDF: returns m (documents, summed over ranks)
   public static native long idfFit(long ctx, long dcsr, long minDocFreq, double[] idfOut, long[] dfOut);
   public static native void idfTransform(long ctx, long dcsr, double[] idf, double zeroFloor);
+  // the IDF model kept on the device (a handle); idfGet copies idf / df out (either may be null), returns m
+  public static native long idfFitDev(long ctx, long dcsr, long minDocFreq);
+  public static native long idfGet(long ctx, long model, long cols, double[] idfOut, long[] dfOut);
+  public static native void idfTransformDev(long ctx, long dcsr, long model, double zeroFloor);
+  public static native void didfFree(long model);
 
   // ---- online LDA (alpha null ⇒ −1 ⇒ 1/k; eta −1 ⇒ 1/k)
   public static native long ldaCreate(long ctx, int k, long vocabSize, double[] alpha, double eta, double tau0,

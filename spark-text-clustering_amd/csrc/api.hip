@@ -1401,6 +1401,40 @@ int stc_tokenize_hashing_tf_dev(stc_ctx* ctx, const uint8_t* text, int64_t n_byt
 }
 
 // ---- IDF --------------------------------------------------------------------------------
+}  // extern "C"
+
+struct stc_didf {
+  Ctx* ctx = nullptr;
+  int device = -1;
+  int64_t cols = 0, m = 0;
+  DevBuf idf, df;
+};
+
+namespace {
+// IDF.fit on the device: df (all ranks' when connected), m, idf into the given buffers
+void idf_fit_impl(Ctx& c, const DCsr& tf, int64_t min_doc_freq, DevBuf& df, DevBuf& idf, int64_t& m) {
+  hipStream_t s = c.stream;
+  df.reserve(8 * tf.cols);
+  idf.reserve(8 * tf.cols);
+  idf::doc_freq(c, tf, df.as<int64_t>());
+  m = tf.rows;
+  if (c.coll()) {  // DocumentFrequencyAggregator.merge over ranks
+    DevBuf mm;
+    mm.reserve(8);
+    HIP_CHECK(hipMemcpyAsync(mm.p, &m, 8, hipMemcpyHostToDevice, s));
+    coll_group_start(c);
+    coll_all_reduce(c, df.p, (size_t)tf.cols, ncclInt64, s);
+    coll_all_reduce(c, mm.p, 1, ncclInt64, s);
+    coll_group_end(c);
+    HIP_CHECK(hipMemcpyAsync(&m, mm.p, 8, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+  }
+  idf::finalize(c, df.as<int64_t>(), tf.cols, m, min_doc_freq, idf.as<double>());
+}
+}  // namespace
+
+extern "C" {
+
 int stc_idf_fit(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, double* idf_out,
                 int64_t* df_out, int64_t* m_out) {
   return guard([&] {
@@ -1411,26 +1445,60 @@ int stc_idf_fit(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, double* 
     hipStream_t s = ctx->stream;
     DevBuf& df = ctx->scratch[9];  // grow-only on the context: no per-call allocation
     DevBuf& idf = ctx->scratch[10];
-    df.reserve(8 * tf->cols);
-    idf.reserve(8 * tf->cols);
-    idf::doc_freq(*ctx, *tf, df.as<int64_t>());
-    int64_t m = tf->rows;
-    if (ctx->coll()) {  // DocumentFrequencyAggregator.merge over ranks
-      DevBuf mm;
-      mm.reserve(8);
-      HIP_CHECK(hipMemcpyAsync(mm.p, &m, 8, hipMemcpyHostToDevice, s));
-      coll_group_start(*ctx);
-      coll_all_reduce(*ctx, df.p, (size_t)tf->cols, ncclInt64, s);
-      coll_all_reduce(*ctx, mm.p, 1, ncclInt64, s);
-      coll_group_end(*ctx);
-      HIP_CHECK(hipMemcpyAsync(&m, mm.p, 8, hipMemcpyDeviceToHost, s));
-      HIP_CHECK(hipStreamSynchronize(s));
-    }
-    idf::finalize(*ctx, df.as<int64_t>(), tf->cols, m, min_doc_freq, idf.as<double>());
+    int64_t m = 0;
+    idf_fit_impl(*ctx, *tf, min_doc_freq, df, idf, m);
     HIP_CHECK(hipMemcpyAsync(idf_out, idf.p, 8 * tf->cols, hipMemcpyDeviceToHost, s));
     if (df_out) HIP_CHECK(hipMemcpyAsync(df_out, df.p, 8 * tf->cols, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     if (m_out) *m_out = m;
+  });
+}
+
+int stc_idf_fit_dev(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, stc_didf** out) {
+  return guard([&] {
+    STC_REQUIRE(ctx && tf && out, "ctx/tf/out");
+    STC_REQUIRE(tf->ctx == ctx, "the matrix belongs to another stc_ctx");
+    STC_REQUIRE(min_doc_freq >= 0, "minDocFreq must be >= 0");
+    ctx->use();
+    auto md = std::make_unique<stc_didf>();
+    md->ctx = ctx;
+    md->device = ctx->device;
+    md->cols = tf->cols;
+    idf_fit_impl(*ctx, *tf, min_doc_freq, md->df, md->idf, md->m);
+    *out = md.release();  // (the stream orders every later use of the model after the fit)
+  });
+}
+
+int stc_idf_get(stc_ctx* ctx, const stc_didf* md, double* idf_out, int64_t* df_out, int64_t* m_out) {
+  return guard([&] {
+    STC_REQUIRE(ctx && md, "ctx/model");
+    STC_REQUIRE(md->ctx == ctx, "the model belongs to another stc_ctx");
+    ctx->use();
+    hipStream_t s = ctx->stream;
+    if (idf_out) HIP_CHECK(hipMemcpyAsync(idf_out, md->idf.p, 8 * md->cols, hipMemcpyDeviceToHost, s));
+    if (df_out) HIP_CHECK(hipMemcpyAsync(df_out, md->df.p, 8 * md->cols, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (m_out) *m_out = md->m;
+  });
+}
+
+int stc_idf_transform_dev(stc_ctx* ctx, stc_dcsr* tf, const stc_didf* md, double zero_floor) {
+  return guard([&] {
+    STC_REQUIRE(ctx && tf && md, "ctx/tf/model");
+    STC_REQUIRE(tf->ctx == ctx && md->ctx == ctx, "the matrix or model belongs to another stc_ctx");
+    STC_REQUIRE(tf->cols == md->cols, "vector size does not match the IDF size");
+    STC_REQUIRE(zero_floor >= 0.0, "zero_floor must be >= 0");
+    ctx->use();
+    idf::transform(*ctx, *tf, md->idf.as<double>(), zero_floor);
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+int stc_didf_free(stc_didf* md) {
+  return guard([&] {
+    if (!md) return;
+    (void)hipSetDevice(md->device);
+    delete md;
   });
 }
 

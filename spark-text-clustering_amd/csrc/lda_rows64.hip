@@ -41,6 +41,9 @@
 #ifndef R64_RCP_NR
 #define R64_RCP_NR 2  // Newton steps after v_rcp_f64 in that chain
 #endif
+#ifndef R64_MIRROR
+#define R64_MIRROR 1  // k > 64: the idle wave of the ψ wave's topic set computes Σ|Δγ| (off the ψ chain)
+#endif
 #ifndef R64_LONG_OCC
 #define R64_LONG_OCC 1  // long-document kernel workgroups per CU the register budget is cut for
 #endif
@@ -247,6 +250,10 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
   const bool town = d.town;
   const int qid = d.qid;
   const double qc = d.qc, qe2 = d.qe2;
+  // mirror mode (k > 64): the waves w and w ^ 2 share a topic set and take turns as its ψ wave and as
+  // its Σ|Δγ| wave; each keeps γ / eθ of its lane's topic as it last computed them (read once below)
+  const bool mir = R64_MIRROR && npsi == 2;
+  double gm = 0.0, em = 0.0;
 
   // ---- B rows, coalesced: per row set the wave copies its eight rows (kp doubles each) with
   // 16-byte loads, stages them in LDS and every lane picks up its (row lane, topic lane) part
@@ -303,6 +310,10 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
   }
 
   __syncthreads();  // the staging area is the loop's partial arrays; (also publishes the first eθ)
+  if (mir && town) {  // γ₀ / eθ₀ of the lane's topic (no ψ phase has overwritten them before barrier 1)
+    gm = sm.gam[tt];
+    em = sm.eth[ttl][ttp];
+  }
 
   double* const pa = &sm.u.l.pa[w][0][0];
   double* const sb = &sm.u.l.sb[0][0];
@@ -380,7 +391,7 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
         double2 xs[16];
 #pragma unroll
         for (int h = 0; h < 16; ++h) xs[h] = sp[h];
-        const double g = sm.gam[tt], eo = sm.eth[ttl][ttp];
+        const double g = mir ? gm : sm.gam[tt], eo = sm.eth[ttl][ttp];
         const double2 ap = *reinterpret_cast<const double2*>(&sm.apc[tt][0]);  // α_t, ψc_t
         const double2 e01 = *reinterpret_cast<const double2*>(&sm.esum[0]);
         const double2 e23 = *reinterpret_cast<const double2*>(&sm.esum[2]);
@@ -396,12 +407,40 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
         const double gn = fma(eo, s, ap.x);  // γ ← eθ ⊙ s + α
         dg = fabs(gn - g);
         sm.gam[tt] = gn;
-        sm.eth[ttl][ttp] = exp_digamma_minus_r64(gn, csn + ap.y);
+        const double en = exp_digamma_minus_r64(gn, csn + ap.y);
+        sm.eth[ttl][ttp] = en;
+        gm = gn;
+        em = en;
         if (tt == 0) sm.cs = csn;
+      }
+      if (!mir) {
+        const double d = wave_sum_d(dg);
+        if (lane == 0) sm.dsum[pw] = d;
+      }
+      if (R64_PRIO >= 1) __builtin_amdgcn_s_setprio(0);
+    } else if (mir) {
+      // the other wave of this topic set: the same γ update from its own γ / eθ registers (bitwise the ψ
+      // wave's: same partials, same order), and Σ|Δγ| — its six-step reduction no longer sits on the ψ chain
+      double dg = 0.0;
+      if (town) {
+        const double2* const sp = reinterpret_cast<const double2*>(sb + tt * kSbPitch);
+        double2 xs[16];
+#pragma unroll
+        for (int h = 0; h < 16; ++h) xs[h] = sp[h];
+        const double al = sm.apc[tt][0];
+        double c4[4];
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const double2 x0 = xs[4 * h], x1 = xs[4 * h + 1], x2 = xs[4 * h + 2], x3 = xs[4 * h + 3];
+          c4[h] = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
+        }
+        const double s = (c4[0] + c4[1]) + (c4[2] + c4[3]);
+        const double gn = fma(em, s, al);
+        dg = fabs(gn - gm);
+        gm = gn;  // (its eθ: the ψ wave's, from LDS, when this wave is next the ψ wave)
       }
       const double d = wave_sum_d(dg);
       if (lane == 0) sm.dsum[pw] = d;
-      if (R64_PRIO >= 1) __builtin_amdgcn_s_setprio(0);
     }
     STAMP(psi ? 5 : 8);  // ψ phase (ψ waves; non-ψ waves: nothing)
     __syncthreads();  // (2) eθ, γ, Σ|Δγ| published

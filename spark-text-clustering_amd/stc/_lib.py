@@ -91,6 +91,10 @@ SIGNATURES = {
                                            C.POINTER(_p)]),
     "stc_idf_fit": (_int, [_p, _p, _i64, _pdbl, _pi64, _pi64]),
     "stc_idf_transform": (_int, [_p, _p, _pdbl, _dbl]),
+    "stc_idf_fit_dev": (_int, [_p, _p, _i64, C.POINTER(_p)]),
+    "stc_idf_get": (_int, [_p, _p, _pdbl, _pi64, _pi64]),
+    "stc_idf_transform_dev": (_int, [_p, _p, _p, C.c_double]),
+    "stc_didf_free": (_int, [_p]),
     "stc_lda_config_default": (None, [C.POINTER(LdaConfig)]),
     "stc_lda_create": (_int, [_p, C.POINTER(LdaConfig), C.POINTER(_p)]),
     "stc_lda_destroy": (_int, [_p]),

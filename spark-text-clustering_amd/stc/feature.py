@@ -198,20 +198,54 @@ class HashingTF:
 
 
 class IDFModel:
-    """Fitted IDF: ``idf`` (float64[numFeatures]), ``docFreq`` (int64), ``numDocs``."""
+    """Fitted IDF: ``idf`` (float64[numFeatures]), ``docFreq`` (int64), ``numDocs``.  A model fitted on the
+    device (IDF.fit_device) stays there (stc_didf): transform_device uses it in place and the host arrays
+    are copied out only when read."""
 
-    def __init__(self, idf, docFreq, numDocs, ctx: Context | None = None):
-        self.idf = np.asarray(idf, np.float64)
-        self.docFreq = np.asarray(docFreq, np.int64)
-        self.numDocs = int(numDocs)
+    def __init__(self, idf=None, docFreq=None, numDocs=None, ctx: Context | None = None, _dev=None, _cols=0):
+        self._idf = None if idf is None else np.asarray(idf, np.float64)
+        self._df = None if docFreq is None else np.asarray(docFreq, np.int64)
+        self._m = None if numDocs is None else int(numDocs)
         self._ctx = ctx
+        self._dev, self._cols = _dev, int(_cols)
 
     @property
     def ctx(self):
         return self._ctx or Context.get()
 
+    def _fetch(self):
+        idf = np.zeros(self._cols, np.float64)
+        df = np.zeros(self._cols, np.int64)
+        m = C.c_int64()
+        L.check(self.ctx.lib.stc_idf_get(self.ctx.handle, self._dev, L.ptr(idf, C.c_double), L.ptr(df, C.c_int64),
+                                         C.byref(m)))
+        self._idf, self._df, self._m = idf, df, m.value
+
+    @property
+    def idf(self):
+        if self._idf is None:
+            self._fetch()
+        return self._idf
+
+    @property
+    def docFreq(self):
+        if self._df is None:
+            self._fetch()
+        return self._df
+
+    @property
+    def numDocs(self):
+        if self._m is None:
+            self._fetch()
+        return self._m
+
     def transform_device(self, tf: DeviceCsr, zero_floor=0.0) -> DeviceCsr:
         """In place on a device CSR.  zero_floor=1e-4 reproduces LDAClustering.scala:184-187."""
+        if self._dev is not None:
+            if tf.num_cols != self._cols:
+                raise ValueError(f"vector size {tf.num_cols} does not match IDF size {self._cols}")
+            L.check(self.ctx.lib.stc_idf_transform_dev(self.ctx.handle, tf.handle, self._dev, float(zero_floor)))
+            return tf
         idf = L.as_f64(self.idf)
         if tf.num_cols != idf.size:
             raise ValueError(f"vector size {tf.num_cols} does not match IDF size {idf.size}")
@@ -225,6 +259,22 @@ class IDFModel:
             return self.transform_device(d, zero_floor).download()
         finally:
             d.free()
+
+    def free(self):
+        """releases the device copy (the host arrays are fetched first, so the model stays usable)"""
+        if self._dev is not None:
+            if self._idf is None:
+                self._fetch()
+            self.ctx.lib.stc_didf_free(self._dev)
+            self._dev = None
+
+    def __del__(self):
+        try:
+            if self._dev is not None:
+                self.ctx.lib.stc_didf_free(self._dev)
+                self._dev = None
+        except Exception:
+            pass
 
 
 class IDF:
@@ -249,16 +299,19 @@ class IDF:
         return self.minDocFreq
 
     def fit_device(self, tf: DeviceCsr) -> IDFModel:
-        idf = np.zeros(tf.num_cols, np.float64)
-        df = np.zeros(tf.num_cols, np.int64)
-        m = C.c_int64()
-        L.check(self.ctx.lib.stc_idf_fit(self.ctx.handle, tf.handle, self.minDocFreq,
-                                         L.ptr(idf, C.c_double), L.ptr(df, C.c_int64), C.byref(m)))
-        return IDFModel(idf, df, m.value, self._ctx)
+        """IDF.fit on a device CSR; the model stays on the device (stc_idf_fit_dev)"""
+        h = C.c_void_p()
+        L.check(self.ctx.lib.stc_idf_fit_dev(self.ctx.handle, tf.handle, self.minDocFreq, C.byref(h)))
+        return IDFModel(ctx=self._ctx, _dev=h, _cols=tf.num_cols)
 
     def fit(self, tf: CsrMatrix) -> IDFModel:
         d = DeviceCsr.upload(self.ctx, tf, L.STC_F64)
         try:
-            return self.fit_device(d)
+            idf = np.zeros(tf.num_cols, np.float64)
+            df = np.zeros(tf.num_cols, np.int64)
+            m = C.c_int64()
+            L.check(self.ctx.lib.stc_idf_fit(self.ctx.handle, d.handle, self.minDocFreq,
+                                             L.ptr(idf, C.c_double), L.ptr(df, C.c_int64), C.byref(m)))
+            return IDFModel(idf, df, m.value, self._ctx)
         finally:
             d.free()

@@ -111,13 +111,19 @@ def test_pipeline_hashing_idf_device_resident(ctx, oracle):
     docs = random_tokens(rng, 200, max_len=60)
     htf = stc.HashingTF(numFeatures=1 << 12, ctx=ctx)  # default: Spark 2.4.3's legacy tail
     d = htf.transform_device(docs)
-    model = stc.IDF(minDocFreq=2, ctx=ctx).fit_device(d)
-    model.transform_device(d)
+    model = stc.IDF(minDocFreq=2, ctx=ctx).fit_device(d)  # stays on the device (stc_idf_fit_dev)
+    model.transform_device(d, zero_floor=1e-4)
     got = d.download()
     ip, ix, vv = oracle.hashing_tf(docs, 1 << 12, variant=oracle.HASH_SPARK24)
-    idf_o, _, _ = oracle.idf_fit(ip, ix, vv, 1 << 12, 2)
+    idf_o, df_o, m_o = oracle.idf_fit(ip, ix, vv, 1 << 12, 2)
     assert np.array_equal(got.indices, ix)
-    np.testing.assert_allclose(got.values, oracle.idf_transform(ix, vv, idf_o), rtol=1e-15, atol=0)
+    np.testing.assert_allclose(got.values, oracle.idf_transform(ix, vv, idf_o, floor=1e-4), rtol=1e-15, atol=0)
+    # the device model's copy-out equals the host fit of the same matrix
+    host = stc.IDF(minDocFreq=2, ctx=ctx).fit(stc.CsrMatrix(ip, ix, vv, 1 << 12))
+    assert np.array_equal(model.idf, host.idf) and np.array_equal(model.docFreq, host.docFreq)
+    assert model.numDocs == host.numDocs == m_o and np.array_equal(model.docFreq, df_o)
+    model.free()
+    assert np.array_equal(model.idf, host.idf)  # host arrays survive the device copy
 
 
 def test_device_resident_tokens_synthetic_dictionary(ctx, oracle):
