@@ -235,6 +235,7 @@ def featurization(stc, ctx, a, log, tokens, reps=3):
         ctx.synchronize()
         t1 = time.perf_counter()
         m = idf.fit_device(d)
+        ctx.synchronize()
         t2 = time.perf_counter()
         m.transform_device(d, zero_floor=1e-4)
         ctx.synchronize()

@@ -36,6 +36,7 @@ struct stc_dtok {
   int device = -1;     // for stc_tokens_free, which may run after that context is gone
   DevBuf utf8, tok_off, doc_off;
   int64_t n_bytes = 0, n_tok = 0, n_docs = 0;
+  int64_t max_doc = -1;  // the longest document's token count (from the upload's offsets)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -1078,6 +1079,11 @@ int stc_init(int device, stc_ctx** out) {
     c->device = device;
     HIP_CHECK(hipSetDevice(device));
     HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIP_CHECK(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device));
+    const char* db = std::getenv("STC_DF_BINNED");  // A/B knob: the round-3 binned df count
+    c->df_tiled = !(db && db[0] == '1');
+    const char* tp = std::getenv("STC_TF_TWO_PASS");  // A/B knob: the round-3 HashingTF passes
+    c->single_pass_tf = !(tp && tp[0] == '1');
     *out = c.release();
   });
 }
@@ -1214,6 +1220,7 @@ int stc_dcsr_free(stc_dcsr* m) {
 namespace {
 struct TokenUpload {
   DevBuf utf8, tok_off, doc_off;
+  int64_t max_doc = -1;  // the longest document's token count (doc_off given), −1 unknown
 };
 void upload_tokens(Ctx& c, TokenUpload& u, const uint8_t* utf8, int64_t n_bytes, const int64_t* tok_off,
                    int64_t n_tok, const int64_t* doc_off, int64_t n_docs) {
@@ -1223,9 +1230,13 @@ void upload_tokens(Ctx& c, TokenUpload& u, const uint8_t* utf8, int64_t n_bytes,
   for (int64_t t = 0; t < n_tok; ++t) STC_REQUIRE(tok_off[t + 1] >= tok_off[t], "tok_off must be non-decreasing");
   if (doc_off) {
     STC_REQUIRE(doc_off[0] == 0 && doc_off[n_docs] == n_tok, "doc_off must span [0, n_tok]");
-    for (int64_t d = 0; d < n_docs; ++d) STC_REQUIRE(doc_off[d + 1] >= doc_off[d], "doc_off must be non-decreasing");
+    u.max_doc = 0;
+    for (int64_t d = 0; d < n_docs; ++d) {
+      STC_REQUIRE(doc_off[d + 1] >= doc_off[d], "doc_off must be non-decreasing");
+      u.max_doc = std::max<int64_t>(u.max_doc, doc_off[d + 1] - doc_off[d]);
+    }
   }
-  u.utf8.reserve(n_bytes + 16);  // k_hash reads whole aligned dwords up to 8 bytes past a token
+  u.utf8.reserve(n_bytes + kHashPad);  // the hash reads 32-byte windows of whole aligned dwords
   u.tok_off.reserve(8 * (n_tok + 1));
   if (n_bytes) HIP_CHECK(hipMemcpyAsync(u.utf8.p, utf8, n_bytes, hipMemcpyHostToDevice, c.stream));
   HIP_CHECK(hipMemcpyAsync(u.tok_off.p, tok_off, 8 * (n_tok + 1), hipMemcpyHostToDevice, c.stream));
@@ -1256,6 +1267,7 @@ int stc_tokens_upload(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const 
     t->n_bytes = n_bytes;
     t->n_tok = n_tok;
     t->n_docs = n_docs;
+    t->max_doc = u.max_doc;
     *out = t.release();
   });
 }
@@ -1282,7 +1294,7 @@ int stc_hashing_tf_tokens(stc_ctx* ctx, const stc_dtok* tokens, int32_t num_feat
     m->device = ctx->device;
     hashing::build_csr(*ctx, tokens->utf8.as<uint8_t>(), tokens->tok_off.as<int64_t>(), tokens->n_tok,
                        tokens->doc_off.as<int64_t>(), tokens->n_docs, num_features, binary, hash_variant,
-                       value_dtype, *m);
+                       value_dtype, tokens->max_doc, *m);
     *out = m.release();
   });
 }
@@ -1320,7 +1332,7 @@ int stc_hashing_tf_dev(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const
     m->ctx = ctx;
     m->device = ctx->device;
     hashing::build_csr(*ctx, u.utf8.as<uint8_t>(), u.tok_off.as<int64_t>(), n_tok, u.doc_off.as<int64_t>(),
-                       n_docs, num_features, binary, hash_variant, value_dtype, *m);
+                       n_docs, num_features, binary, hash_variant, value_dtype, u.max_doc, *m);
     *out = m.release();
   });
 }
@@ -1395,7 +1407,7 @@ int stc_tokenize_hashing_tf_dev(stc_ctx* ctx, const uint8_t* text, int64_t n_byt
     m->ctx = ctx;
     m->device = ctx->device;
     hashing::build_csr(*ctx, t.utf8.as<uint8_t>(), t.tok_off.as<int64_t>(), t.n_tok, t.doc_off.as<int64_t>(),
-                       n_docs, num_features, binary, hash_variant, value_dtype, *m);
+                       n_docs, num_features, binary, hash_variant, value_dtype, -1, *m);
     *out = m.release();
   });
 }

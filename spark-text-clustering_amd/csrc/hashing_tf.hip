@@ -39,32 +39,61 @@ __device__ __forceinline__ uint32_t fmix(uint32_t h1, uint32_t len) {
 
 // MurmurHash3_x86_32(seed 42) of n bytes at p.  SPARK24 = Spark 2.4 hashUnsafeBytes (each tail
 // byte sign-extended and mixed as a block); otherwise the standard tail (Spark 3 hashUnsafeBytes2).
-// The bytes are read as whole aligned dwords (the buffers carry ≥ 8 bytes of padding) and realigned
-// with v_alignbyte: a byte load per character was the kernel's issue bottleneck.
+// The bytes are read as whole aligned dwords and realigned with v_alignbyte (a byte load per character
+// was the kernel's issue bottleneck).  Round 4: the first 8 dwords of a token arrive as one window of
+// two 16-byte loads issued together (load_win, before the hash needs them) — tokens of ≤ 27 bytes hash
+// from registers with no dependent load; longer ones read their remaining dwords one by one.  The
+// buffers carry ≥ kHashPad bytes of padding, so a window never leaves the allocation.
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+struct Win {
+  u32x4a lo, hi;
+};
+__device__ __forceinline__ Win load_win(const uint8_t* p) {
+  // (pointer arithmetic, not an integer round trip: the loads stay global_load, not flat_load)
+  const u32x4a* w = reinterpret_cast<const u32x4a*>(p - (reinterpret_cast<uintptr_t>(p) & 3));
+  return Win{w[0], w[1]};
+}
+
 template <bool SPARK24>
-__device__ __forceinline__ int32_t murmur3(const uint8_t* p, uint32_t n) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-  const uint32_t sh = (uint32_t)(a & 3);
+__device__ __forceinline__ int32_t murmur3_win(const uint8_t* p, uint32_t n, const Win& W) {
+  const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p - sh);
+  const uint32_t d[8] = {W.lo.x, W.lo.y, W.lo.z, W.lo.w, W.hi.x, W.hi.y, W.hi.z, W.hi.w};
   uint32_t h1 = 42u;
-  uint32_t cur = w[0];
   const uint32_t nb = n & ~3u;
-  for (uint32_t i = 0; i < nb; i += 4) {
-    const uint32_t nxt = w[(i >> 2) + 1];
-    h1 = mix_h1(h1, mix_k1(__builtin_amdgcn_alignbyte(nxt, cur, sh)));
-    cur = nxt;
-  }
+#pragma unroll
+  for (uint32_t k = 0; k < 7; ++k)  // blocks inside the window (bytes 4k..4k+3 use dwords k, k+1)
+    if (4 * k + 4 <= nb) h1 = mix_h1(h1, mix_k1(__builtin_amdgcn_alignbyte(d[k + 1], d[k], sh)));
+  for (uint32_t i = 28; i < nb; i += 4)  // past the window
+    h1 = mix_h1(h1, mix_k1(__builtin_amdgcn_alignbyte(w[(i >> 2) + 1], w[i >> 2], sh)));
   const uint32_t tail = n - nb;
   if (tail) {
-    const uint32_t t = __builtin_amdgcn_alignbyte(w[(nb >> 2) + 1], cur, sh);  // bytes nb.. in order
+    const uint32_t kk = nb >> 2;
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 7; ++k)
+      if (kk == k) {
+        lo = d[k];
+        hi = d[k + 1];
+      }
+    if (kk >= 7) {
+      lo = w[kk];
+      hi = w[kk + 1];
+    }
+    const uint32_t t = __builtin_amdgcn_alignbyte(hi, lo, sh);  // bytes nb.. in order
     if (SPARK24) {
-      for (uint32_t i = 0; i < tail; ++i)
-        h1 = mix_h1(h1, mix_k1((uint32_t)(int32_t)(int8_t)(t >> (8 * i))));
+#pragma unroll
+      for (uint32_t i = 0; i < 3; ++i)
+        if (i < tail) h1 = mix_h1(h1, mix_k1((uint32_t)(int32_t)(int8_t)(t >> (8 * i))));
     } else {
       h1 ^= mix_k1(t & (0xFFFFFFFFu >> (8 * (4 - tail))));
     }
   }
   return (int32_t)fmix(h1, n);
+}
+template <bool SPARK24>
+__device__ __forceinline__ int32_t murmur3(const uint8_t* p, uint32_t n) {
+  return murmur3_win<SPARK24>(p, n, load_win(p));
 }
 
 // four tokens per thread and step, a grid stride apart (neighbouring lanes keep neighbouring tokens,
@@ -194,10 +223,8 @@ constexpr int kFusedCap = 256;  // documents up to this many tokens are hashed a
 // sorts any starting order), is hashed there, and the P registers are sorted and their distinct ids
 // counted exactly as sort_doc does.
 template <bool SPARK24, int P>
-__device__ __forceinline__ int64_t hash_sort_doc(const uint8_t* __restrict__ utf8, const int64_t* __restrict__ tok_off,
-                                                 int64_t s, int n, int32_t nf, int32_t* __restrict__ sorted,
-                                                 int lane) {
-  int32_t x[P];
+__device__ __forceinline__ int hash_sort_regs(const uint8_t* __restrict__ utf8, const int64_t* __restrict__ tok_off,
+                                              int64_t s, int n, int32_t nf, int32_t (&x)[P], int lane) {
   int64_t b[P], e[P];
 #pragma unroll
   for (int p = 0; p < P; ++p) {
@@ -205,15 +232,19 @@ __device__ __forceinline__ int64_t hash_sort_doc(const uint8_t* __restrict__ utf
     b[p] = q < n ? tok_off[s + q] : 0;
     e[p] = q < n ? tok_off[s + q + 1] : 0;
   }
+  Win cur = load_win(utf8 + b[0]);  // pad lanes read the blob's first bytes (b = 0), unused
 #pragma unroll
   for (int p = 0; p < P; ++p) {
+    Win nxt;
+    if (p + 1 < P) nxt = load_win(utf8 + b[p + 1]);  // the next token's window in flight while this one hashes
     const int q = p * 64 + lane;
     if (q < n) {
-      const int32_t raw = murmur3<SPARK24>(utf8 + b[p], (uint32_t)(e[p] - b[p])) % nf;  // Utils.nonNegativeMod
+      const int32_t raw = murmur3_win<SPARK24>(utf8 + b[p], (uint32_t)(e[p] - b[p]), cur) % nf;  // Utils.nonNegativeMod
       x[p] = raw + (raw < 0 ? nf : 0);
     } else {
       x[p] = INT32_MAX;  // pads sort last
     }
+    if (p + 1 < P) cur = nxt;
   }
   bitonic_regs<P>(x, lane);
   const int32_t prev_last = __shfl_up(x[P - 1], 1, 64);
@@ -221,13 +252,24 @@ __device__ __forceinline__ int64_t hash_sort_doc(const uint8_t* __restrict__ utf
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     const int q = lane * P + p;
-    if (q < n) {
-      sorted[s + q] = x[p];
-      const int32_t prev = p == 0 ? prev_last : x[p - 1];
-      heads += (q == 0 || x[p] != prev) ? 1 : 0;
-    }
+    const int32_t prev = p == 0 ? prev_last : x[p - 1];
+    heads += (q < n && (q == 0 || x[p] != prev)) ? 1 : 0;
   }
   for (int o = 32; o > 0; o >>= 1) heads += __shfl_xor(heads, o, 64);
+  return heads;  // distinct ids (wave total)
+}
+
+template <bool SPARK24, int P>
+__device__ __forceinline__ int64_t hash_sort_doc(const uint8_t* __restrict__ utf8, const int64_t* __restrict__ tok_off,
+                                                 int64_t s, int n, int32_t nf, int32_t* __restrict__ sorted,
+                                                 int lane) {
+  int32_t x[P];
+  const int heads = hash_sort_regs<SPARK24, P>(utf8, tok_off, s, n, nf, x, lane);
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int q = lane * P + p;
+    if (q < n) sorted[s + q] = x[p];
+  }
   return heads;
 }
 
@@ -236,7 +278,7 @@ __device__ __forceinline__ int64_t hash_sort_doc(const uint8_t* __restrict__ utf
 // segmented radix sort (appended to `large`).  Capping the fused path at 4 keys per lane keeps the kernel
 // at ~50 VGPRs: the hashing's dependent offset → byte loads need the occupancy (the P = 16 form held 132).
 template <bool SPARK24>
-__global__ __launch_bounds__(64 * kDocWaves) void k_doc_hash_sort(const uint8_t* __restrict__ utf8,
+__global__ __launch_bounds__(64 * kDocWaves, 8) void k_doc_hash_sort(const uint8_t* __restrict__ utf8,
                                                                  const int64_t* __restrict__ tok_off,
                                                                  const int64_t* __restrict__ doc_off, int64_t n_docs,
                                                                  int32_t nf, int32_t* __restrict__ keys,
@@ -245,8 +287,8 @@ __global__ __launch_bounds__(64 * kDocWaves) void k_doc_hash_sort(const uint8_t*
                                                                  int32_t* __restrict__ n_large,
                                                                  int32_t* __restrict__ n_medium) {
   const int lane = threadIdx.x & 63;
-  for (int64_t d = (int64_t)blockIdx.x * kDocWaves + (threadIdx.x >> 6); d < n_docs;
-       d += (int64_t)gridDim.x * kDocWaves) {
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar doc_off loads
+  for (int64_t d = (int64_t)blockIdx.x * kDocWaves + wv; d < n_docs; d += (int64_t)gridDim.x * kDocWaves) {
     const int64_t s = doc_off[d], n64 = doc_off[d + 1] - s;
     if (n64 > kFusedCap) {
       for (int64_t q = lane; q < n64; q += 64) {
@@ -266,6 +308,155 @@ __global__ __launch_bounds__(64 * kDocWaves) void k_doc_hash_sort(const uint8_t*
     else if (n <= 128) h = hash_sort_doc<SPARK24, 2>(utf8, tok_off, s, n, nf, sorted, lane);
     else h = hash_sort_doc<SPARK24, 4>(utf8, tok_off, s, n, nf, sorted, lane);
     if (lane == 0) nnz[d] = h;
+  }
+}
+
+// ---- single pass (round 4) for corpora whose documents all hold ≤ kFusedCap tokens (known at upload):
+// hash + register sort + CSR emission in one kernel, the row offsets from a decoupled look-back over
+// tiles of kDocWaves documents — no sorted-key array, no nnz scan, no second pass over the keys.
+// Workgroups take tiles in ticket order (an atomic counter), so every tile a look-back waits on has
+// already started and finishes: no dependence on dispatch order.  status[t] = flag << 62 | value
+// (flag 1: the tile's own entry count, 2: the inclusive count of tiles 0..t), written by one lane with
+// agent-scope atomic stores and read with agent-scope atomic loads (vector memory, L2-coherent).
+constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = kLbAgg - 1;
+
+// the exclusive entry count before `tile` (wave 0 of the workgroup; every lane returns it)
+// A bounded wait: a predecessor silent for ~2^20 polls (far beyond any tile's run time) sets *fault and the
+// look-back ends, so the grid always drains; the host then fails the call (STC_ERR_HIP).
+constexpr int kLbMaxPolls = 1 << 20;
+__device__ __forceinline__ int64_t tile_lookback(uint64_t* status, int64_t tile, int64_t agg, int lane,
+                                                 uint64_t* fault) {
+  if (tile == 0) {
+    if (lane == 0) __hip_atomic_store(&status[0], kLbInc | (uint64_t)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0) __hip_atomic_store(&status[tile], kLbAgg | (uint64_t)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int64_t excl = 0;
+  for (int64_t j = tile - 1;; j -= 64) {  // a window of 64 predecessors, closest in lane 0
+    const int64_t k = j - lane;
+    uint64_t v = k >= 0 ? __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbInc;
+    for (int polls = 0; __ballot((v >> 62) == 0); ++polls) {  // a predecessor not yet published: it is running
+      if (polls == kLbMaxPolls) {
+        if (lane == 0) __hip_atomic_store(fault, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = kLbInc;  // give up (the output is discarded)
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if ((v >> 62) == 0) v = __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint64_t inc = __ballot((v >> 62) == 2);
+    const int lp = inc ? __ffsll((unsigned long long)inc) - 1 : 63;  // the closest inclusive count
+    int64_t sum = lane <= lp ? (int64_t)(v & kLbVal) : 0;
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    excl += sum;
+    if (inc) break;
+  }
+  if (lane == 0) __hip_atomic_store(&status[tile], kLbInc | (uint64_t)(excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
+// one document's sorted keys (x[p] = element lane·P + p) → its distinct ids and run lengths at out0
+template <int P, typename V>
+__device__ __forceinline__ void emit_runs(const int32_t (&x)[4], int n, int lane, int64_t out0, int binary,
+                                          int32_t* __restrict__ idx, V* __restrict__ vals) {
+  const int32_t prev_last = __shfl_up(x[P - 1], 1, 64);
+  bool hd[P];
+  int hc = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int q = lane * P + p;
+    const int32_t prev = p == 0 ? prev_last : x[p - 1];
+    hd[p] = q < n && (q == 0 || x[p] != prev);
+    hc += hd[p] ? 1 : 0;
+  }
+  int inc = hc;  // inclusive lane prefix of the head counts
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  int first = n;  // this lane's first head position; then the first head after this lane
+#pragma unroll
+  for (int p = P - 1; p >= 0; --p)
+    if (hd[p]) first = lane * P + p;
+  int sm = first;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_down(sm, o, 64);
+    if (lane + o < 64) sm = min(sm, y);
+  }
+  int nx = __shfl_down(sm, 1, 64);
+  if (lane == 63) nx = n;
+  int nxt[P];
+#pragma unroll
+  for (int p = P - 1; p >= 0; --p) {
+    nxt[p] = nx;
+    if (hd[p]) nx = lane * P + p;
+  }
+  int64_t r = out0 + (inc - hc);
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+    if (hd[p]) {
+      idx[r] = x[p];
+      vals[r] = binary ? V(1) : V(nxt[p] - (lane * P + p));
+      ++r;
+    }
+}
+
+template <bool SPARK24, typename V>
+__global__ __launch_bounds__(64 * kDocWaves, 8) void k_doc_hash_emit(
+    const uint8_t* __restrict__ utf8, const int64_t* __restrict__ tok_off, const int64_t* __restrict__ doc_off,
+    int64_t n_docs, int32_t nf, int binary, int64_t* __restrict__ indptr, int32_t* __restrict__ idx,
+    V* __restrict__ vals, uint64_t* __restrict__ status, unsigned long long* __restrict__ ticket) {
+  __shared__ int tile_s;
+  __shared__ int64_t wn[kDocWaves];
+  __shared__ int64_t base_s;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t tiles = (n_docs + kDocWaves - 1) / kDocWaves;
+  for (;;) {
+    if (threadIdx.x == 0) tile_s = (int)atomicAdd(ticket, 1ull);
+    __syncthreads();
+    const int64_t tile = __builtin_amdgcn_readfirstlane(tile_s);
+    if (tile >= tiles) break;  // every workgroup gets here: the tickets only grow
+    const int64_t d = tile * kDocWaves + wv;
+    int32_t x[4] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX};
+    int n = 0, h = 0;
+    if (d < n_docs) {
+      const int64_t s = doc_off[d];
+      n = (int)(doc_off[d + 1] - s);
+      if (n <= 64) {
+        int32_t xp[1];
+        h = hash_sort_regs<SPARK24, 1>(utf8, tok_off, s, n, nf, xp, lane);
+        x[0] = xp[0];
+      } else if (n <= 128) {
+        int32_t xp[2];
+        h = hash_sort_regs<SPARK24, 2>(utf8, tok_off, s, n, nf, xp, lane);
+        x[0] = xp[0];
+        x[1] = xp[1];
+      } else {
+        int32_t xp[4];
+        h = hash_sort_regs<SPARK24, 4>(utf8, tok_off, s, n, nf, xp, lane);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) x[p] = xp[p];
+      }
+    }
+    if (lane == 0) wn[wv] = h;
+    __syncthreads();
+    int64_t agg = 0;
+#pragma unroll
+    for (int w = 0; w < kDocWaves; ++w) agg += wn[w];
+    if (wv == 0) {
+      const int64_t ex = tile_lookback(status, tile, agg, lane, status + tiles + 1);
+      if (lane == 0) base_s = ex;
+    }
+    __syncthreads();
+    int64_t out0 = base_s;
+    for (int w = 0; w < wv; ++w) out0 += wn[w];
+    if (d < n_docs) {
+      if (n <= 64) emit_runs<1, V>(x, n, lane, out0, binary, idx, vals);
+      else if (n <= 128) emit_runs<2, V>(x, n, lane, out0, binary, idx, vals);
+      else emit_runs<4, V>(x, n, lane, out0, binary, idx, vals);
+      if (lane == 0) indptr[d + 1] = out0 + h;
+    }
   }
 }
 
@@ -308,10 +499,12 @@ __device__ __forceinline__ void doc_runs(const int32_t* __restrict__ src, int64_
   int64_t done = 0;                  // runs started so far (wave-uniform)
   int64_t pend_start = -1, pend_slot = 0;
   int32_t last = 0;                  // the previous chunk's last key
+  int32_t key_n = lane < n ? src[s + lane] : 0;  // one chunk ahead: its load overlaps this chunk's work
   for (int64_t c0 = 0; c0 < n; c0 += 64) {
     const int64_t i = c0 + lane;
     const bool valid = i < n;
-    const int32_t key = valid ? src[s + i] : 0;
+    const int32_t key = key_n;
+    if (c0 + 64 < n) key_n = i + 64 < n ? src[s + i + 64] : 0;
     int32_t prev = __shfl_up(key, 1, 64);
     if (lane == 0) prev = last;
     const bool head = valid && (i == 0 || key != prev);
@@ -354,9 +547,9 @@ __global__ __launch_bounds__(64 * kDocWaves) void k_doc_runs(const int32_t* __re
                                                  int32_t* __restrict__ idx, V* __restrict__ vals,
                                                  int64_t* __restrict__ nnz) {
   const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar offset loads
   const int64_t count = EMIT ? n_docs : n_large;  // COUNT runs over the long documents only
-  for (int64_t w = (int64_t)blockIdx.x * kDocWaves + (threadIdx.x >> 6); w < count;
-       w += (int64_t)gridDim.x * kDocWaves) {
+  for (int64_t w = (int64_t)blockIdx.x * kDocWaves + wv; w < count; w += (int64_t)gridDim.x * kDocWaves) {
     const int64_t d = EMIT ? w : large[w];
     const int64_t s = doc_off[d], n = doc_off[d + 1] - s;
     const int32_t* src = (is_large && is_large[d]) ? sorted_l : sorted;
@@ -415,7 +608,7 @@ void row_order_by_df(Ctx& c, const DCsr& m, const int64_t* d_df, int32_t* d_orde
 
 void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t n_tok,
                const int64_t* d_doc_off, int64_t n_docs, int32_t num_features, int binary,
-               int variant, int value_dtype, DCsr& out) {
+               int variant, int value_dtype, int64_t max_doc, DCsr& out) {
   STC_REQUIRE(n_tok < (int64_t(1) << 31), "at most 2^31-1 tokens per call (split the corpus)");
   hipStream_t st = c.stream;
   out.rows = n_docs;
@@ -425,6 +618,42 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
   if (n_tok == 0) {
     HIP_CHECK(hipMemsetAsync(out.indptr.p, 0, sizeof(int64_t) * (n_docs + 1), st));
     out.nnz = 0;
+    return;
+  }
+  if (max_doc >= 0 && max_doc <= kFusedCap && c.single_pass_tf) {  // every document fits the register sort
+    const int64_t tiles = ceil_div(n_docs, (int64_t)kDocWaves);
+    DevBuf& lb = c.scratch[2];
+    lb.reserve(sizeof(uint64_t) * (tiles + 2));
+    uint64_t* status = lb.as<uint64_t>();  // [tiles] look-back words, then the ticket, then the fault word
+    auto* ticket = reinterpret_cast<unsigned long long*>(status + tiles);
+    HIP_CHECK(hipMemsetAsync(status, 0, sizeof(uint64_t) * (tiles + 2), st));
+    HIP_CHECK(hipMemsetAsync(out.indptr.p, 0, sizeof(int64_t), st));
+    // nnz ≤ n_tok: the output is sized before the counts exist
+    out.indices.reserve(sizeof(int32_t) * n_tok);
+    out.values.reserve((value_dtype == STC_F32 ? 4 : 8) * n_tok);
+    const unsigned g = (unsigned)std::min<int64_t>(tiles, (int64_t)c.cus * 8);  // ≤ the resident count
+    auto go = [&](auto spark, auto* vals) {
+      constexpr bool S24 = decltype(spark)::value;
+      k_doc_hash_emit<S24><<<g, 64 * kDocWaves, 0, st>>>(d_utf8, d_tok_off, d_doc_off, n_docs, num_features, binary,
+                                                          out.indptr.as<int64_t>(), out.indices.as<int32_t>(), vals,
+                                                          status, ticket);
+    };
+    if (value_dtype == STC_F32) {
+      if (variant == STC_HASH_SPARK24) go(std::true_type{}, out.values.as<float>());
+      else go(std::false_type{}, out.values.as<float>());
+    } else {
+      if (variant == STC_HASH_SPARK24) go(std::true_type{}, out.values.as<double>());
+      else go(std::false_type{}, out.values.as<double>());
+    }
+    KERNEL_CHECK();
+    int64_t total = 0;
+    uint64_t fault = 0;
+    HIP_CHECK(hipMemcpyAsync(&total, out.indptr.as<int64_t>() + n_docs, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(&fault, status + tiles + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (fault) throw Error(STC_ERR_HIP, "HashingTF: a row-offset look-back timed out (device oversubscribed?)");
+    out.nnz = total;
+    out.positive = true;
     return;
   }
   // grow-only scratch kept on the context (the featurisation of one corpus reuses it): no allocation,

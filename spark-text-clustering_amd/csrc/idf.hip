@@ -24,9 +24,10 @@ static int grid_for(int64_t n) {
 // df[j] = #entries (rows hold each id once) with id j and value > 0 (DocumentFrequencyAggregator.add).
 // A Zipf corpus's hot ids sit in almost every row, and device-scope atomics run at a few G/s, so
 // the histogram is built without per-entry global atomics:
-//  * numFeatures ≤ 2^18: vocabulary tiles of 2^15 ids.  k_df_bin splits each entry chunk by tile
-//    (one read of the CSR), k_df_binned counts a tile over a group of chunks in LDS (128 KB of u32)
-//    and writes its partial histogram, k_df_reduce sums the partials in group order.
+//  * numFeatures ≤ 2^18: vocabulary tiles of 2^15 ids counted in LDS (128 KB of u32) per chunk group,
+//    partial histograms summed in group order by k_df_reduce.  k_df_tiled (default) streams a group's
+//    ids once per tile from L2; k_df_bin + k_df_binned (round 3, STC_DF_BINNED=1) first split each
+//    chunk by tile into a u16 bin array.
 //  * larger vocabularies: the (value > 0) ids are radix-sorted and each run's [lo, hi) recorded.
 // Both are exact integer counts, identical run to run.
 constexpr int kTileBits = 15;
@@ -135,6 +136,74 @@ __global__ __launch_bounds__(kTileThreads) void k_df_binned(const uint16_t* __re
   for (int i = threadIdx.x; i < kTile && j0 + i < cols; i += kTileThreads) out[i] = cnt[i];
 }
 
+// Tiled variant (round 4, the default for numFeatures ≤ 2^18): no bin array.  Workgroup (g, t) streams
+// the whole index range of chunk group g and counts the ids of vocabulary tile t in LDS; the T
+// workgroups of one group are placed on one XCD (blockIdx % 8 picks the XCD) and start together, so
+// the group's indices come from HBM once and are re-read T times from that XCD's L2.  Bytes per
+// entry from HBM: 4 (id) [+ s (value) when not known positive]; one workgroup per CU (128 KB of LDS).
+constexpr int kTiledThreads = 1024;
+constexpr int kTiledUnroll = 4;  // int4 index loads in flight per thread
+
+__device__ __forceinline__ void tile_add(uint32_t* cnt, uint32_t id, uint32_t t) {
+  if ((id >> kTileBits) == t) atomicAdd(&cnt[id & (kTile - 1)], 1u);
+}
+
+template <typename V>
+__global__ __launch_bounds__(kTiledThreads) void k_df_tiled(const int32_t* __restrict__ idx,
+                                                            const V* __restrict__ val, int64_t nnz,
+                                                            int n_tiles, int64_t groups, int64_t per,
+                                                            int64_t cols, uint32_t* __restrict__ part) {
+  extern __shared__ uint32_t cnt[];
+  const int64_t b = blockIdx.x;
+  int t;
+  int64_t g;
+  if (groups % 8 == 0) {  // XCD-aware: the n_tiles workgroups of a group share blockIdx % 8
+    const int64_t l = b >> 3;
+    t = (int)(l % n_tiles);
+    g = (l / n_tiles) * 8 + (b & 7);
+  } else {
+    t = (int)(b % n_tiles);
+    g = b / n_tiles;
+  }
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kTile; i += kTiledThreads) cnt[i] = 0;
+  __syncthreads();
+  const int64_t e0 = g * per, e1 = e0 + per < nnz ? e0 + per : nnz;  // per % 4 == 0
+  const uint32_t ut = (uint32_t)t;
+  if (val == nullptr) {  // every value known > 0: ids only, 16-byte loads
+    const int4* i4 = reinterpret_cast<const int4*>(idx + e0);
+    const int64_t n4 = e1 > e0 ? (e1 - e0) >> 2 : 0;
+    int64_t q = tid;
+    for (; q + (kTiledUnroll - 1) * kTiledThreads < n4; q += kTiledUnroll * kTiledThreads) {
+      int4 v[kTiledUnroll];
+#pragma unroll
+      for (int u = 0; u < kTiledUnroll; ++u) v[u] = i4[q + u * kTiledThreads];
+#pragma unroll
+      for (int u = 0; u < kTiledUnroll; ++u) {
+        tile_add(cnt, (uint32_t)v[u].x, ut);
+        tile_add(cnt, (uint32_t)v[u].y, ut);
+        tile_add(cnt, (uint32_t)v[u].z, ut);
+        tile_add(cnt, (uint32_t)v[u].w, ut);
+      }
+    }
+    for (; q < n4; q += kTiledThreads) {
+      const int4 v = i4[q];
+      tile_add(cnt, (uint32_t)v.x, ut);
+      tile_add(cnt, (uint32_t)v.y, ut);
+      tile_add(cnt, (uint32_t)v.z, ut);
+      tile_add(cnt, (uint32_t)v.w, ut);
+    }
+    for (int64_t e = e0 + 4 * n4 + tid; e < e1; e += kTiledThreads) tile_add(cnt, (uint32_t)idx[e], ut);
+  } else {
+    for (int64_t e = e0 + tid; e < e1; e += kTiledThreads)
+      if (val[e] > V(0)) tile_add(cnt, (uint32_t)idx[e], ut);
+  }
+  __syncthreads();
+  const int64_t j0 = (int64_t)t * kTile;
+  uint32_t* out = part + g * cols + j0;
+  for (int i = tid; i < kTile && j0 + i < cols; i += kTiledThreads) out[i] = cnt[i];
+}
+
 __global__ __launch_bounds__(256) void k_df_reduce(const uint32_t* __restrict__ part, int64_t chunks, int64_t cols,
                                                    int64_t* __restrict__ df) {
   for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < cols; j += (int64_t)gridDim.x * 256) {
@@ -167,6 +236,37 @@ void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df) {
   hipStream_t s = c.stream;
   HIP_CHECK(hipMemsetAsync(d_df, 0, sizeof(int64_t) * m.cols, s));
   if (m.nnz == 0) return;
+  if (m.cols <= (int64_t(kMaxTiles) << kTileBits) && c.df_tiled) {
+    const int T = (int)ceil_div(m.cols, (int64_t)kTile);
+    // groups: a multiple of 8 (the XCD mapping) with T·groups ≈ one workgroup per CU, fewer for small
+    // inputs (≥ 64 Ki entries per group)
+    const int64_t want = std::max<int64_t>(1, (int64_t)c.cus / T);
+    int64_t G = std::min<int64_t>(want, ceil_div(m.nnz, (int64_t)65536));
+    if (G >= 8) G -= G % 8;
+    G = std::max<int64_t>(G, 1);
+    const int64_t per = ceil_div(ceil_div(m.nnz, G), (int64_t)4) * 4;
+    G = ceil_div(m.nnz, per);  // (rounding `per` up can leave G off a multiple of 8: the plain mapping)
+    DevBuf& part = c.scratch[0];
+    part.reserve(sizeof(uint32_t) * G * m.cols);
+    const size_t lds = sizeof(uint32_t) * kTile;
+    if (m.dtype == STC_F32) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)k_df_tiled<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+      k_df_tiled<float><<<(unsigned)(T * G), kTiledThreads, lds, s>>>(
+          m.indices.as<int32_t>(), m.positive ? nullptr : m.values.as<float>(), m.nnz, T, G, per, m.cols,
+          part.as<uint32_t>());
+    } else {
+      HIP_CHECK(hipFuncSetAttribute((const void*)k_df_tiled<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+      k_df_tiled<double><<<(unsigned)(T * G), kTiledThreads, lds, s>>>(
+          m.indices.as<int32_t>(), m.positive ? nullptr : m.values.as<double>(), m.nnz, T, G, per, m.cols,
+          part.as<uint32_t>());
+    }
+    KERNEL_CHECK();
+    k_df_reduce<<<grid_for(m.cols), 256, 0, s>>>(part.as<uint32_t>(), G, m.cols, d_df);
+    KERNEL_CHECK();
+    return;
+  }
   if (m.cols <= (int64_t(kMaxTiles) << kTileBits)) {
     const int T = (int)ceil_div(m.cols, (int64_t)kTile);
     const int64_t chunks = ceil_div(m.nnz, (int64_t)kBinChunk);
@@ -251,19 +351,38 @@ __device__ __forceinline__ V idf_scale(V v, double w, double zero_floor) {
   if (zero_floor > 0.0 && w == 0.0) w = zero_floor;
   return (V)((double)v * w);
 }
+// Round 4: two quads per thread and step with all their loads issued before any use, and the index
+// and value streams marked non-temporal so they do not evict the idf vector from L2.
 template <typename V>
 __global__ __launch_bounds__(256) void k_transform(const int32_t* __restrict__ idx, V* __restrict__ val,
                                                    int64_t nnz, const double* __restrict__ idf,
                                                    double zero_floor) {
+  typedef V V4 __attribute__((ext_vector_type(4)));
+  typedef int32_t I4 __attribute__((ext_vector_type(4)));
   const int64_t n4 = nnz / 4;
-  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n4; q += (int64_t)gridDim.x * 256) {
-    const int4 i = reinterpret_cast<const int4*>(idx)[q];
-    V* p = val + 4 * q;
-    const double w0 = idf[i.x], w1 = idf[i.y], w2 = idf[i.z], w3 = idf[i.w];
-    p[0] = idf_scale(p[0], w0, zero_floor);
-    p[1] = idf_scale(p[1], w1, zero_floor);
-    p[2] = idf_scale(p[2], w2, zero_floor);
-    p[3] = idf_scale(p[3], w3, zero_floor);
+  const int64_t S = (int64_t)gridDim.x * 256;
+  const I4* i4 = reinterpret_cast<const I4*>(idx);
+  V4* v4 = reinterpret_cast<V4*>(val);
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n4; q += 2 * S) {
+    const bool two = q + S < n4;
+    const I4 ia = __builtin_nontemporal_load(i4 + q);
+    const I4 ib = two ? __builtin_nontemporal_load(i4 + q + S) : I4{};
+    V4 a = __builtin_nontemporal_load(v4 + q);
+    V4 b = two ? __builtin_nontemporal_load(v4 + q + S) : V4{};
+    const double wa0 = idf[ia.x], wa1 = idf[ia.y], wa2 = idf[ia.z], wa3 = idf[ia.w];
+    const double wb0 = idf[ib.x], wb1 = idf[ib.y], wb2 = idf[ib.z], wb3 = idf[ib.w];
+    a.x = idf_scale(a.x, wa0, zero_floor);
+    a.y = idf_scale(a.y, wa1, zero_floor);
+    a.z = idf_scale(a.z, wa2, zero_floor);
+    a.w = idf_scale(a.w, wa3, zero_floor);
+    __builtin_nontemporal_store(a, v4 + q);
+    if (two) {
+      b.x = idf_scale(b.x, wb0, zero_floor);
+      b.y = idf_scale(b.y, wb1, zero_floor);
+      b.z = idf_scale(b.z, wb2, zero_floor);
+      b.w = idf_scale(b.w, wb3, zero_floor);
+      __builtin_nontemporal_store(b, v4 + q + S);
+    }
   }
   const int64_t e = 4 * n4 + (int64_t)blockIdx.x * 256 + threadIdx.x;  // the last nnz % 4 entries
   if (e < nnz) val[e] = idf_scale(val[e], idf[idx[e]], zero_floor);

@@ -42,7 +42,8 @@
 #define R64_RCP_NR 2  // Newton steps after v_rcp_f64 in that chain
 #endif
 #ifndef R64_MIRROR
-#define R64_MIRROR 1  // k > 64: the idle wave of the ψ wave's topic set computes Σ|Δγ| (off the ψ chain)
+#define R64_MIRROR 0  // 1 (k > 64): the idle wave of the ψ wave's topic set computes Σ|Δγ| off the ψ chain —
+                      // measured +1.3 % E-step on the headline (r04: 31.96 vs 31.54 ms), so off
 #endif
 #ifndef R64_LONG_OCC
 #define R64_LONG_OCC 1  // long-document kernel workgroups per CU the register budget is cut for

@@ -16,6 +16,10 @@
 
 namespace stc {
 
+// device UTF-8 token blobs are allocated this many bytes past their end: hashing_tf.hip reads each
+// token as a 32-byte window of whole aligned dwords from its aligned start
+constexpr int64_t kHashPad = 64;
+
 // ---------------------------------------------------------------------------------------
 // Errors: every entry point runs inside guard(); failures throw stc::Error and come back to
 // the caller as a status code + thread-local message (stc_last_error).  Never abort().
@@ -105,6 +109,9 @@ struct Ctx {
   LocalColl* local = nullptr;  // set instead of comm for same-device group members (owned by the group)
   int n_ranks = 1;
   int rank = 0;
+  int cus = 256;          // compute units (the df count sizes its grid to one workgroup per CU)
+  bool df_tiled = true;   // idf.hip doc_freq: the tiled count (false: the binned one, STC_DF_BINNED=1)
+  bool single_pass_tf = true;  // hashing_tf.hip: the look-back single pass when max_doc allows (STC_TF_TWO_PASS=1: off)
   DevBuf scratch[12];  // grow-only scratch of the featurisation kernels (hashing_tf.hip, idf.hip, api.hip IDF)
   DevBuf coll_tmp;    // the in-process all-reduce's staging buffer
   void use() const { HIP_CHECK(hipSetDevice(device)); }
@@ -481,7 +488,8 @@ void hash_tokens(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_
 void row_order_by_df(Ctx& c, const DCsr& m, const int64_t* d_df, int32_t* d_order);
 void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t n_tok,
                const int64_t* d_doc_off, int64_t n_docs, int32_t num_features, int binary,
-               int variant, int value_dtype, DCsr& out);
+               int variant, int value_dtype, int64_t max_doc /* longest document's tokens, −1 unknown */,
+               DCsr& out);
 }  // namespace hashing
 namespace tokenizer {
 // Spark ML Tokenizer on device: d_text/d_text_off (n_docs+1) in; lower-cased, separator-free blob,

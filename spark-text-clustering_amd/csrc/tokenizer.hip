@@ -313,7 +313,7 @@ void tokenize(Ctx& c, const uint8_t* d_text, const int64_t* d_text_off, int64_t 
   HIP_CHECK(hipStreamSynchronize(s));
   n_tok = h[0];
   n_out_bytes = h[1];
-  out_utf8.reserve(n_out_bytes + 16);  // k_hash reads whole aligned dwords past a token
+  out_utf8.reserve(n_out_bytes + kHashPad);  // the hash reads 32-byte windows of whole aligned dwords
   out_tok_off.reserve(8 * (n_tok + 1));
   if (n_docs > 0) {
     k_emit<<<grid_docs(n_docs), 64 * kWaves, 0, s>>>(d_text, d_text_off, n_docs,

@@ -169,7 +169,7 @@ def test_hashing_tf_document_lengths(ctx, oracle, nf):
 def test_idf_doc_freq_zipf_hot_ids(ctx, V):
     """doc_freq: heavy-hitter document frequencies on a Zipf corpus (hot ids in every row, more
     distinct ids per workgroup slice than LDS slots) equal the exact column counts of positive values;
-    2^18 buckets take the binned LDS vocabulary tiles, 2^20 and 2^21 the radix-sorted runs."""
+    2^18 buckets take the LDS vocabulary tiles, 2^20 and 2^21 the radix-sorted runs."""
     import stc
     from stc import synth
 
@@ -181,3 +181,66 @@ def test_idf_doc_freq_zipf_hot_ids(ctx, V):
     df = np.bincount(tf.indices[vals > 0], minlength=tf.num_cols)
     assert np.array_equal(m.docFreq, df)
     assert m.numDocs == tf.num_rows
+
+
+@pytest.mark.parametrize("V", [1000, (1 << 15) + 3, 1 << 18])
+@pytest.mark.parametrize("D", [3, 7001])
+def test_idf_doc_freq_tiled_and_binned(ctx, monkeypatch, V, D):
+    """doc_freq's two LDS-tile counts (idf.hip: k_df_tiled, the default, one XCD's workgroups sharing a
+    chunk group's index stream; k_df_bin + k_df_binned under STC_DF_BINNED=1) and HashingTF's single
+    look-back pass vs its sorted-key passes (STC_TF_TWO_PASS=1, same CSR) on a device-resident
+    HashingTF matrix (values known positive: indices only) and on an uploaded matrix with explicit zeros
+    (values read): exact column counts, with group counts that do and do not fill the XCD mapping."""
+    import stc
+    from stc import synth
+
+    monkeypatch.setenv("STC_DF_BINNED", "1")
+    monkeypatch.setenv("STC_TF_TWO_PASS", "1")
+    ctx_b = stc.Context(ctx.device)  # reads the knobs at stc_init
+    monkeypatch.delenv("STC_DF_BINNED")
+    monkeypatch.delenv("STC_TF_TWO_PASS")
+    (blob, tok_off, doc_off), _ = synth.token_corpus(D, 150, n_words=40000, seed=11)
+    csr = []
+    for c in (ctx, ctx_b):
+        dt = stc.DeviceTokens(c, blob, tok_off, doc_off)
+        d = stc.HashingTF(numFeatures=V, ctx=c).transform_tokens_device(dt)
+        host = d.download()
+        csr.append(host)
+        m = stc.IDF(minDocFreq=0, ctx=c).fit_device(d)
+        assert np.array_equal(m.docFreq, np.bincount(host.indices, minlength=V))
+        vals = host.values.copy()
+        vals[::5] = 0.0  # explicit zeros do not count
+        m2 = stc.IDF(minDocFreq=0, ctx=c).fit(stc.CsrMatrix(host.indptr, host.indices, vals, V))
+        assert np.array_equal(m2.docFreq, np.bincount(host.indices[vals > 0], minlength=V))
+        m.free()
+        d.free()
+        dt.free()
+    ctx_b.close()
+    # HashingTF's single look-back pass (default) and the round-3 passes give the same CSR
+    a, b = csr
+    assert np.array_equal(a.indptr, b.indptr) and np.array_equal(a.indices, b.indices)
+    assert np.array_equal(a.values, b.values)
+
+
+@pytest.mark.parametrize("algo,variant", [("murmur3", 0), ("murmur3-spark24", 1)])
+def test_hash_window_lengths_and_alignments(ctx, oracle, algo, variant):
+    """The 32-byte hash window (hashing_tf.hip load_win / murmur3_win): every token length 0–70 characters (1–2 UTF-8 bytes each)
+    (inside the window, at its edge and past it) at every start alignment, in documents the fused
+    hash + sort pass takes (≤ 256 tokens) and through stc_hash_tokens; the last token ends the blob."""
+    import stc
+
+    rng = np.random.default_rng(12)
+    docs = []
+    for pre in range(4):  # shifts every later token's start by pre bytes
+        doc = ["p" * pre] if pre else []
+        for n in range(71):
+            doc.append(bytes(rng.integers(1, 256, n, dtype=np.uint8)).decode("latin-1"))
+        docs.append(doc)
+    htf = stc.HashingTF(numFeatures=1 << 18, hashAlgorithm=algo, ctx=ctx)
+    out = htf.transform(docs)
+    ip, ix, vv = oracle.hashing_tf(docs, 1 << 18, False, variant)
+    assert np.array_equal(out.indptr, ip) and np.array_equal(out.indices, ix) and np.array_equal(out.values, vv)
+    terms = [t for d in docs for t in d]
+    got = htf.indices_of(terms)
+    exp = [oracle.non_negative_mod(oracle.murmur3_x86_32(t.encode(), 42, variant), 1 << 18) for t in terms]
+    assert np.array_equal(got, np.asarray(exp, np.int32))

@@ -1,9 +1,11 @@
 #!/bin/bash
-# Featurisation A/B: the featurisation-only bench line with the current library and (OLD_LIB) an earlier
-# build, then rocprofv3 kernel stats of the featurisation pass.  One time limit per step.
+# featurisation: parity tests, the bench line (default vs STC_DF_BINNED=1), a kernel profile; optional ubench
 mkdir -p gpurun_out; : > gpurun_out/status.log
 step() { local name=$1 secs=$2; shift 2; timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc" >> gpurun_out/status.log; if [ $rc -ne 0 ]; then exit $rc; fi; }
-step t_feat 300 python -u -m pytest tests/test_gpu_feature.py tests/test_gpu_tokenizer.py -x -q -m gpu --timeout 150 --timeout-method thread
-step f_new 300 python bench.py --featurisation-only
-if [ -n "$OLD_LIB" ]; then step f_old 300 env STC_LIB=$OLD_LIB python bench.py --featurisation-only; fi
-step proff 400 env PROF_PASSES="stats" BENCH_ARGS="--featurisation-only" PROF_OUT=gpurun_out/proff bash tools/gpu_prof.sh
+step t_feat 400 python -u -m pytest ${TESTS:-tests/test_gpu_feature.py} -x -v -m gpu --timeout 150 --timeout-method thread
+step feat 300 python bench.py --featurisation-only --steps 5
+step feat_old 300 env STC_DF_BINNED=1 STC_TF_TWO_PASS=1 python bench.py --featurisation-only --steps 5
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+rm -rf gpurun_out/featprof
+step featprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/featprof -o fp --output-format csv -- python3 bench.py --featurisation-only --steps 3 --workers 1
+if [ -n "$UBENCH" ]; then step ubench 120 ./tools/ubench_f64; fi

@@ -25,7 +25,7 @@ __device__ __forceinline__ unsigned long long now() {
 }
 
 enum Op { FMA_DEP, FMA_IND8, RCP_DEP, PSI_S, PSI_S_X2, PSI_FAST, LDS_DEP, WSUM, BARRIER, RCPNR_DEP, PSI_V2_2, PSI_V2_1,
-          PKFMA_IND8 };
+          PKFMA_IND8, FMA_BANK_SAME, FMA_BANK_SPLIT, FMA_SHARED_E };
 
 template <int OP>
 __global__ void k_bench(double* out, unsigned long long* cyc, double a, double b) {
@@ -90,6 +90,34 @@ __global__ void k_bench(double* out, unsigned long long* cyc, double a, double b
         for (int j = 0; j < 8; ++j) asm volatile("v_pk_fma_f32 %0, %0, %1, %2" : "+v"(p[j]) : "v"(fa), "v"(fb));
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] = p[j].x + p[j].y;
+    } else if (OP == FMA_BANK_SAME || OP == FMA_BANK_SPLIT || OP == FMA_SHARED_E) {
+      // register-bank patterns of the E-step's v_fmac_f64 acc, B, e: explicit VGPRs (v64+ is free here)
+      // SAME: acc, B, e all start on a bank ≡ 0 (mod 4); SPLIT: acc ≡ 0, B ≡ 2, e ≡ 0 (B on the other
+      // bank pair); SHARED_E: the kernel's shape — 8 accumulators, 8 B, one e for all
+#pragma unroll 4
+      for (int i = 0; i < kN / 8; ++i) {
+        if (OP == FMA_BANK_SAME)
+          asm volatile(
+              "v_fmac_f64 v[64:65], v[96:97], v[128:129]\n v_fmac_f64 v[68:69], v[100:101], v[132:133]\n"
+              "v_fmac_f64 v[72:73], v[104:105], v[136:137]\n v_fmac_f64 v[76:77], v[108:109], v[140:141]\n"
+              "v_fmac_f64 v[80:81], v[112:113], v[144:145]\n v_fmac_f64 v[84:85], v[116:117], v[148:149]\n"
+              "v_fmac_f64 v[88:89], v[120:121], v[152:153]\n v_fmac_f64 v[92:93], v[124:125], v[156:157]" ::
+                  : "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159");
+        else if (OP == FMA_BANK_SPLIT)
+          asm volatile(
+              "v_fmac_f64 v[64:65], v[98:99], v[128:129]\n v_fmac_f64 v[68:69], v[102:103], v[132:133]\n"
+              "v_fmac_f64 v[72:73], v[106:107], v[136:137]\n v_fmac_f64 v[76:77], v[110:111], v[140:141]\n"
+              "v_fmac_f64 v[80:81], v[114:115], v[144:145]\n v_fmac_f64 v[84:85], v[118:119], v[148:149]\n"
+              "v_fmac_f64 v[88:89], v[122:123], v[152:153]\n v_fmac_f64 v[92:93], v[126:127], v[156:157]" ::
+                  : "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159");
+        else
+          asm volatile(
+              "v_fmac_f64 v[64:65], v[98:99], v[128:129]\n v_fmac_f64 v[68:69], v[102:103], v[128:129]\n"
+              "v_fmac_f64 v[72:73], v[106:107], v[128:129]\n v_fmac_f64 v[76:77], v[110:111], v[128:129]\n"
+              "v_fmac_f64 v[80:81], v[114:115], v[128:129]\n v_fmac_f64 v[84:85], v[118:119], v[128:129]\n"
+              "v_fmac_f64 v[88:89], v[122:123], v[128:129]\n v_fmac_f64 v[92:93], v[126:127], v[128:129]" ::
+                  : "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159");
+      }
     } else if (OP == PSI_FAST) {
 #pragma unroll 2
       for (int i = 0; i < kN / 16; ++i) {
@@ -195,6 +223,9 @@ int main() {
     run<PSI_V2_2>("exp_digamma_minus_v2_nr2_dependent", w, d_out, d_cyc);
     run<PSI_V2_1>("exp_digamma_minus_v2_nr1_dependent", w, d_out, d_cyc);
     run<PKFMA_IND8>("pk_fma_f32_8_independent", w, d_out, d_cyc);
+    run<FMA_BANK_SAME>("fmac_f64_banks_same", w, d_out, d_cyc);
+    run<FMA_BANK_SPLIT>("fmac_f64_banks_split", w, d_out, d_cyc);
+    run<FMA_SHARED_E>("fmac_f64_shared_e", w, d_out, d_cyc);
     run<LDS_DEP>("ds_read_b128_dependent", w, d_out, d_cyc);
     run<WSUM>("wave_sum_d_dependent", w, d_out, d_cyc);
     run<BARRIER>("s_barrier", w, d_out, d_cyc);
