@@ -1084,6 +1084,8 @@ int stc_init(int device, stc_ctx** out) {
     c->df_tiled = !(db && db[0] == '1');
     const char* tp = std::getenv("STC_TF_TWO_PASS");  // A/B knob: the round-3 HashingTF passes
     c->single_pass_tf = !(tp && tp[0] == '1');
+    const char* nc = std::getenv("STC_IDF_NO_CACHE");  // A/B knob: plain idf gathers in the transform
+    c->idf_cache = !(nc && nc[0] == '1');
     *out = c.release();
   });
 }
@@ -1420,6 +1422,7 @@ struct stc_didf {
   int device = -1;
   int64_t cols = 0, m = 0;
   DevBuf idf, df;
+  DevBuf cache;  // the hot-idf table of idf.hip k_transform_cached (empty: not used)
 };
 
 namespace {
@@ -1477,6 +1480,7 @@ int stc_idf_fit_dev(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, stc_
     md->device = ctx->device;
     md->cols = tf->cols;
     idf_fit_impl(*ctx, *tf, min_doc_freq, md->df, md->idf, md->m);
+    idf::build_cache(*ctx, md->df.as<int64_t>(), md->idf.as<double>(), md->cols, md->cache);
     *out = md.release();  // (the stream orders every later use of the model after the fit)
   });
 }
@@ -1501,7 +1505,7 @@ int stc_idf_transform_dev(stc_ctx* ctx, stc_dcsr* tf, const stc_didf* md, double
     STC_REQUIRE(tf->cols == md->cols, "vector size does not match the IDF size");
     STC_REQUIRE(zero_floor >= 0.0, "zero_floor must be >= 0");
     ctx->use();
-    idf::transform(*ctx, *tf, md->idf.as<double>(), zero_floor);
+    idf::transform(*ctx, *tf, md->idf.as<double>(), zero_floor, &md->cache);
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
   });
 }

@@ -324,13 +324,18 @@ constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = kLbAgg - 1
 // A bounded wait: a predecessor silent for ~2^20 polls (far beyond any tile's run time) sets *fault and the
 // look-back ends, so the grid always drains; the host then fails the call (STC_ERR_HIP).
 constexpr int kLbMaxPolls = 1 << 20;
+
+// publish a tile's own entry count (tile 0: its inclusive count) — never waits
+__device__ __forceinline__ void tile_publish(uint64_t* status, int64_t tile, int64_t agg) {
+  __hip_atomic_store(&status[tile], (tile == 0 ? kLbInc : kLbAgg) | (uint64_t)agg, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the exclusive entry count before `tile` (one wave; every lane returns it), then the tile's inclusive
+// count published.  Waits only for predecessors' own counts, which tile_publish writes unconditionally.
 __device__ __forceinline__ int64_t tile_lookback(uint64_t* status, int64_t tile, int64_t agg, int lane,
                                                  uint64_t* fault) {
-  if (tile == 0) {
-    if (lane == 0) __hip_atomic_store(&status[0], kLbInc | (uint64_t)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return 0;
-  }
-  if (lane == 0) __hip_atomic_store(&status[tile], kLbAgg | (uint64_t)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tile == 0) return 0;
   int64_t excl = 0;
   for (int64_t j = tile - 1;; j -= 64) {  // a window of 64 predecessors, closest in lane 0
     const int64_t k = j - lane;
@@ -401,62 +406,98 @@ __device__ __forceinline__ void emit_runs(const int32_t (&x)[4], int n, int lane
     }
 }
 
+// Pipelined one tile deep: a workgroup publishes tile t's count as soon as its documents are sorted, hashes
+// and sorts its next tile, and only then resolves t's offset and emits t — by then t's predecessors have
+// published, so the look-back seldom waits (the unpipelined form idled ~40 % of the time there).
+#ifndef TF_EMIT_OCC
+#define TF_EMIT_OCC 7  // waves per SIMD: 72 VGPRs; 8 spills two
+#endif
+#ifndef TF_EMIT_WAVES
+#define TF_EMIT_WAVES 4  // documents per tile (one per wave): one ticket and one look-back per tile
+#endif
+constexpr int kEmitWaves = TF_EMIT_WAVES;
+template <int P>
+__device__ __forceinline__ void take(int32_t (&x)[4], const int32_t (&xp)[P]) {
+#pragma unroll
+  for (int p = 0; p < P; ++p) x[p] = xp[p];
+}
+
 template <bool SPARK24, typename V>
-__global__ __launch_bounds__(64 * kDocWaves, 8) void k_doc_hash_emit(
+__global__ __launch_bounds__(64 * kEmitWaves, TF_EMIT_OCC) void k_doc_hash_emit(
     const uint8_t* __restrict__ utf8, const int64_t* __restrict__ tok_off, const int64_t* __restrict__ doc_off,
     int64_t n_docs, int32_t nf, int binary, int64_t* __restrict__ indptr, int32_t* __restrict__ idx,
     V* __restrict__ vals, uint64_t* __restrict__ status, unsigned long long* __restrict__ ticket) {
   __shared__ int tile_s;
-  __shared__ int64_t wn[kDocWaves];
+  __shared__ int wn[kEmitWaves];
   __shared__ int64_t base_s;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t tiles = (n_docs + kDocWaves - 1) / kDocWaves;
+  const int64_t tiles = (n_docs + kEmitWaves - 1) / kEmitWaves;
+  // the previous tile, sorted and published, awaiting its offset
+  int64_t tp = -1;
+  int32_t xq[4];
+  int nq = 0, hq = 0, preq = 0, aggq = 0;
   for (;;) {
     if (threadIdx.x == 0) tile_s = (int)atomicAdd(ticket, 1ull);
     __syncthreads();
     const int64_t tile = __builtin_amdgcn_readfirstlane(tile_s);
-    if (tile >= tiles) break;  // every workgroup gets here: the tickets only grow
-    const int64_t d = tile * kDocWaves + wv;
+    const bool have = tile < tiles;  // the tickets only grow: once past the end, the loop drains tp and exits
+    if (!have && tp < 0) break;
     int32_t x[4] = {INT32_MAX, INT32_MAX, INT32_MAX, INT32_MAX};
-    int n = 0, h = 0;
-    if (d < n_docs) {
-      const int64_t s = doc_off[d];
-      n = (int)(doc_off[d + 1] - s);
-      if (n <= 64) {
-        int32_t xp[1];
-        h = hash_sort_regs<SPARK24, 1>(utf8, tok_off, s, n, nf, xp, lane);
-        x[0] = xp[0];
-      } else if (n <= 128) {
-        int32_t xp[2];
-        h = hash_sort_regs<SPARK24, 2>(utf8, tok_off, s, n, nf, xp, lane);
-        x[0] = xp[0];
-        x[1] = xp[1];
-      } else {
-        int32_t xp[4];
-        h = hash_sort_regs<SPARK24, 4>(utf8, tok_off, s, n, nf, xp, lane);
+    int n = 0, h = 0, pre = 0, agg = 0;
+    if (have) {
+      const int64_t d = tile * kEmitWaves + wv;
+      if (d < n_docs) {
+        const int64_t s = doc_off[d];
+        n = (int)(doc_off[d + 1] - s);
+        if (n <= 64) {
+          int32_t xp[1];
+          h = hash_sort_regs<SPARK24, 1>(utf8, tok_off, s, n, nf, xp, lane);
+          take<1>(x, xp);
+        } else if (n <= 128) {
+          int32_t xp[2];
+          h = hash_sort_regs<SPARK24, 2>(utf8, tok_off, s, n, nf, xp, lane);
+          take<2>(x, xp);
+        } else {
+          int32_t xp[4];
+          h = hash_sort_regs<SPARK24, 4>(utf8, tok_off, s, n, nf, xp, lane);
+          take<4>(x, xp);
+        }
+      }
+      if (lane == 0) wn[wv] = h;
+    }
+    __syncthreads();
+    if (have) {
 #pragma unroll
-        for (int p = 0; p < 4; ++p) x[p] = xp[p];
+      for (int w = 0; w < kEmitWaves; ++w) {
+        const int c = wn[w];
+        pre += w < wv ? c : 0;
+        agg += c;
+      }
+      if (threadIdx.x == 0) tile_publish(status, tile, agg);
+    }
+    if (tp >= 0) {
+      if (wv == 0) {
+        const int64_t ex = tile_lookback(status, tp, aggq, lane, status + tiles + 1);
+        if (lane == 0) base_s = ex;
+      }
+      __syncthreads();
+      const int64_t d = tp * kEmitWaves + wv;
+      if (d < n_docs) {
+        const int64_t out0 = base_s + preq;
+        if (nq <= 64) emit_runs<1, V>(xq, nq, lane, out0, binary, idx, vals);
+        else if (nq <= 128) emit_runs<2, V>(xq, nq, lane, out0, binary, idx, vals);
+        else emit_runs<4, V>(xq, nq, lane, out0, binary, idx, vals);
+        if (lane == 0) indptr[d + 1] = out0 + hq;
       }
     }
-    if (lane == 0) wn[wv] = h;
-    __syncthreads();
-    int64_t agg = 0;
+    tp = have ? tile : -1;
 #pragma unroll
-    for (int w = 0; w < kDocWaves; ++w) agg += wn[w];
-    if (wv == 0) {
-      const int64_t ex = tile_lookback(status, tile, agg, lane, status + tiles + 1);
-      if (lane == 0) base_s = ex;
-    }
-    __syncthreads();
-    int64_t out0 = base_s;
-    for (int w = 0; w < wv; ++w) out0 += wn[w];
-    if (d < n_docs) {
-      if (n <= 64) emit_runs<1, V>(x, n, lane, out0, binary, idx, vals);
-      else if (n <= 128) emit_runs<2, V>(x, n, lane, out0, binary, idx, vals);
-      else emit_runs<4, V>(x, n, lane, out0, binary, idx, vals);
-      if (lane == 0) indptr[d + 1] = out0 + h;
-    }
+    for (int p = 0; p < 4; ++p) xq[p] = x[p];
+    nq = n;
+    hq = h;
+    preq = pre;
+    aggq = agg;
   }
 }
 
@@ -621,7 +662,7 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
     return;
   }
   if (max_doc >= 0 && max_doc <= kFusedCap && c.single_pass_tf) {  // every document fits the register sort
-    const int64_t tiles = ceil_div(n_docs, (int64_t)kDocWaves);
+    const int64_t tiles = ceil_div(n_docs, (int64_t)kEmitWaves);
     DevBuf& lb = c.scratch[2];
     lb.reserve(sizeof(uint64_t) * (tiles + 2));
     uint64_t* status = lb.as<uint64_t>();  // [tiles] look-back words, then the ticket, then the fault word
@@ -631,10 +672,10 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
     // nnz ≤ n_tok: the output is sized before the counts exist
     out.indices.reserve(sizeof(int32_t) * n_tok);
     out.values.reserve((value_dtype == STC_F32 ? 4 : 8) * n_tok);
-    const unsigned g = (unsigned)std::min<int64_t>(tiles, (int64_t)c.cus * 8);  // ≤ the resident count
+    const unsigned g = (unsigned)std::min<int64_t>(tiles, (int64_t)c.cus * TF_EMIT_OCC * 4 / kEmitWaves);
     auto go = [&](auto spark, auto* vals) {
       constexpr bool S24 = decltype(spark)::value;
-      k_doc_hash_emit<S24><<<g, 64 * kDocWaves, 0, st>>>(d_utf8, d_tok_off, d_doc_off, n_docs, num_features, binary,
+      k_doc_hash_emit<S24><<<g, 64 * kEmitWaves, 0, st>>>(d_utf8, d_tok_off, d_doc_off, n_docs, num_features, binary,
                                                           out.indptr.as<int64_t>(), out.indices.as<int32_t>(), vals,
                                                           status, ticket);
     };

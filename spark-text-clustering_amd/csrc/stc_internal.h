@@ -111,7 +111,8 @@ struct Ctx {
   int rank = 0;
   int cus = 256;          // compute units (the df count sizes its grid to one workgroup per CU)
   bool df_tiled = true;   // idf.hip doc_freq: the tiled count (false: the binned one, STC_DF_BINNED=1)
-  bool single_pass_tf = true;  // hashing_tf.hip: the look-back single pass when max_doc allows (STC_TF_TWO_PASS=1: off)
+  bool single_pass_tf = true;
+  bool idf_cache = true;  // idf.hip: the device IDF model's hot-idf LDS table (STC_IDF_NO_CACHE=1: off)  // hashing_tf.hip: the look-back single pass when max_doc allows (STC_TF_TWO_PASS=1: off)
   DevBuf scratch[12];  // grow-only scratch of the featurisation kernels (hashing_tf.hip, idf.hip, api.hip IDF)
   DevBuf coll_tmp;    // the in-process all-reduce's staging buffer
   void use() const { HIP_CHECK(hipSetDevice(device)); }
@@ -502,7 +503,10 @@ void tokenize(Ctx& c, const uint8_t* d_text, const int64_t* d_text_off, int64_t 
 namespace idf {
 void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df /* cols */);
 void finalize(Ctx& c, const int64_t* d_df, int64_t cols, int64_t m, int64_t min_df, double* d_idf);
-void transform(Ctx& c, DCsr& m, const double* d_idf, double zero_floor);
+// cache: the hot-idf table build_cache made for this idf (nullptr: plain gathers)
+void transform(Ctx& c, DCsr& m, const double* d_idf, double zero_floor, const DevBuf* cache = nullptr);
+// the device IDF model's hot-idf table (false, cache untouched: vocabulary too large or disabled)
+bool build_cache(Ctx& c, const int64_t* d_df, const double* d_idf, int64_t cols, DevBuf& cache);
 }  // namespace idf
 
 }  // namespace stc

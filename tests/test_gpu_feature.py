@@ -188,7 +188,8 @@ def test_idf_doc_freq_zipf_hot_ids(ctx, V):
 def test_idf_doc_freq_tiled_and_binned(ctx, monkeypatch, V, D):
     """doc_freq's two LDS-tile counts (idf.hip: k_df_tiled, the default, one XCD's workgroups sharing a
     chunk group's index stream; k_df_bin + k_df_binned under STC_DF_BINNED=1) and HashingTF's single
-    look-back pass vs its sorted-key passes (STC_TF_TWO_PASS=1, same CSR) on a device-resident
+    look-back pass vs its sorted-key passes (STC_TF_TWO_PASS=1, same CSR), and the transform with the
+    model's hot-idf LDS table (default) and without it (STC_IDF_NO_CACHE=1) on a device-resident
     HashingTF matrix (values known positive: indices only) and on an uploaded matrix with explicit zeros
     (values read): exact column counts, with group counts that do and do not fill the XCD mapping."""
     import stc
@@ -196,9 +197,10 @@ def test_idf_doc_freq_tiled_and_binned(ctx, monkeypatch, V, D):
 
     monkeypatch.setenv("STC_DF_BINNED", "1")
     monkeypatch.setenv("STC_TF_TWO_PASS", "1")
+    monkeypatch.setenv("STC_IDF_NO_CACHE", "1")
     ctx_b = stc.Context(ctx.device)  # reads the knobs at stc_init
-    monkeypatch.delenv("STC_DF_BINNED")
-    monkeypatch.delenv("STC_TF_TWO_PASS")
+    for k in ("STC_DF_BINNED", "STC_TF_TWO_PASS", "STC_IDF_NO_CACHE"):
+        monkeypatch.delenv(k)
     (blob, tok_off, doc_off), _ = synth.token_corpus(D, 150, n_words=40000, seed=11)
     csr = []
     for c in (ctx, ctx_b):
@@ -208,6 +210,10 @@ def test_idf_doc_freq_tiled_and_binned(ctx, monkeypatch, V, D):
         csr.append(host)
         m = stc.IDF(minDocFreq=0, ctx=c).fit_device(d)
         assert np.array_equal(m.docFreq, np.bincount(host.indices, minlength=V))
+        # the transform through the model's hot-idf LDS table (tag hits and misses) == host idf gathers
+        m.transform_device(d, zero_floor=1e-4)
+        w = np.where(m.idf == 0.0, 1e-4, m.idf)
+        np.testing.assert_array_equal(d.download().values, host.values * w[host.indices])
         vals = host.values.copy()
         vals[::5] = 0.0  # explicit zeros do not count
         m2 = stc.IDF(minDocFreq=0, ctx=c).fit(stc.CsrMatrix(host.indptr, host.indices, vals, V))
