@@ -37,6 +37,7 @@ struct stc_dtok {
   DevBuf utf8, tok_off, doc_off;
   int64_t n_bytes = 0, n_tok = 0, n_docs = 0;
   int64_t max_doc = -1;  // the longest document's token count (from the upload's offsets)
+  bool off32 = false;    // tok_off holds u32 offsets (blob + padding < 4 GiB), else int64
 };
 
 // ---------------------------------------------------------------------------------------
@@ -1082,8 +1083,10 @@ int stc_init(int device, stc_ctx** out) {
     HIP_CHECK(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device));
     const char* db = std::getenv("STC_DF_BINNED");  // A/B knob: the round-3 binned df count
     c->df_tiled = !(db && db[0] == '1');
-    const char* tp = std::getenv("STC_TF_TWO_PASS");  // A/B knob: the round-3 HashingTF passes
-    c->single_pass_tf = !(tp && tp[0] == '1');
+    const char* tm = std::getenv("STC_TF_MODE");  // A/B knob: HashingTF's structure (stc_internal.h Ctx)
+    if (tm && tm[0] >= '0' && tm[0] <= '2' && tm[1] == 0) c->tf_mode = tm[0] - '0';
+    const char* tf = std::getenv("STC_TF_FAULT");  // test knob
+    c->tf_force_fault = tf && tf[0] == '1';
     const char* nc = std::getenv("STC_IDF_NO_CACHE");  // A/B knob: plain idf gathers in the transform
     c->idf_cache = !(nc && nc[0] == '1');
     *out = c.release();
@@ -1262,8 +1265,15 @@ int stc_tokens_upload(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const 
     HIP_CHECK(hipStreamSynchronize(ctx->stream));
     std::swap(t->utf8.p, u.utf8.p);
     std::swap(t->utf8.bytes, u.utf8.bytes);
-    std::swap(t->tok_off.p, u.tok_off.p);
-    std::swap(t->tok_off.bytes, u.tok_off.bytes);
+    if (n_bytes + kHashPad <= (int64_t(1) << 32)) {  // u32 offsets: half the bytes HashingTF reads for them
+      t->tok_off.reserve(4 * (n_tok + 1));
+      hashing::narrow_offsets(*ctx, u.tok_off.as<int64_t>(), n_tok + 1, t->tok_off.as<uint32_t>());
+      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      t->off32 = true;
+    } else {
+      std::swap(t->tok_off.p, u.tok_off.p);
+      std::swap(t->tok_off.bytes, u.tok_off.bytes);
+    }
     std::swap(t->doc_off.p, u.doc_off.p);
     std::swap(t->doc_off.bytes, u.doc_off.bytes);
     t->n_bytes = n_bytes;
@@ -1294,7 +1304,8 @@ int stc_hashing_tf_tokens(stc_ctx* ctx, const stc_dtok* tokens, int32_t num_feat
     auto m = std::make_unique<stc_dcsr>();
     m->ctx = ctx;
     m->device = ctx->device;
-    hashing::build_csr(*ctx, tokens->utf8.as<uint8_t>(), tokens->tok_off.as<int64_t>(), tokens->n_tok,
+    hashing::build_csr(*ctx, tokens->utf8.as<uint8_t>(), tokens->off32 ? nullptr : tokens->tok_off.as<int64_t>(),
+                       tokens->off32 ? tokens->tok_off.as<uint32_t>() : nullptr, tokens->n_tok,
                        tokens->doc_off.as<int64_t>(), tokens->n_docs, num_features, binary, hash_variant,
                        value_dtype, tokens->max_doc, *m);
     *out = m.release();
@@ -1333,7 +1344,7 @@ int stc_hashing_tf_dev(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const
     auto m = std::make_unique<stc_dcsr>();
     m->ctx = ctx;
     m->device = ctx->device;
-    hashing::build_csr(*ctx, u.utf8.as<uint8_t>(), u.tok_off.as<int64_t>(), n_tok, u.doc_off.as<int64_t>(),
+    hashing::build_csr(*ctx, u.utf8.as<uint8_t>(), u.tok_off.as<int64_t>(), nullptr, n_tok, u.doc_off.as<int64_t>(),
                        n_docs, num_features, binary, hash_variant, value_dtype, u.max_doc, *m);
     *out = m.release();
   });
@@ -1408,7 +1419,7 @@ int stc_tokenize_hashing_tf_dev(stc_ctx* ctx, const uint8_t* text, int64_t n_byt
     auto m = std::make_unique<stc_dcsr>();
     m->ctx = ctx;
     m->device = ctx->device;
-    hashing::build_csr(*ctx, t.utf8.as<uint8_t>(), t.tok_off.as<int64_t>(), t.n_tok, t.doc_off.as<int64_t>(),
+    hashing::build_csr(*ctx, t.utf8.as<uint8_t>(), t.tok_off.as<int64_t>(), nullptr, t.n_tok, t.doc_off.as<int64_t>(),
                        n_docs, num_features, binary, hash_variant, value_dtype, -1, *m);
     *out = m.release();
   });

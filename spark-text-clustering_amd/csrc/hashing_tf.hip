@@ -97,27 +97,29 @@ __device__ __forceinline__ int32_t murmur3(const uint8_t* p, uint32_t n) {
 }
 
 // four tokens per thread and step, a grid stride apart (neighbouring lanes keep neighbouring tokens,
-// so the byte loads stay coalesced) — four independent offset → bytes → hash chains in flight
-template <bool SPARK24>
+// so the byte loads stay coalesced) — four independent offset → window → hash chains in flight, every
+// window issued before the first hash
+template <bool SPARK24, typename O>
 __global__ __launch_bounds__(256) void k_hash(const uint8_t* __restrict__ utf8,
-                                              const int64_t* __restrict__ tok_off, int64_t n_tok,
+                                              const O* __restrict__ tok_off, int64_t n_tok,
                                               int32_t num_features, int32_t* __restrict__ out) {
   const int64_t S = (int64_t)gridDim.x * 256;
   for (int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x; t0 < n_tok; t0 += 4 * S) {
-    int64_t b[4], e[4];
+    O b[4], e[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int64_t t = t0 + q * S < n_tok ? t0 + q * S : n_tok - 1;
       b[q] = tok_off[t];
       e[q] = tok_off[t + 1];
     }
-    int32_t h[4];
+    Win w[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) h[q] = murmur3<SPARK24>(utf8 + b[q], (uint32_t)(e[q] - b[q]));
+    for (int q = 0; q < 4; ++q) w[q] = load_win(utf8 + b[q]);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      const int32_t h = murmur3_win<SPARK24>(utf8 + b[q], (uint32_t)(e[q] - b[q]), w[q]);
       if (t0 + q * S < n_tok) {
-        const int32_t raw = h[q] % num_features;  // Utils.nonNegativeMod (Java % truncates toward zero)
+        const int32_t raw = h % num_features;  // Utils.nonNegativeMod (Java % truncates toward zero)
         out[t0 + q * S] = raw + (raw < 0 ? num_features : 0);
       }
     }
@@ -141,6 +143,16 @@ void hash_tokens(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_
     k_hash<false><<<g, 256, 0, c.stream>>>(d_utf8, d_tok_off, n_tok, num_features, d_idx);
   KERNEL_CHECK();
 }
+template <typename O>
+static void hash_tokens_t(Ctx& c, const uint8_t* d_utf8, const O* d_tok_off, int64_t n_tok, int32_t num_features,
+                          int variant, int32_t* d_idx) {
+  const int g = grid_for(ceil_div(n_tok, (int64_t)4), 256, 256 * 32);
+  if (variant == STC_HASH_SPARK24)
+    k_hash<true><<<g, 256, 0, c.stream>>>(d_utf8, d_tok_off, n_tok, num_features, d_idx);
+  else
+    k_hash<false><<<g, 256, 0, c.stream>>>(d_utf8, d_tok_off, n_tok, num_features, d_idx);
+  KERNEL_CHECK();
+}
 
 // ---------------------------------------------------------------------------------------
 // K2: per-document sort + run-length count → CSR.  One wave per document.
@@ -156,6 +168,44 @@ void hash_tokens(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_
 // hipcub's segments, so the CSR is bit-identical run to run.
 // ---------------------------------------------------------------------------------------
 constexpr int kSortCap = 1024;  // ≤ 16 keys per lane
+#ifndef TF_DPP
+#define TF_DPP 1  // the sort's cross-lane exchanges by DPP / swizzle (0: ds_bpermute throughout)
+#endif
+
+// x from lane ^ lx without the LDS crossbar where a DPP pattern exists (round 4: every shuffle of the
+// network was a ds_bpermute, ~60 % of the sort): xor 1 / 2 quad_perm, xor 4 = half-row mirror (xor 7)
+// after quad_perm xor 3, xor 8 = row rotate by 8; xor 16 ds_swizzle (no address VGPR); xor 32 bpermute.
+__device__ __forceinline__ int32_t shfl_xor_dpp(int32_t v, int lx) {
+  switch (lx) {
+    case 1: return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    case 2: return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    case 4: return __builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(v, 0x1B, 0xF, 0xF, false),  // [3,2,1,0]
+                                            0x141, 0xF, 0xF, false);     // row_half_mirror
+    case 8: return __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    case 16: return __builtin_amdgcn_ds_swizzle(v, 0x401F);              // and 0x1F, xor 0x10
+    default: return __shfl_xor(v, lx, 64);
+  }
+}
+
+// Σ over the wave of a per-lane count in [0, P] from bit-sliced ballots (scalar popcounts, no shuffles)
+template <int P>
+__device__ __forceinline__ int wave_sum_small(int v) {
+  int tot = 0;
+#pragma unroll
+  for (int b = 0; (1 << b) <= P; ++b) tot += __popcll(__ballot((v >> b) & 1)) << b;
+  return tot;
+}
+// the exclusive prefix of such a count over the lanes below this one
+template <int P>
+__device__ __forceinline__ int wave_excl_small(int v) {
+  int pre = 0;
+#pragma unroll
+  for (int b = 0; (1 << b) <= P; ++b) {
+    const uint64_t m = __ballot((v >> b) & 1);
+    pre += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+  }
+  return pre;
+}
 
 template <int P>
 __device__ __forceinline__ void bitonic_regs(int32_t (&x)[P], int lane) {
@@ -169,7 +219,7 @@ __device__ __forceinline__ void bitonic_regs(int32_t (&x)[P], int lane) {
 #pragma unroll
         for (int p = 0; p < P; ++p) {
           const int e = lane * P + p;
-          const int32_t o = __shfl_xor(x[p], lx, 64);
+          const int32_t o = TF_DPP ? shfl_xor_dpp(x[p], lx) : __shfl_xor(x[p], lx, 64);
           const bool lower = (e & j) == 0, asc = (e & k) == 0;
           x[p] = (lower == asc) ? min(x[p], o) : max(x[p], o);
         }
@@ -222,10 +272,10 @@ constexpr int kFusedCap = 256;  // documents up to this many tokens are hashed a
 // of the document goes to register p of the lane (coalesced offset and byte loads; the bitonic network
 // sorts any starting order), is hashed there, and the P registers are sorted and their distinct ids
 // counted exactly as sort_doc does.
-template <bool SPARK24, int P>
-__device__ __forceinline__ int hash_sort_regs(const uint8_t* __restrict__ utf8, const int64_t* __restrict__ tok_off,
+template <bool SPARK24, int P, typename O>
+__device__ __forceinline__ int hash_sort_regs(const uint8_t* __restrict__ utf8, const O* __restrict__ tok_off,
                                               int64_t s, int n, int32_t nf, int32_t (&x)[P], int lane) {
-  int64_t b[P], e[P];
+  O b[P], e[P];
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     const int q = p * 64 + lane;
@@ -255,16 +305,36 @@ __device__ __forceinline__ int hash_sort_regs(const uint8_t* __restrict__ utf8, 
     const int32_t prev = p == 0 ? prev_last : x[p - 1];
     heads += (q < n && (q == 0 || x[p] != prev)) ? 1 : 0;
   }
-  for (int o = 32; o > 0; o >>= 1) heads += __shfl_xor(heads, o, 64);
-  return heads;  // distinct ids (wave total)
+  return wave_sum_small<P>(heads);  // distinct ids (wave total)
 }
 
-template <bool SPARK24, int P>
-__device__ __forceinline__ int64_t hash_sort_doc(const uint8_t* __restrict__ utf8, const int64_t* __restrict__ tok_off,
+// the same from bucket ids already hashed into `keys` (token order): load, sort, count distinct
+template <int P>
+__device__ __forceinline__ int keys_sort_regs(const int32_t* __restrict__ keys, int64_t s, int n, int32_t (&x)[P],
+                                              int lane) {
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int q = p * 64 + lane;
+    x[p] = q < n ? keys[s + q] : INT32_MAX;  // pads sort last
+  }
+  bitonic_regs<P>(x, lane);
+  const int32_t prev_last = __shfl_up(x[P - 1], 1, 64);
+  int heads = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int q = lane * P + p;
+    const int32_t prev = p == 0 ? prev_last : x[p - 1];
+    heads += (q < n && (q == 0 || x[p] != prev)) ? 1 : 0;
+  }
+  return wave_sum_small<P>(heads);
+}
+
+template <bool SPARK24, int P, typename O>
+__device__ __forceinline__ int64_t hash_sort_doc(const uint8_t* __restrict__ utf8, const O* __restrict__ tok_off,
                                                  int64_t s, int n, int32_t nf, int32_t* __restrict__ sorted,
                                                  int lane) {
   int32_t x[P];
-  const int heads = hash_sort_regs<SPARK24, P>(utf8, tok_off, s, n, nf, x, lane);
+  const int heads = hash_sort_regs<SPARK24, P, O>(utf8, tok_off, s, n, nf, x, lane);
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     const int q = lane * P + p;
@@ -277,9 +347,9 @@ __device__ __forceinline__ int64_t hash_sort_doc(const uint8_t* __restrict__ utf
 // documents hashed into `keys` — ≤ kSortCap tokens for k_doc_sort (counted in *n_medium), the rest for the
 // segmented radix sort (appended to `large`).  Capping the fused path at 4 keys per lane keeps the kernel
 // at ~50 VGPRs: the hashing's dependent offset → byte loads need the occupancy (the P = 16 form held 132).
-template <bool SPARK24>
+template <bool SPARK24, typename O>
 __global__ __launch_bounds__(64 * kDocWaves, 8) void k_doc_hash_sort(const uint8_t* __restrict__ utf8,
-                                                                 const int64_t* __restrict__ tok_off,
+                                                                 const O* __restrict__ tok_off,
                                                                  const int64_t* __restrict__ doc_off, int64_t n_docs,
                                                                  int32_t nf, int32_t* __restrict__ keys,
                                                                  int32_t* __restrict__ sorted,
@@ -304,9 +374,9 @@ __global__ __launch_bounds__(64 * kDocWaves, 8) void k_doc_hash_sort(const uint8
     }
     const int n = (int)n64;
     int64_t h = 0;
-    if (n <= 64) h = hash_sort_doc<SPARK24, 1>(utf8, tok_off, s, n, nf, sorted, lane);
-    else if (n <= 128) h = hash_sort_doc<SPARK24, 2>(utf8, tok_off, s, n, nf, sorted, lane);
-    else h = hash_sort_doc<SPARK24, 4>(utf8, tok_off, s, n, nf, sorted, lane);
+    if (n <= 64) h = hash_sort_doc<SPARK24, 1, O>(utf8, tok_off, s, n, nf, sorted, lane);
+    else if (n <= 128) h = hash_sort_doc<SPARK24, 2, O>(utf8, tok_off, s, n, nf, sorted, lane);
+    else h = hash_sort_doc<SPARK24, 4, O>(utf8, tok_off, s, n, nf, sorted, lane);
     if (lane == 0) nnz[d] = h;
   }
 }
@@ -314,8 +384,13 @@ __global__ __launch_bounds__(64 * kDocWaves, 8) void k_doc_hash_sort(const uint8
 // ---- single pass (round 4) for corpora whose documents all hold ≤ kFusedCap tokens (known at upload):
 // hash + register sort + CSR emission in one kernel, the row offsets from a decoupled look-back over
 // tiles of kDocWaves documents — no sorted-key array, no nnz scan, no second pass over the keys.
-// Workgroups take tiles in ticket order (an atomic counter), so every tile a look-back waits on has
-// already started and finishes: no dependence on dispatch order.  status[t] = flag << 62 | value
+// Workgroups take tiles in ticket order (an atomic counter), so every tile a look-back waits on is held
+// by a running workgroup that reaches it waiting only on lower tiles: no dependence on dispatch order or
+// residency.  A look-back that waits past its poll bound sets the fault word; the host then rebuilds
+// the CSR with the sorted-key passes (mode 0).  Measured without gain: batching tickets (2–8 consecutive
+// tiles per atomic: 1.2× to 300× slower, a batch's later tiles publish their counts an iteration late)
+// and a static tile order over a resident grid (tile = step·grid + blockIdx: 2.89 vs 2.11 ms, a slow
+// workgroup stalls every later tile; and with the flat-hash mode the grid was not all resident).  status[t] = flag << 62 | value
 // (flag 1: the tile's own entry count, 2: the inclusive count of tiles 0..t), written by one lane with
 // agent-scope atomic stores and read with agent-scope atomic loads (vector memory, L2-coherent).
 constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = kLbAgg - 1;
@@ -334,14 +409,14 @@ __device__ __forceinline__ void tile_publish(uint64_t* status, int64_t tile, int
 // the exclusive entry count before `tile` (one wave; every lane returns it), then the tile's inclusive
 // count published.  Waits only for predecessors' own counts, which tile_publish writes unconditionally.
 __device__ __forceinline__ int64_t tile_lookback(uint64_t* status, int64_t tile, int64_t agg, int lane,
-                                                 uint64_t* fault) {
+                                                 uint64_t* fault, int max_polls) {
   if (tile == 0) return 0;
   int64_t excl = 0;
   for (int64_t j = tile - 1;; j -= 64) {  // a window of 64 predecessors, closest in lane 0
     const int64_t k = j - lane;
     uint64_t v = k >= 0 ? __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbInc;
     for (int polls = 0; __ballot((v >> 62) == 0); ++polls) {  // a predecessor not yet published: it is running
-      if (polls == kLbMaxPolls) {
+      if (polls >= max_polls) {
         if (lane == 0) __hip_atomic_store(fault, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         v = kLbInc;  // give up (the output is discarded)
         break;
@@ -374,29 +449,24 @@ __device__ __forceinline__ void emit_runs(const int32_t (&x)[4], int n, int lane
     hd[p] = q < n && (q == 0 || x[p] != prev);
     hc += hd[p] ? 1 : 0;
   }
-  int inc = hc;  // inclusive lane prefix of the head counts
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += y;
-  }
-  int first = n;  // this lane's first head position; then the first head after this lane
+  const int excl = wave_excl_small<P>(hc);  // head slots before this lane
+  int first = n;  // this lane's first head position
 #pragma unroll
   for (int p = P - 1; p >= 0; --p)
     if (hd[p]) first = lane * P + p;
-  int sm = first;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_down(sm, o, 64);
-    if (lane + o < 64) sm = min(sm, y);
-  }
-  int nx = __shfl_down(sm, 1, 64);
-  if (lane == 63) nx = n;
+  // the first head after this lane: the next lane holding one (ballot), its `first`
+  const uint64_t has = __ballot(hc > 0);
+  const uint64_t after = lane == 63 ? 0ull : has >> (lane + 1);
+  const int nl = after ? lane + 1 + __builtin_ctzll(after) : lane;
+  const int nf = __shfl(first, nl, 64);
+  int nx = after ? nf : n;
   int nxt[P];
 #pragma unroll
   for (int p = P - 1; p >= 0; --p) {
     nxt[p] = nx;
     if (hd[p]) nx = lane * P + p;
   }
-  int64_t r = out0 + (inc - hc);
+  int64_t r = out0 + excl;
 #pragma unroll
   for (int p = 0; p < P; ++p)
     if (hd[p]) {
@@ -413,20 +483,22 @@ __device__ __forceinline__ void emit_runs(const int32_t (&x)[4], int n, int lane
 #define TF_EMIT_OCC 7  // waves per SIMD: 72 VGPRs; 8 spills two
 #endif
 #ifndef TF_EMIT_WAVES
-#define TF_EMIT_WAVES 4  // documents per tile (one per wave): one ticket and one look-back per tile
+#define TF_EMIT_WAVES 8  // documents per tile (one per wave): one ticket and one look-back per tile (4: +30 %)
 #endif
 constexpr int kEmitWaves = TF_EMIT_WAVES;
+
 template <int P>
 __device__ __forceinline__ void take(int32_t (&x)[4], const int32_t (&xp)[P]) {
 #pragma unroll
   for (int p = 0; p < P; ++p) x[p] = xp[p];
 }
 
-template <bool SPARK24, typename V>
+template <bool SPARK24, bool KEYS, typename V, typename O>
 __global__ __launch_bounds__(64 * kEmitWaves, TF_EMIT_OCC) void k_doc_hash_emit(
-    const uint8_t* __restrict__ utf8, const int64_t* __restrict__ tok_off, const int64_t* __restrict__ doc_off,
+    const int32_t* __restrict__ keys /* KEYS: the hashed ids, token order */,
+    const uint8_t* __restrict__ utf8, const O* __restrict__ tok_off, const int64_t* __restrict__ doc_off,
     int64_t n_docs, int32_t nf, int binary, int64_t* __restrict__ indptr, int32_t* __restrict__ idx,
-    V* __restrict__ vals, uint64_t* __restrict__ status, unsigned long long* __restrict__ ticket) {
+    V* __restrict__ vals, uint64_t* __restrict__ status, unsigned long long* __restrict__ ticket, int max_polls) {
   __shared__ int tile_s;
   __shared__ int wn[kEmitWaves];
   __shared__ int64_t base_s;
@@ -452,15 +524,15 @@ __global__ __launch_bounds__(64 * kEmitWaves, TF_EMIT_OCC) void k_doc_hash_emit(
         n = (int)(doc_off[d + 1] - s);
         if (n <= 64) {
           int32_t xp[1];
-          h = hash_sort_regs<SPARK24, 1>(utf8, tok_off, s, n, nf, xp, lane);
+          h = KEYS ? keys_sort_regs<1>(keys, s, n, xp, lane) : hash_sort_regs<SPARK24, 1, O>(utf8, tok_off, s, n, nf, xp, lane);
           take<1>(x, xp);
         } else if (n <= 128) {
           int32_t xp[2];
-          h = hash_sort_regs<SPARK24, 2>(utf8, tok_off, s, n, nf, xp, lane);
+          h = KEYS ? keys_sort_regs<2>(keys, s, n, xp, lane) : hash_sort_regs<SPARK24, 2, O>(utf8, tok_off, s, n, nf, xp, lane);
           take<2>(x, xp);
         } else {
           int32_t xp[4];
-          h = hash_sort_regs<SPARK24, 4>(utf8, tok_off, s, n, nf, xp, lane);
+          h = KEYS ? keys_sort_regs<4>(keys, s, n, xp, lane) : hash_sort_regs<SPARK24, 4, O>(utf8, tok_off, s, n, nf, xp, lane);
           take<4>(x, xp);
         }
       }
@@ -478,7 +550,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, TF_EMIT_OCC) void k_doc_hash_emit(
     }
     if (tp >= 0) {
       if (wv == 0) {
-        const int64_t ex = tile_lookback(status, tp, aggq, lane, status + tiles + 1);
+        const int64_t ex = tile_lookback(status, tp, aggq, lane, status + tiles + 1, max_polls);
         if (lane == 0) base_s = ex;
       }
       __syncthreads();
@@ -647,7 +719,92 @@ void row_order_by_df(Ctx& c, const DCsr& m, const int64_t* d_df, int32_t* d_orde
   KERNEL_CHECK();
 }
 
-void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t n_tok,
+// resident token corpora keep their token offsets as u32 when the blob allows (stc_tokens_upload): the
+// offsets are 8 of the ~16 bytes HashingTF reads per token
+__global__ __launch_bounds__(256) void k_narrow(const int64_t* __restrict__ src, int64_t n, uint32_t* __restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    dst[i] = (uint32_t)src[i];
+}
+void narrow_offsets(Ctx& c, const int64_t* d_src, int64_t n, uint32_t* d_dst) {
+  if (n == 0) return;
+  k_narrow<<<grid_for(n, 256, 256 * 32), 256, 0, c.stream>>>(d_src, n, d_dst);
+  KERNEL_CHECK();
+}
+
+// the look-back single pass (modes 1 / 2); false: a look-back timed out, the caller runs the passes
+static bool single_pass(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off64, const uint32_t* d_tok_off32,
+                        int64_t n_tok, const int64_t* d_doc_off, int64_t n_docs, int32_t num_features, int binary,
+                        int variant, int value_dtype, DCsr& out) {
+  hipStream_t st = c.stream;
+  const int64_t tiles = ceil_div(n_docs, (int64_t)kEmitWaves);
+  DevBuf& lb = c.scratch[2];
+  lb.reserve(sizeof(uint64_t) * (tiles + 2));
+  uint64_t* status = lb.as<uint64_t>();  // [tiles] look-back words, then the ticket, then the fault word
+  HIP_CHECK(hipMemsetAsync(status, 0, sizeof(uint64_t) * (tiles + 2), st));
+  HIP_CHECK(hipMemsetAsync(out.indptr.p, 0, sizeof(int64_t), st));
+  // nnz ≤ n_tok: the output is sized before the counts exist
+  out.indices.reserve(sizeof(int32_t) * n_tok);
+  out.values.reserve((value_dtype == STC_F32 ? 4 : 8) * n_tok);
+  // mode 1 (default): hashed inside the per-document pass; mode 2: the tokens hashed flat first (k_hash,
+  // four independent chains per lane), the per-document pass then loads, sorts and emits
+  const bool flat = c.tf_mode == 2;
+  int32_t* keys = nullptr;
+  if (flat) {
+    DevBuf& kb = c.scratch[0];
+    kb.reserve(sizeof(int32_t) * n_tok);
+    keys = kb.as<int32_t>();
+    if (d_tok_off32) hash_tokens_t(c, d_utf8, d_tok_off32, n_tok, num_features, variant, keys);
+    else hash_tokens_t(c, d_utf8, d_tok_off64, n_tok, num_features, variant, keys);
+  }
+  int max_polls = c.tf_force_fault ? 0 : kLbMaxPolls;
+  auto go = [&](auto spark, auto* vals) {
+    constexpr bool S24 = decltype(spark)::value;
+    using V = std::remove_pointer_t<decltype(vals)>;
+    auto launch = [&](const void* kern, auto tok_off) {
+      int per_cu = 0;  // a grid of what is resident (more workgroups would only take tickets past the end)
+      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kEmitWaves, 0));
+      const int64_t resident = (int64_t)std::max(per_cu, 1) * c.cus;
+      const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(tiles, resident));
+      unsigned long long* ticket = reinterpret_cast<unsigned long long*>(status + tiles);
+      const uint8_t* u8 = d_utf8;
+      const int64_t* doff = d_doc_off;
+      int64_t nd = n_docs;
+      int32_t nf = num_features;
+      int bin = binary;
+      int64_t* ip = out.indptr.as<int64_t>();
+      int32_t* ix = out.indices.as<int32_t>();
+      V* vv = vals;
+      uint64_t* stp = status;
+      void* args[] = {&keys, &u8, &tok_off, &doff, &nd, &nf, &bin, &ip, &ix, &vv, &stp, &ticket, &max_polls};
+      HIP_CHECK(hipLaunchKernel(kern, dim3(g), dim3(64 * kEmitWaves), args, 0, st));
+    };
+    if (flat) launch((const void*)k_doc_hash_emit<S24, true, V, int64_t>, d_tok_off64);
+    else if (d_tok_off32) launch((const void*)k_doc_hash_emit<S24, false, V, uint32_t>, d_tok_off32);
+    else launch((const void*)k_doc_hash_emit<S24, false, V, int64_t>, d_tok_off64);
+  };
+  if (value_dtype == STC_F32) {
+    if (variant == STC_HASH_SPARK24) go(std::true_type{}, out.values.as<float>());
+    else go(std::false_type{}, out.values.as<float>());
+  } else {
+    if (variant == STC_HASH_SPARK24) go(std::true_type{}, out.values.as<double>());
+    else go(std::false_type{}, out.values.as<double>());
+  }
+  KERNEL_CHECK();
+  int64_t total = 0;
+  uint64_t fault = 0;
+  HIP_CHECK(hipMemcpyAsync(&total, out.indptr.as<int64_t>() + n_docs, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipMemcpyAsync(&fault, status + tiles + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  if (fault) {
+    ++c.tf_fallbacks;
+    return false;
+  }
+  out.nnz = total;
+  out.positive = true;
+  return true;
+}
+
+void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off64, const uint32_t* d_tok_off32, int64_t n_tok,
                const int64_t* d_doc_off, int64_t n_docs, int32_t num_features, int binary,
                int variant, int value_dtype, int64_t max_doc, DCsr& out) {
   STC_REQUIRE(n_tok < (int64_t(1) << 31), "at most 2^31-1 tokens per call (split the corpus)");
@@ -661,42 +818,10 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
     out.nnz = 0;
     return;
   }
-  if (max_doc >= 0 && max_doc <= kFusedCap && c.single_pass_tf) {  // every document fits the register sort
-    const int64_t tiles = ceil_div(n_docs, (int64_t)kEmitWaves);
-    DevBuf& lb = c.scratch[2];
-    lb.reserve(sizeof(uint64_t) * (tiles + 2));
-    uint64_t* status = lb.as<uint64_t>();  // [tiles] look-back words, then the ticket, then the fault word
-    auto* ticket = reinterpret_cast<unsigned long long*>(status + tiles);
-    HIP_CHECK(hipMemsetAsync(status, 0, sizeof(uint64_t) * (tiles + 2), st));
-    HIP_CHECK(hipMemsetAsync(out.indptr.p, 0, sizeof(int64_t), st));
-    // nnz ≤ n_tok: the output is sized before the counts exist
-    out.indices.reserve(sizeof(int32_t) * n_tok);
-    out.values.reserve((value_dtype == STC_F32 ? 4 : 8) * n_tok);
-    const unsigned g = (unsigned)std::min<int64_t>(tiles, (int64_t)c.cus * TF_EMIT_OCC * 4 / kEmitWaves);
-    auto go = [&](auto spark, auto* vals) {
-      constexpr bool S24 = decltype(spark)::value;
-      k_doc_hash_emit<S24><<<g, 64 * kEmitWaves, 0, st>>>(d_utf8, d_tok_off, d_doc_off, n_docs, num_features, binary,
-                                                          out.indptr.as<int64_t>(), out.indices.as<int32_t>(), vals,
-                                                          status, ticket);
-    };
-    if (value_dtype == STC_F32) {
-      if (variant == STC_HASH_SPARK24) go(std::true_type{}, out.values.as<float>());
-      else go(std::false_type{}, out.values.as<float>());
-    } else {
-      if (variant == STC_HASH_SPARK24) go(std::true_type{}, out.values.as<double>());
-      else go(std::false_type{}, out.values.as<double>());
-    }
-    KERNEL_CHECK();
-    int64_t total = 0;
-    uint64_t fault = 0;
-    HIP_CHECK(hipMemcpyAsync(&total, out.indptr.as<int64_t>() + n_docs, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(&fault, status + tiles + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-    if (fault) throw Error(STC_ERR_HIP, "HashingTF: a row-offset look-back timed out (device oversubscribed?)");
-    out.nnz = total;
-    out.positive = true;
+  if (max_doc >= 0 && max_doc <= kFusedCap && c.tf_mode > 0 &&
+      single_pass(c, d_utf8, d_tok_off64, d_tok_off32, n_tok, d_doc_off, n_docs, num_features, binary, variant,
+                  value_dtype, out))
     return;
-  }
   // grow-only scratch kept on the context (the featurisation of one corpus reuses it): no allocation,
   // and so no implicit device synchronisation of hipFree, per call
   DevBuf& keys = c.scratch[0];
@@ -712,14 +837,19 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t 
   HIP_CHECK(hipMemsetAsync(n_large_d, 0, 2 * sizeof(int32_t), st));
   const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>(ceil_div(n_docs, kDocWaves), 1), 1 << 14);
   keys.reserve(sizeof(int32_t) * n_tok);  // the long documents' bucket ids, at their token positions
-  if (variant == STC_HASH_SPARK24)
-    k_doc_hash_sort<true><<<g, 64 * kDocWaves, 0, st>>>(d_utf8, d_tok_off, d_doc_off, n_docs, num_features,
-                                                        keys.as<int32_t>(), sorted.as<int32_t>(), nnz.as<int64_t>() + 1,
-                                                        large, n_large_d, n_large_d + 1);
-  else
-    k_doc_hash_sort<false><<<g, 64 * kDocWaves, 0, st>>>(d_utf8, d_tok_off, d_doc_off, n_docs, num_features,
-                                                         keys.as<int32_t>(), sorted.as<int32_t>(), nnz.as<int64_t>() + 1,
-                                                         large, n_large_d, n_large_d + 1);
+  auto pass_a = [&](auto spark, const auto* tok_off) {
+    constexpr bool S24 = decltype(spark)::value;
+    k_doc_hash_sort<S24><<<g, 64 * kDocWaves, 0, st>>>(d_utf8, tok_off, d_doc_off, n_docs, num_features,
+                                                       keys.as<int32_t>(), sorted.as<int32_t>(), nnz.as<int64_t>() + 1,
+                                                       large, n_large_d, n_large_d + 1);
+  };
+  if (variant == STC_HASH_SPARK24) {
+    if (d_tok_off32) pass_a(std::true_type{}, d_tok_off32);
+    else pass_a(std::true_type{}, d_tok_off64);
+  } else {
+    if (d_tok_off32) pass_a(std::false_type{}, d_tok_off32);
+    else pass_a(std::false_type{}, d_tok_off64);
+  }
   KERNEL_CHECK();
   int32_t counts[2] = {0, 0};
   HIP_CHECK(hipMemcpyAsync(counts, n_large_d, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));

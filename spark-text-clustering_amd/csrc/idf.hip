@@ -396,6 +396,10 @@ __global__ __launch_bounds__(256) void k_transform(const int32_t* __restrict__ i
 constexpr int kCacheBits = 14;
 constexpr int kCacheSlots = 1 << kCacheBits;
 constexpr int kCacheThreads = 1024;
+#ifndef IDF_CACHE_UNROLL
+#define IDF_CACHE_UNROLL 4
+#endif
+constexpr int kCacheUnroll = IDF_CACHE_UNROLL;  // quads per thread and step (2: 0.81 ms)
 constexpr uint8_t kCacheEmpty = 0xFF;
 
 __global__ __launch_bounds__(256) void k_idf_cache(const int64_t* __restrict__ df, const double* __restrict__ idf,
@@ -445,25 +449,27 @@ __global__ __launch_bounds__(kCacheThreads) void k_transform_cached(const int32_
   const int64_t S = (int64_t)gridDim.x * kCacheThreads;
   const I4* i4 = reinterpret_cast<const I4*>(idx);
   V4* v4 = reinterpret_cast<V4*>(val);
-  for (int64_t q = (int64_t)blockIdx.x * kCacheThreads + threadIdx.x; q < n4; q += 2 * S) {
-    const bool two = q + S < n4;
-    const I4 ia = __builtin_nontemporal_load(i4 + q);
-    const I4 ib = two ? __builtin_nontemporal_load(i4 + q + S) : I4{};
-    V4 a = __builtin_nontemporal_load(v4 + q);
-    V4 b = two ? __builtin_nontemporal_load(v4 + q + S) : V4{};
-    const double wa0 = w_of(ia.x), wa1 = w_of(ia.y), wa2 = w_of(ia.z), wa3 = w_of(ia.w);
-    a.x = idf_scale(a.x, wa0, zero_floor);
-    a.y = idf_scale(a.y, wa1, zero_floor);
-    a.z = idf_scale(a.z, wa2, zero_floor);
-    a.w = idf_scale(a.w, wa3, zero_floor);
-    __builtin_nontemporal_store(a, v4 + q);
-    if (two) {
-      const double wb0 = w_of(ib.x), wb1 = w_of(ib.y), wb2 = w_of(ib.z), wb3 = w_of(ib.w);
-      b.x = idf_scale(b.x, wb0, zero_floor);
-      b.y = idf_scale(b.y, wb1, zero_floor);
-      b.z = idf_scale(b.z, wb2, zero_floor);
-      b.w = idf_scale(b.w, wb3, zero_floor);
-      __builtin_nontemporal_store(b, v4 + q + S);
+  // kCacheUnroll quads per thread and step, every load issued before the first lookup: one workgroup per
+  // CU (the table's LDS) leaves 4 waves per SIMD, so the memory parallelism has to come from each thread
+  for (int64_t q0 = (int64_t)blockIdx.x * kCacheThreads + threadIdx.x; q0 < n4; q0 += kCacheUnroll * S) {
+    I4 ii[kCacheUnroll];
+    V4 vv[kCacheUnroll];
+#pragma unroll
+    for (int u = 0; u < kCacheUnroll; ++u) {
+      const int64_t q = q0 + u * S;
+      ii[u] = q < n4 ? __builtin_nontemporal_load(i4 + q) : I4{};
+      vv[u] = q < n4 ? __builtin_nontemporal_load(v4 + q) : V4{};
+    }
+#pragma unroll
+    for (int u = 0; u < kCacheUnroll; ++u) {
+      const int64_t q = q0 + u * S;
+      const double w0 = w_of(ii[u].x), w1 = w_of(ii[u].y), w2 = w_of(ii[u].z), w3 = w_of(ii[u].w);
+      V4 a = vv[u];
+      a.x = idf_scale(a.x, w0, zero_floor);
+      a.y = idf_scale(a.y, w1, zero_floor);
+      a.z = idf_scale(a.z, w2, zero_floor);
+      a.w = idf_scale(a.w, w3, zero_floor);
+      if (q < n4) __builtin_nontemporal_store(a, v4 + q);
     }
   }
   const int64_t e = 4 * n4 + (int64_t)blockIdx.x * kCacheThreads + threadIdx.x;  // the last nnz % 4 entries

@@ -111,8 +111,13 @@ struct Ctx {
   int rank = 0;
   int cus = 256;          // compute units (the df count sizes its grid to one workgroup per CU)
   bool df_tiled = true;   // idf.hip doc_freq: the tiled count (false: the binned one, STC_DF_BINNED=1)
-  bool single_pass_tf = true;
-  bool idf_cache = true;  // idf.hip: the device IDF model's hot-idf LDS table (STC_IDF_NO_CACHE=1: off)  // hashing_tf.hip: the look-back single pass when max_doc allows (STC_TF_TWO_PASS=1: off)
+  // hashing_tf.hip build_csr when every document fits the register sort (STC_TF_MODE): 0 the round-3
+  // passes (hash + sort → sorted keys, scan, runs), 1 (default) hash + sort + emit in one look-back pass,
+  // 2 a flat hash then the look-back sort + emit pass
+  int tf_mode = 1;
+  bool tf_force_fault = false;  // test knob (STC_TF_FAULT=1): every look-back gives up at once
+  int64_t tf_fallbacks = 0;     // single passes that fell back to the sorted-key passes
+  bool idf_cache = true;  // idf.hip: the device IDF model's hot-idf LDS table (STC_IDF_NO_CACHE=1: off)
   DevBuf scratch[12];  // grow-only scratch of the featurisation kernels (hashing_tf.hip, idf.hip, api.hip IDF)
   DevBuf coll_tmp;    // the in-process all-reduce's staging buffer
   void use() const { HIP_CHECK(hipSetDevice(device)); }
@@ -487,10 +492,12 @@ namespace hashing {
 void hash_tokens(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t n_tok,
                  int32_t num_features, int variant, int32_t* d_idx);
 void row_order_by_df(Ctx& c, const DCsr& m, const int64_t* d_df, int32_t* d_order);
-void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off, int64_t n_tok,
+// token offsets as int64 (d_tok_off64) or, when d_tok_off32 is given, u32 (a resident upload's narrowed copy)
+void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off64, const uint32_t* d_tok_off32, int64_t n_tok,
                const int64_t* d_doc_off, int64_t n_docs, int32_t num_features, int binary,
                int variant, int value_dtype, int64_t max_doc /* longest document's tokens, −1 unknown */,
                DCsr& out);
+void narrow_offsets(Ctx& c, const int64_t* d_src, int64_t n, uint32_t* d_dst);
 }  // namespace hashing
 namespace tokenizer {
 // Spark ML Tokenizer on device: d_text/d_text_off (n_docs+1) in; lower-cased, separator-free blob,

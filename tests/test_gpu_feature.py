@@ -188,7 +188,7 @@ def test_idf_doc_freq_zipf_hot_ids(ctx, V):
 def test_idf_doc_freq_tiled_and_binned(ctx, monkeypatch, V, D):
     """doc_freq's two LDS-tile counts (idf.hip: k_df_tiled, the default, one XCD's workgroups sharing a
     chunk group's index stream; k_df_bin + k_df_binned under STC_DF_BINNED=1) and HashingTF's single
-    look-back pass vs its sorted-key passes (STC_TF_TWO_PASS=1, same CSR), and the transform with the
+    look-back pass vs its sorted-key passes (STC_TF_MODE=0, same CSR), and the transform with the
     model's hot-idf LDS table (default) and without it (STC_IDF_NO_CACHE=1) on a device-resident
     HashingTF matrix (values known positive: indices only) and on an uploaded matrix with explicit zeros
     (values read): exact column counts, with group counts that do and do not fill the XCD mapping."""
@@ -196,10 +196,10 @@ def test_idf_doc_freq_tiled_and_binned(ctx, monkeypatch, V, D):
     from stc import synth
 
     monkeypatch.setenv("STC_DF_BINNED", "1")
-    monkeypatch.setenv("STC_TF_TWO_PASS", "1")
+    monkeypatch.setenv("STC_TF_MODE", "0")
     monkeypatch.setenv("STC_IDF_NO_CACHE", "1")
     ctx_b = stc.Context(ctx.device)  # reads the knobs at stc_init
-    for k in ("STC_DF_BINNED", "STC_TF_TWO_PASS", "STC_IDF_NO_CACHE"):
+    for k in ("STC_DF_BINNED", "STC_TF_MODE", "STC_IDF_NO_CACHE"):
         monkeypatch.delenv(k)
     (blob, tok_off, doc_off), _ = synth.token_corpus(D, 150, n_words=40000, seed=11)
     csr = []
@@ -250,3 +250,33 @@ def test_hash_window_lengths_and_alignments(ctx, oracle, algo, variant):
     got = htf.indices_of(terms)
     exp = [oracle.non_negative_mod(oracle.murmur3_x86_32(t.encode(), 42, variant), 1 << 18) for t in terms]
     assert np.array_equal(got, np.asarray(exp, np.int32))
+
+
+def test_hashing_tf_single_pass_orders_and_fallback(ctx, monkeypatch):
+    """HashingTF's look-back single pass (hashing_tf.hip single_pass; default), with the flat hash first
+    (STC_TF_MODE=2), and with every look-back
+    giving up at once (STC_TF_FAULT=1: the call falls back to the sorted-key passes and still succeeds):
+    the same CSR as the sorted-key passes (STC_TF_MODE=0), bit for bit."""
+    import stc
+    from stc import synth
+
+    (blob, tok_off, doc_off), _ = synth.token_corpus(3001, 120, n_words=30000, seed=21)
+    got = {}
+    for tag, env in [("single", {}), ("flat", {"STC_TF_MODE": "2"}),
+                     ("fault", {"STC_TF_FAULT": "1"}), ("passes", {"STC_TF_MODE": "0"})]:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        c = stc.Context(ctx.device)
+        for k in env:
+            monkeypatch.delenv(k)
+        dt = stc.DeviceTokens(c, blob, tok_off, doc_off)
+        d = stc.HashingTF(numFeatures=1 << 18, ctx=c).transform_tokens_device(dt)
+        got[tag] = d.download()
+        d.free()
+        dt.free()
+        c.close()
+    ref = got.pop("passes")
+    for tag, m in got.items():
+        assert np.array_equal(m.indptr, ref.indptr), tag
+        assert np.array_equal(m.indices, ref.indices), tag
+        assert np.array_equal(m.values, ref.values), tag
