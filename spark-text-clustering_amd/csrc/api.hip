@@ -1083,6 +1083,8 @@ int stc_init(int device, stc_ctx** out) {
     HIP_CHECK(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device));
     const char* db = std::getenv("STC_DF_BINNED");  // A/B knob: the round-3 binned df count
     c->df_tiled = !(db && db[0] == '1');
+    const char* d32 = std::getenv("STC_DF_U32");  // A/B knob: the u32 tiled count for unique-id rows too
+    c->df_rows16 = !(d32 && d32[0] == '1');
     const char* tm = std::getenv("STC_TF_MODE");  // A/B knob: HashingTF's structure (stc_internal.h Ctx)
     if (tm && tm[0] >= '0' && tm[0] <= '2' && tm[1] == 0) c->tf_mode = tm[0] - '0';
     const char* tf = std::getenv("STC_TF_FAULT");  // test knob

@@ -11,6 +11,9 @@
 // distinct ids + run lengths — no atomics on the CSR, so hot terms ("the") cost nothing extra.
 #include <hipcub/hipcub.hpp>
 
+#include <map>
+#include <mutex>
+
 #include "stc_internal.h"
 
 namespace stc {
@@ -761,8 +764,21 @@ static bool single_pass(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off6
     constexpr bool S24 = decltype(spark)::value;
     using V = std::remove_pointer_t<decltype(vals)>;
     auto launch = [&](const void* kern, auto tok_off) {
-      int per_cu = 0;  // a grid of what is resident (more workgroups would only take tickets past the end)
-      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kEmitWaves, 0));
+      // a grid of what is resident (more workgroups would only take tickets past the end); the occupancy
+      // query once per kernel and process
+      static std::mutex mu;
+      static std::map<const void*, int> occ;
+      int per_cu = 0;
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = occ.find(kern);
+        if (it == occ.end()) {
+          HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kEmitWaves, 0));
+          occ[kern] = per_cu;
+        } else {
+          per_cu = it->second;
+        }
+      }
       const int64_t resident = (int64_t)std::max(per_cu, 1) * c.cus;
       const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(tiles, resident));
       unsigned long long* ticket = reinterpret_cast<unsigned long long*>(status + tiles);
@@ -801,6 +817,7 @@ static bool single_pass(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off6
   }
   out.nnz = total;
   out.positive = true;
+  out.unique_ids = true;
   return true;
 }
 
@@ -900,6 +917,7 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off64, const 
   HIP_CHECK(hipStreamSynchronize(st));
   out.nnz = total;
   out.positive = true;  // counts ≥ 1 (binary: 1)
+  out.unique_ids = true;  // one entry per distinct id
   out.indices.reserve(sizeof(int32_t) * std::max<int64_t>(total, 1));
   out.values.reserve((value_dtype == STC_F32 ? 4 : 8) * std::max<int64_t>(total, 1));
   const uint8_t* fl = n_large > 0 ? flags.as<uint8_t>() : nullptr;

@@ -204,6 +204,73 @@ __global__ __launch_bounds__(kTiledThreads) void k_df_tiled(const int32_t* __res
   for (int i = tid; i < kTile && j0 + i < cols; i += kTiledThreads) out[i] = cnt[i];
 }
 
+// Row-grouped u16 variant (round 4, HashingTF output: every row holds an id at most once).  A group
+// of ≤ 65535 rows counts any id at most 65535 times, so two ids share one u32 LDS word as u16 halves
+// and a 128 KB tile spans 2^16 ids: 4 tiles at 2^18 buckets (half the L2 re-reads of k_df_tiled).
+// Workgroup (g, t) reads its rows' entry range from indptr.
+constexpr int kTile16Bits = 16;
+__device__ __forceinline__ void tile16_add(uint32_t* cnt, uint32_t id, uint32_t t) {
+  if ((id >> kTile16Bits) == t) atomicAdd(&cnt[(id & 0xFFFF) >> 1], 1u << (16 * (id & 1)));
+}
+__global__ __launch_bounds__(kTiledThreads) void k_df_rows16(const int32_t* __restrict__ idx,
+                                                             const int64_t* __restrict__ indptr, int64_t rows,
+                                                             int n_tiles, int64_t groups, int64_t rpg,
+                                                             int64_t cols, uint32_t* __restrict__ part) {
+  extern __shared__ uint32_t cnt[];
+  const int64_t b = blockIdx.x;
+  int t;
+  int64_t g;
+  if (groups % 8 == 0) {  // XCD-aware, as k_df_tiled
+    const int64_t l = b >> 3;
+    t = (int)(l % n_tiles);
+    g = (l / n_tiles) * 8 + (b & 7);
+  } else {
+    t = (int)(b % n_tiles);
+    g = b / n_tiles;
+  }
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kTile; i += kTiledThreads) cnt[i] = 0;  // 2^15 words = 2^16 u16 counters
+  __syncthreads();
+  const int64_t r0 = g * rpg, r1 = r0 + rpg < rows ? r0 + rpg : rows;
+  const int64_t e0 = indptr[r0], e1 = indptr[r1];
+  const uint32_t ut = (uint32_t)t;
+  const int64_t a0 = (e0 + 3) & ~int64_t(3);  // the int4-aligned middle [a0, a1)
+  const int64_t a1 = e1 & ~int64_t(3);
+  if (a0 >= a1) {
+    for (int64_t e = e0 + tid; e < e1; e += kTiledThreads) tile16_add(cnt, (uint32_t)idx[e], ut);
+  } else {
+    if (e0 + tid < a0) tile16_add(cnt, (uint32_t)idx[e0 + tid], ut);
+    if (a1 + tid < e1) tile16_add(cnt, (uint32_t)idx[a1 + tid], ut);
+    const int4* i4 = reinterpret_cast<const int4*>(idx + a0);
+    const int64_t n4 = (a1 - a0) >> 2;
+    int64_t q = tid;
+    for (; q + (kTiledUnroll - 1) * kTiledThreads < n4; q += kTiledUnroll * kTiledThreads) {
+      int4 v[kTiledUnroll];
+#pragma unroll
+      for (int u = 0; u < kTiledUnroll; ++u) v[u] = i4[q + u * kTiledThreads];
+#pragma unroll
+      for (int u = 0; u < kTiledUnroll; ++u) {
+        tile16_add(cnt, (uint32_t)v[u].x, ut);
+        tile16_add(cnt, (uint32_t)v[u].y, ut);
+        tile16_add(cnt, (uint32_t)v[u].z, ut);
+        tile16_add(cnt, (uint32_t)v[u].w, ut);
+      }
+    }
+    for (; q < n4; q += kTiledThreads) {
+      const int4 v = i4[q];
+      tile16_add(cnt, (uint32_t)v.x, ut);
+      tile16_add(cnt, (uint32_t)v.y, ut);
+      tile16_add(cnt, (uint32_t)v.z, ut);
+      tile16_add(cnt, (uint32_t)v.w, ut);
+    }
+  }
+  __syncthreads();
+  const int64_t j0 = (int64_t)t << kTile16Bits;
+  uint32_t* out = part + g * cols + j0;
+  for (int i = tid; i < (1 << kTile16Bits) && j0 + i < cols; i += kTiledThreads)
+    out[i] = (cnt[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+}
+
 __global__ __launch_bounds__(256) void k_df_reduce(const uint32_t* __restrict__ part, int64_t chunks, int64_t cols,
                                                    int64_t* __restrict__ df) {
   for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < cols; j += (int64_t)gridDim.x * 256) {
@@ -236,6 +303,25 @@ void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df) {
   hipStream_t s = c.stream;
   HIP_CHECK(hipMemsetAsync(d_df, 0, sizeof(int64_t) * m.cols, s));
   if (m.nnz == 0) return;
+  if (m.unique_ids && m.cols <= (int64_t(kMaxTiles / 2) << kTile16Bits) && c.df_tiled && c.df_rows16 &&
+      m.rows > 0) {
+    const int T = (int)ceil_div(m.cols, (int64_t)1 << kTile16Bits);
+    const int64_t want = std::max<int64_t>(1, (int64_t)c.cus / T);
+    int64_t G = std::max<int64_t>(std::min<int64_t>(want, ceil_div(m.nnz, (int64_t)65536)), 1);
+    if (G >= 8) G -= G % 8;
+    int64_t rpg = std::min<int64_t>(ceil_div(m.rows, G), 65535);  // ≤ 65535 rows: the u16 bound
+    G = ceil_div(m.rows, rpg);
+    DevBuf& part = c.scratch[0];
+    part.reserve(sizeof(uint32_t) * G * m.cols);
+    const size_t lds = sizeof(uint32_t) * kTile;
+    HIP_CHECK(hipFuncSetAttribute((const void*)k_df_rows16, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    k_df_rows16<<<(unsigned)(T * G), kTiledThreads, lds, s>>>(m.indices.as<int32_t>(), m.indptr.as<int64_t>(), m.rows,
+                                                              T, G, rpg, m.cols, part.as<uint32_t>());
+    KERNEL_CHECK();
+    k_df_reduce<<<grid_for(m.cols), 256, 0, s>>>(part.as<uint32_t>(), G, m.cols, d_df);
+    KERNEL_CHECK();
+    return;
+  }
   if (m.cols <= (int64_t(kMaxTiles) << kTileBits) && c.df_tiled) {
     const int T = (int)ceil_div(m.cols, (int64_t)kTile);
     // groups: a multiple of 8 (the XCD mapping) with T·groups ≈ one workgroup per CU, fewer for small

@@ -111,6 +111,7 @@ struct Ctx {
   int rank = 0;
   int cus = 256;          // compute units (the df count sizes its grid to one workgroup per CU)
   bool df_tiled = true;   // idf.hip doc_freq: the tiled count (false: the binned one, STC_DF_BINNED=1)
+  bool df_rows16 = true;  // … its row-grouped u16 form for unique-id rows (STC_DF_U32=1: off)
   // hashing_tf.hip build_csr when every document fits the register sort (STC_TF_MODE): 0 the round-3
   // passes (hash + sort → sorted keys, scan, runs), 1 (default) hash + sort + emit in one look-back pass,
   // 2 a flat hash then the look-back sort + emit pass
@@ -133,6 +134,9 @@ struct DCsr {
   // every value is > 0 (a HashingTF output: counts / binary 1; kept by a floored IDF transform), so a
   // df count needs only the indices (cleared by anything that may write a value ≤ 0)
   bool positive = false;
+  // every row holds an id at most once (a HashingTF output; kept by the transform): idf.hip may count df
+  // in u16 per group of ≤ 65535 rows
+  bool unique_ids = false;
   DevBuf indptr;   // int64[rows+1]
   DevBuf indices;  // int32[nnz]
   DevBuf values;   // float/double[nnz]
