@@ -253,11 +253,11 @@ def featurization(stc, ctx, a, log, tokens, reps=3):
     dt.free()
     V = a.vocab
     # algorithmic bytes: HashingTF reads the blob + offsets once and writes the CSR; IDF fit reads the
-    # CSR (indices + values) and writes df + idf; the transform reads indices + idf[j] + values, writes values
+    # CSR's indices and writes df + idf; the transform reads indices + idf[j] + values, writes values
     # (a resident upload keeps its token offsets as u32 when the blob is under 4 GiB: stc_tokens_upload)
     off_b = 4.0 if blob.size + 64 <= 1 << 32 else 8.0
     b_hash = blob.size + off_b * (n_tok + 1) + 8.0 * (n_docs + 1) + nnz * (4 + 8) + 8.0 * (n_docs + 1)
-    b_fit = nnz * (4 + 8) + 2 * 8.0 * V
+    b_fit = nnz * 4 + 2 * 8.0 * V  # a HashingTF matrix's values are known > 0: df reads the ids only
     b_tr = nnz * (4 + 8 + 8) + 8.0 * V
     total = float(t.sum())
     return {

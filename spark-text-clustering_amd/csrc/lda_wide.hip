@@ -526,9 +526,10 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide(EStepArgs<T> a, int nl
 //               rule are bit-identical in every member and the team leaves the loop together.
 // Persistent: G = 8·P·⌊CUs/(8P)⌋ blocks (one per CU: the kernel takes all 160 KB of LDS), launched
 // once the occupancy check says the grid is resident (launch_resident); team members share blockIdx % 8 (one XCD,
-// for L2 locality only).  Exchange (cdna_hip_programming.md Guideline 16, R2: the data is the flag):
-// every value travels in a 16-byte granule {epoch, value} written by ONE 16-B sc1 buffer store and
-// read by 16-B sc1 buffer loads (untorn on gfx950); each consumer wave re-reads its granules until
+// for L2 locality, and for the plain granule stores below).  Exchange (cdna_hip_programming.md
+// Guideline 16, R2: the data is the flag): every value travels in a 16-byte granule {epoch, value}
+// written by ONE 16-B buffer store and read by 16-B sc1 (L1-bypassing) buffer loads (untorn on gfx950);
+// each consumer wave re-reads its granules until
 // every tag equals the epoch — no flag, no fence, no block barrier.  Granules double-buffered by epoch
 // parity (a member can run at most one exchange ahead, so a slot never holds a newer epoch than the
 // one awaited).  Every spin is bounded: on timeout the kernel sets the timeout word and every team
@@ -554,6 +555,13 @@ __device__ __forceinline__ T ld_sc1(const T* p) {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kSc1 = 16;  // buffer aux bit: sc1 (write-through store / L1-bypassing load)
+#ifndef WIDE_GRANULE_STORE_AUX
+// the granule stores' cache policy: plain (0) keeps the line in the XCD's L2, where the team's other
+// members (same blockIdx % 8, so the same XCD) poll it; sc1 (write-through) drops it and every poll
+// then goes to the MALL.  Config 4 fp64 E-step 324 → 307 ms (r04).  A member on another XCD would read
+// its own L2's stale line: tags never match, the bounded spin times out, the one-CU rerun keeps the result.
+#define WIDE_GRANULE_STORE_AUX 0
+#endif
 
 template <typename T>
 __device__ __forceinline__ void put_granule(__amdgpu_buffer_rsrc_t rs, int idx, unsigned epoch, T v) {
@@ -564,7 +572,7 @@ __device__ __forceinline__ void put_granule(__amdgpu_buffer_rsrc_t rs, int idx, 
   // store whose halves become visible at different times is re-polled, never consumed torn (the
   // memory model guarantees single-copy atomicity up to 64 bits only)
   const u32x4 g = {epoch, (unsigned)bits, epoch, (unsigned)(bits >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b128(g, rs, idx * 16, 0, kSc1);
+  __builtin_amdgcn_raw_buffer_store_b128(g, rs, idx * 16, 0, WIDE_GRANULE_STORE_AUX);
 }
 template <typename T>
 __device__ __forceinline__ bool get_granule(__amdgpu_buffer_rsrc_t rs, int idx, unsigned epoch, T& v) {

@@ -36,7 +36,7 @@ PHASE = re.compile(r"k_estep|k_sstats|k_fixup|rocprim|fillBuffer|k_part_|k_fill_
 # k_estep_grid64 / k_estep_rows64 <shape, true, false, LONG>; k_estep_wide_mc / _tc <T, Q, NR, true>
 ESTEP = re.compile(r"k_estep_grid64<DShape<[^>]*>, true, false, (true|false)>$"  # round-2 profiles
                    r"|k_estep_rows64(_long)?<RShape<[^>]*>, true, false(, (true|false))?>$"
-                   r"|k_estep_grid(_long)?<GShape<[^>]*>, true, false>$"
+                   r"|k_estep_grid(_long)?<GShape<[^>]*>, true, false(, (true|false))?>$"
                    r"|k_estep_wide_(mc|tc)<\w+, \d+, \d+, true>$"
                    r"|k_estep(_wave|_wide)?<(?!DShape|RShape|GShape).*, true, false>$")
 
