@@ -387,9 +387,10 @@ __global__ __launch_bounds__(64 * kDocWaves, 8) void k_doc_hash_sort(const uint8
 // ---- single pass (round 4) for corpora whose documents all hold ≤ kFusedCap tokens (known at upload):
 // hash + register sort + CSR emission in one kernel, the row offsets from a decoupled look-back over
 // tiles of kDocWaves documents — no sorted-key array, no nnz scan, no second pass over the keys.
-// Workgroups take tiles in ticket order (an atomic counter), so every tile a look-back waits on is held
-// by a running workgroup that reaches it waiting only on lower tiles: no dependence on dispatch order or
-// residency.  A look-back that waits past its poll bound sets the fault word; the host then rebuilds
+// Workgroups take tiles in ticket order — eight counters, one per XCD, counter c handing out tiles
+// c, c + 8, … in order — so every tile a look-back waits on is held by a running workgroup, or is the
+// next one its counter hands out to a workgroup whose own look-back waits only on lower tiles (the
+// lowest unpublished tile always makes progress): no dependence on dispatch order or residency.  A look-back that waits past its poll bound sets the fault word; the host then rebuilds
 // the CSR with the sorted-key passes (mode 0).  Measured without gain: batching tickets (2–8 consecutive
 // tiles per atomic: 1.2× to 300× slower, a batch's later tiles publish their counts an iteration late)
 // and a static tile order over a resident grid (tile = step·grid + blockIdx: 2.89 vs 2.11 ms, a slow
@@ -397,6 +398,10 @@ __global__ __launch_bounds__(64 * kDocWaves, 8) void k_doc_hash_sort(const uint8
 // (flag 1: the tile's own entry count, 2: the inclusive count of tiles 0..t), written by one lane with
 // agent-scope atomic stores and read with agent-scope atomic loads (vector memory, L2-coherent).
 constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = kLbAgg - 1;
+// the ticket counters: one per XCD, each on its own 128-byte line (one word takes ≈ 88 returning atomics
+// per µs — MI355X_MICROARCH.md "dequeue" — against 125 k tiles per launch at config 2)
+constexpr int kTicketPitch = 16;                       // u64 words between counters
+constexpr int kTicketWords = kTicketPitch * 9;         // fault word's line + 8 counters
 
 // the exclusive entry count before `tile` (wave 0 of the workgroup; every lane returns it)
 // A bounded wait: a predecessor silent for ~2^20 polls (far beyond any tile's run time) sets *fault and the
@@ -513,7 +518,8 @@ __global__ __launch_bounds__(64 * kEmitWaves, TF_EMIT_OCC) void k_doc_hash_emit(
   int32_t xq[4];
   int nq = 0, hq = 0, preq = 0, aggq = 0;
   for (;;) {
-    if (threadIdx.x == 0) tile_s = (int)atomicAdd(ticket, 1ull);
+    if (threadIdx.x == 0)  // counter c hands out tiles c, c + 8, … (one counter per XCD: blockIdx % 8)
+      tile_s = (int)(atomicAdd(ticket + kTicketPitch * (blockIdx.x & 7), 1ull) * 8 + (blockIdx.x & 7));
     __syncthreads();
     const int64_t tile = __builtin_amdgcn_readfirstlane(tile_s);
     const bool have = tile < tiles;  // the tickets only grow: once past the end, the loop drains tp and exits
@@ -553,7 +559,7 @@ __global__ __launch_bounds__(64 * kEmitWaves, TF_EMIT_OCC) void k_doc_hash_emit(
     }
     if (tp >= 0) {
       if (wv == 0) {
-        const int64_t ex = tile_lookback(status, tp, aggq, lane, status + tiles + 1, max_polls);
+        const int64_t ex = tile_lookback(status, tp, aggq, lane, status + tiles, max_polls);
         if (lane == 0) base_s = ex;
       }
       __syncthreads();
@@ -741,9 +747,9 @@ static bool single_pass(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off6
   hipStream_t st = c.stream;
   const int64_t tiles = ceil_div(n_docs, (int64_t)kEmitWaves);
   DevBuf& lb = c.scratch[2];
-  lb.reserve(sizeof(uint64_t) * (tiles + 2));
-  uint64_t* status = lb.as<uint64_t>();  // [tiles] look-back words, then the ticket, then the fault word
-  HIP_CHECK(hipMemsetAsync(status, 0, sizeof(uint64_t) * (tiles + 2), st));
+  lb.reserve(sizeof(uint64_t) * (tiles + kTicketWords));
+  uint64_t* status = lb.as<uint64_t>();  // [tiles] look-back words, the fault word, 8 ticket counters
+  HIP_CHECK(hipMemsetAsync(status, 0, sizeof(uint64_t) * (tiles + kTicketWords), st));
   HIP_CHECK(hipMemsetAsync(out.indptr.p, 0, sizeof(int64_t), st));
   // nnz ≤ n_tok: the output is sized before the counts exist
   out.indices.reserve(sizeof(int32_t) * n_tok);
@@ -781,7 +787,7 @@ static bool single_pass(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off6
       }
       const int64_t resident = (int64_t)std::max(per_cu, 1) * c.cus;
       const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(tiles, resident));
-      unsigned long long* ticket = reinterpret_cast<unsigned long long*>(status + tiles);
+      unsigned long long* ticket = reinterpret_cast<unsigned long long*>(status + tiles + kTicketPitch);
       const uint8_t* u8 = d_utf8;
       const int64_t* doff = d_doc_off;
       int64_t nd = n_docs;
@@ -809,7 +815,7 @@ static bool single_pass(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off6
   int64_t total = 0;
   uint64_t fault = 0;
   HIP_CHECK(hipMemcpyAsync(&total, out.indptr.as<int64_t>() + n_docs, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipMemcpyAsync(&fault, status + tiles + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipMemcpyAsync(&fault, status + tiles, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipStreamSynchronize(st));
   if (fault) {
     ++c.tf_fallbacks;

@@ -479,7 +479,11 @@ __global__ __launch_bounds__(256) void k_transform(const int32_t* __restrict__ i
 // slots (id mod 2^14), the idf of the slot's highest-df id and that id's tag (id >> 14, u8), so a
 // workgroup holds 144 KB of the table in LDS and gathers from L2 only on a tag miss.  Config 2: ~75 %
 // of entries hit.  Tags need ids < 2^21 (numFeatures ≤ 2^21; larger vocabularies use k_transform).
-constexpr int kCacheBits = 14;
+#ifndef IDF_CACHE_BITS
+#define IDF_CACHE_BITS 14  // 2^14 slots, 144 KB: one workgroup per CU
+#endif
+constexpr int kCacheBits = IDF_CACHE_BITS;
+constexpr int kCacheWgPerCu = IDF_CACHE_BITS <= 13 ? 2 : 1;  // workgroups whose tables fit a CU's LDS
 constexpr int kCacheSlots = 1 << kCacheBits;
 constexpr int kCacheThreads = 1024;
 #ifndef IDF_CACHE_UNROLL
@@ -580,7 +584,7 @@ void transform(Ctx& c, DCsr& m, const double* d_idf, double zero_floor, const De
     const double* cval = cache->as<double>();
     const uint8_t* ctag = reinterpret_cast<const uint8_t*>(cval + kCacheSlots);
     const size_t lds = sizeof(double) * kCacheSlots + kCacheSlots;
-    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(c.cus, ceil_div(m.nnz / 4, (int64_t)kCacheThreads)));
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)c.cus * kCacheWgPerCu, ceil_div(m.nnz / 4, (int64_t)kCacheThreads)));
     if (m.dtype == STC_F32) {
       HIP_CHECK(hipFuncSetAttribute((const void*)k_transform_cached<float>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       k_transform_cached<float><<<g, kCacheThreads, lds, c.stream>>>(m.indices.as<int32_t>(), m.values.as<float>(),
