@@ -17,6 +17,7 @@
 #include <mutex>
 #include <thread>
 #include <type_traits>
+#include <unordered_set>
 
 #include "lda_kernels.h"
 
@@ -30,6 +31,10 @@ void set_last_error(const std::string& msg) { g_last_error = msg; }
 using namespace stc;
 
 struct stc_ctx : Ctx {};
+
+// the contexts that exist (stc_dcsr_free hands a matrix's buffers back only to a live one)
+static std::mutex g_live_mu;
+static std::unordered_set<stc_ctx*> g_live;
 struct stc_dcsr : DCsr {};
 struct stc_dtok {
   Ctx* ctx = nullptr;  // the context it was uploaded on; only it may read the buffers
@@ -1081,6 +1086,10 @@ int stc_init(int device, stc_ctx** out) {
     HIP_CHECK(hipSetDevice(device));
     HIP_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIP_CHECK(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device));
+    {
+      std::lock_guard<std::mutex> lk(g_live_mu);
+      g_live.insert(c.get());
+    }
     const char* db = std::getenv("STC_DF_BINNED");  // A/B knob: the round-3 binned df count
     c->df_tiled = !(db && db[0] == '1');
     const char* d32 = std::getenv("STC_DF_U32");  // A/B knob: the u32 tiled count for unique-id rows too
@@ -1098,6 +1107,10 @@ int stc_init(int device, stc_ctx** out) {
 int stc_destroy(stc_ctx* ctx) {
   return guard([&] {
     if (!ctx) return;
+    {
+      std::lock_guard<std::mutex> lk(g_live_mu);
+      g_live.erase(ctx);
+    }
     (void)hipSetDevice(ctx->device);
     if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1163,9 +1176,9 @@ int stc_dcsr_upload(stc_ctx* ctx, int64_t n_rows, int64_t n_cols, const int64_t*
     m->dtype = value_dtype;
     m->max_row = 0;
     for (int64_t r = 0; r < n_rows; ++r) m->max_row = std::max(m->max_row, indptr[r + 1] - indptr[r]);
-    m->indptr.reserve(8 * (n_rows + 1));
-    m->indices.reserve(4 * std::max<int64_t>(nnz, 1));
-    m->values.reserve((value_dtype == STC_F32 ? 4 : 8) * std::max<int64_t>(nnz, 1));
+    ctx->recycle.take(m->indptr, 8 * (n_rows + 1));
+    ctx->recycle.take(m->indices, 4 * std::max<int64_t>(nnz, 1));
+    ctx->recycle.take(m->values, (value_dtype == STC_F32 ? 4 : 8) * std::max<int64_t>(nnz, 1));
     HIP_CHECK(hipMemcpyAsync(m->indptr.p, indptr, 8 * (n_rows + 1), hipMemcpyHostToDevice, ctx->stream));
     if (nnz > 0) {
       HIP_CHECK(hipMemcpyAsync(m->indices.p, indices, 4 * nnz, hipMemcpyHostToDevice, ctx->stream));
@@ -1219,6 +1232,14 @@ int stc_dcsr_free(stc_dcsr* m) {
   return guard([&] {
     if (!m) return;
     if (m->device >= 0) (void)hipSetDevice(m->device);
+    {  // hand the allocations back to the context that made it, if it still exists (Recycler)
+      std::lock_guard<std::mutex> lk(g_live_mu);
+      if (m->ctx && g_live.count(static_cast<stc_ctx*>(m->ctx)) && m->ctx->device == m->device) {
+        m->ctx->recycle.put(m->indices);
+        m->ctx->recycle.put(m->values);
+        m->ctx->recycle.put(m->indptr);
+      }
+    }
     delete m;
   });
 }
@@ -1442,11 +1463,17 @@ namespace {
 // IDF.fit on the device: df (all ranks' when connected), m, idf into the given buffers
 void idf_fit_impl(Ctx& c, const DCsr& tf, int64_t min_doc_freq, DevBuf& df, DevBuf& idf, int64_t& m) {
   hipStream_t s = c.stream;
-  df.reserve(8 * tf.cols);
-  idf.reserve(8 * tf.cols);
-  idf::doc_freq(c, tf, df.as<int64_t>());
+  c.recycle.take(df, 8 * tf.cols);
+  c.recycle.take(idf, 8 * tf.cols);
   m = tf.rows;
-  if (c.coll()) {  // DocumentFrequencyAggregator.merge over ranks
+  if (!c.coll()) {  // m known: idf written by the df reduction itself
+    const idf::IdfFinal fin{(double)m, min_doc_freq, idf.as<double>()};
+    if (idf::doc_freq(c, tf, df.as<int64_t>(), &fin)) return;
+    idf::finalize(c, df.as<int64_t>(), tf.cols, m, min_doc_freq, idf.as<double>());
+    return;
+  }
+  idf::doc_freq(c, tf, df.as<int64_t>());
+  {  // DocumentFrequencyAggregator.merge over ranks
     DevBuf mm;
     mm.reserve(8);
     HIP_CHECK(hipMemcpyAsync(mm.p, &m, 8, hipMemcpyHostToDevice, s));
@@ -1527,6 +1554,13 @@ int stc_didf_free(stc_didf* md) {
   return guard([&] {
     if (!md) return;
     (void)hipSetDevice(md->device);
+    {  // back to the context that made it, if it still exists (Recycler)
+      std::lock_guard<std::mutex> lk(g_live_mu);
+      if (md->ctx && g_live.count(static_cast<stc_ctx*>(md->ctx)) && md->ctx->device == md->device) {
+        md->ctx->recycle.put(md->idf);
+        md->ctx->recycle.put(md->df);
+      }
+    }
     delete md;
   });
 }

@@ -752,8 +752,8 @@ static bool single_pass(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off6
   HIP_CHECK(hipMemsetAsync(status, 0, sizeof(uint64_t) * (tiles + kTicketWords), st));
   HIP_CHECK(hipMemsetAsync(out.indptr.p, 0, sizeof(int64_t), st));
   // nnz ≤ n_tok: the output is sized before the counts exist
-  out.indices.reserve(sizeof(int32_t) * n_tok);
-  out.values.reserve((value_dtype == STC_F32 ? 4 : 8) * n_tok);
+  c.recycle.take(out.indices, sizeof(int32_t) * n_tok);
+  c.recycle.take(out.values, (value_dtype == STC_F32 ? 4 : 8) * n_tok);
   // mode 1 (default): hashed inside the per-document pass; mode 2: the tokens hashed flat first (k_hash,
   // four independent chains per lane), the per-document pass then loads, sorts and emits
   const bool flat = c.tf_mode == 2;
@@ -835,7 +835,7 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off64, const 
   out.rows = n_docs;
   out.cols = num_features;
   out.dtype = value_dtype;
-  out.indptr.reserve(sizeof(int64_t) * (n_docs + 1));
+  c.recycle.take(out.indptr, sizeof(int64_t) * (n_docs + 1));
   if (n_tok == 0) {
     HIP_CHECK(hipMemsetAsync(out.indptr.p, 0, sizeof(int64_t) * (n_docs + 1), st));
     out.nnz = 0;
@@ -924,8 +924,8 @@ void build_csr(Ctx& c, const uint8_t* d_utf8, const int64_t* d_tok_off64, const 
   out.nnz = total;
   out.positive = true;  // counts ≥ 1 (binary: 1)
   out.unique_ids = true;  // one entry per distinct id
-  out.indices.reserve(sizeof(int32_t) * std::max<int64_t>(total, 1));
-  out.values.reserve((value_dtype == STC_F32 ? 4 : 8) * std::max<int64_t>(total, 1));
+  c.recycle.take(out.indices, sizeof(int32_t) * std::max<int64_t>(total, 1));
+  c.recycle.take(out.values, (value_dtype == STC_F32 ? 4 : 8) * std::max<int64_t>(total, 1));
   const uint8_t* fl = n_large > 0 ? flags.as<uint8_t>() : nullptr;
   if (value_dtype == STC_F32)
     k_doc_runs<true, float><<<g, 64 * kDocWaves, 0, st>>>(sorted.as<int32_t>(), sorted_l.as<int32_t>(), fl, large, n_large,

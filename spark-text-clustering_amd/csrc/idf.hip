@@ -272,11 +272,13 @@ __global__ __launch_bounds__(kTiledThreads) void k_df_rows16(const int32_t* __re
 }
 
 __global__ __launch_bounds__(256) void k_df_reduce(const uint32_t* __restrict__ part, int64_t chunks, int64_t cols,
-                                                   int64_t* __restrict__ df) {
+                                                   int64_t* __restrict__ df, double m, int64_t min_df,
+                                                   double* __restrict__ idf /* nullptr: df only */) {
   for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < cols; j += (int64_t)gridDim.x * 256) {
     int64_t s = 0;
     for (int64_t c = 0; c < chunks; ++c) s += part[c * cols + j];
     df[j] = s;
+    if (idf) idf[j] = s >= min_df ? log((m + 1.0) / ((double)s + 1.0)) : 0.0;  // as k_idf
   }
 }
 
@@ -299,10 +301,15 @@ __global__ __launch_bounds__(256) void k_runs(const uint32_t* __restrict__ k, in
   }
 }
 
-void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df) {
+bool doc_freq(Ctx& c, const DCsr& m, int64_t* d_df, const IdfFinal* fin) {
   hipStream_t s = c.stream;
-  HIP_CHECK(hipMemsetAsync(d_df, 0, sizeof(int64_t) * m.cols, s));
-  if (m.nnz == 0) return;
+  const double fin_m = fin ? fin->m : 0.0;
+  const int64_t fin_min = fin ? fin->min_df : 0;
+  double* const fin_idf = fin ? fin->idf : nullptr;
+  if (m.nnz == 0) {
+    HIP_CHECK(hipMemsetAsync(d_df, 0, sizeof(int64_t) * m.cols, s));
+    return false;
+  }
   if (m.unique_ids && m.cols <= (int64_t(kMaxTiles / 2) << kTile16Bits) && c.df_tiled && c.df_rows16 &&
       m.rows > 0) {
     const int T = (int)ceil_div(m.cols, (int64_t)1 << kTile16Bits);
@@ -318,9 +325,9 @@ void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df) {
     k_df_rows16<<<(unsigned)(T * G), kTiledThreads, lds, s>>>(m.indices.as<int32_t>(), m.indptr.as<int64_t>(), m.rows,
                                                               T, G, rpg, m.cols, part.as<uint32_t>());
     KERNEL_CHECK();
-    k_df_reduce<<<grid_for(m.cols), 256, 0, s>>>(part.as<uint32_t>(), G, m.cols, d_df);
+    k_df_reduce<<<grid_for(m.cols), 256, 0, s>>>(part.as<uint32_t>(), G, m.cols, d_df, fin_m, fin_min, fin_idf);
     KERNEL_CHECK();
-    return;
+    return fin != nullptr;
   }
   if (m.cols <= (int64_t(kMaxTiles) << kTileBits) && c.df_tiled) {
     const int T = (int)ceil_div(m.cols, (int64_t)kTile);
@@ -349,9 +356,9 @@ void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df) {
           part.as<uint32_t>());
     }
     KERNEL_CHECK();
-    k_df_reduce<<<grid_for(m.cols), 256, 0, s>>>(part.as<uint32_t>(), G, m.cols, d_df);
+    k_df_reduce<<<grid_for(m.cols), 256, 0, s>>>(part.as<uint32_t>(), G, m.cols, d_df, fin_m, fin_min, fin_idf);
     KERNEL_CHECK();
-    return;
+    return fin != nullptr;
   }
   if (m.cols <= (int64_t(kMaxTiles) << kTileBits)) {
     const int T = (int)ceil_div(m.cols, (int64_t)kTile);
@@ -384,11 +391,12 @@ void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df) {
     k_df_binned<<<(unsigned)(T * groups), kTileThreads, lds, s>>>(bins.as<uint16_t>(), tab.as<int32_t>(), chunks,
                                                                   per_group, T, m.cols, part.as<uint32_t>());
     KERNEL_CHECK();
-    k_df_reduce<<<grid_for(m.cols), 256, 0, s>>>(part.as<uint32_t>(), groups, m.cols, d_df);
+    k_df_reduce<<<grid_for(m.cols), 256, 0, s>>>(part.as<uint32_t>(), groups, m.cols, d_df, fin_m, fin_min, fin_idf);
     KERNEL_CHECK();
-    return;
+    return fin != nullptr;
   }
   STC_REQUIRE(m.nnz < (int64_t(1) << 31), "idf: at most 2^31-1 entries per call");
+  HIP_CHECK(hipMemsetAsync(d_df, 0, sizeof(int64_t) * m.cols, s));  // k_runs adds into it
   const uint32_t sentinel = (uint32_t)m.cols;
   int nbits = 1;
   while ((int64_t(1) << nbits) <= (int64_t)sentinel) ++nbits;
@@ -413,6 +421,7 @@ void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df) {
   k_runs<<<grid_for(m.nnz), 256, 0, s>>>(sorted.as<uint32_t>(), m.nnz, sentinel, d_df);
   KERNEL_CHECK();
   HIP_CHECK(hipStreamSynchronize(s));  // tmp dies at scope exit
+  return false;
 }
 
 // DocumentFrequencyAggregator.idf(): df >= minDocFreq ? ln((m + 1) / (df + 1)) : 0

@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -98,6 +99,52 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// Device allocations a freed stc_dcsr handed back to the context that made it, so the next output of a
+// similar size (HashingTF, upload) takes one instead of calling hipMalloc (tens of µs for GB-sized
+// buffers, inside every call).  At most kMax are kept; the context frees them when it is destroyed.
+struct Recycler {
+  static constexpr size_t kMax = 6;
+  static constexpr size_t kMin = size_t(1) << 20;  // smaller buffers are freed, not kept
+  std::mutex mu;
+  std::vector<std::pair<void*, size_t>> bufs;
+  void put(DevBuf& b) {  // takes b's allocation (b is empty afterwards)
+    if (!b.p || b.bytes < kMin) return;
+    std::lock_guard<std::mutex> lk(mu);
+    if (bufs.size() >= kMax) {  // drop the smallest kept one (or this one)
+      size_t sm = 0;
+      for (size_t i = 1; i < bufs.size(); ++i)
+        if (bufs[i].second < bufs[sm].second) sm = i;
+      if (bufs[sm].second >= b.bytes) return;
+      (void)hipFree(bufs[sm].first);
+      bufs.erase(bufs.begin() + (std::ptrdiff_t)sm);
+    }
+    bufs.emplace_back(b.p, b.bytes);
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  void take(DevBuf& b, size_t n) {  // b.reserve(n), from a kept allocation of n…2n bytes when one exists
+    if (n <= b.bytes) return;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      size_t best = bufs.size();
+      for (size_t i = 0; i < bufs.size(); ++i)
+        if (bufs[i].second >= n && bufs[i].second <= 2 * n && (best == bufs.size() || bufs[i].second < bufs[best].second))
+          best = i;
+      if (best < bufs.size()) {
+        b.release();
+        b.p = bufs[best].first;
+        b.bytes = bufs[best].second;
+        bufs.erase(bufs.begin() + (std::ptrdiff_t)best);
+        return;
+      }
+    }
+    b.reserve(n);
+  }
+  ~Recycler() {
+    for (auto& x : bufs) (void)hipFree(x.first);
+  }
+};
+
 // ---------------------------------------------------------------------------------------
 // Context: one device, one stream, optional RCCL communicator.
 // ---------------------------------------------------------------------------------------
@@ -119,6 +166,7 @@ struct Ctx {
   bool tf_force_fault = false;  // test knob (STC_TF_FAULT=1): every look-back gives up at once
   int64_t tf_fallbacks = 0;     // single passes that fell back to the sorted-key passes
   bool idf_cache = true;  // idf.hip: the device IDF model's hot-idf LDS table (STC_IDF_NO_CACHE=1: off)
+  Recycler recycle;    // freed stc_dcsr allocations for the next outputs (stc_dcsr_free)
   DevBuf scratch[12];  // grow-only scratch of the featurisation kernels (hashing_tf.hip, idf.hip, api.hip IDF)
   DevBuf coll_tmp;    // the in-process all-reduce's staging buffer
   void use() const { HIP_CHECK(hipSetDevice(device)); }
@@ -512,7 +560,14 @@ void tokenize(Ctx& c, const uint8_t* d_text, const int64_t* d_text_off, int64_t 
               int64_t& n_out_bytes);
 }  // namespace tokenizer
 namespace idf {
-void doc_freq(Ctx& c, const DCsr& m, int64_t* d_df /* cols */);
+// idf finalised inside the df reduction when the caller already knows m (no collective in between)
+struct IdfFinal {
+  double m;
+  int64_t min_df;
+  double* idf;
+};
+// df (cols); with fin, also idf when the path allows — returns true then (else call finalize)
+bool doc_freq(Ctx& c, const DCsr& m, int64_t* d_df /* cols */, const IdfFinal* fin = nullptr);
 void finalize(Ctx& c, const int64_t* d_df, int64_t cols, int64_t m, int64_t min_df, double* d_idf);
 // cache: the hot-idf table build_cache made for this idf (nullptr: plain gathers)
 void transform(Ctx& c, DCsr& m, const double* d_idf, double zero_floor, const DevBuf* cache = nullptr);
