@@ -280,3 +280,31 @@ def test_hashing_tf_single_pass_orders_and_fallback(ctx, monkeypatch):
         assert np.array_equal(m.indptr, ref.indptr), tag
         assert np.array_equal(m.indices, ref.indices), tag
         assert np.array_equal(m.values, ref.values), tag
+
+
+def test_recycled_output_buffers_carry_no_stale_data(ctx, oracle):
+    """A freed stc_dcsr / stc_didf hands its allocations back to the context (api.hip Recycler); the next
+    HashingTF / IDF outputs of similar size reuse them: results of a large corpus, then a smaller one,
+    then the large one again, each equal to the oracle (no entry of an earlier output survives)."""
+    import stc
+    from stc import synth
+
+    big = synth.token_corpus(6000, 60, n_words=20000, seed=31)[0]
+    small = synth.token_corpus(4500, 60, n_words=20000, seed=32)[0]
+    for blob, tok_off, doc_off in (big, small, big):
+        dt = stc.DeviceTokens(ctx, blob, tok_off, doc_off)
+        d = stc.HashingTF(numFeatures=1 << 18, ctx=ctx).transform_tokens_device(dt)
+        m = stc.IDF(minDocFreq=2, ctx=ctx).fit_device(d)
+        m.transform_device(d, zero_floor=1e-4)
+        got = d.download()
+        raw = blob.tobytes()
+        n_docs = doc_off.size - 1
+        docs = [[raw[tok_off[t]:tok_off[t + 1]] for t in range(doc_off[i], doc_off[i + 1])] for i in range(n_docs)]
+        ip, ix, vv = oracle.hashing_tf(docs, 1 << 18, False, oracle.HASH_SPARK24)
+        idf_o, df_o, _ = oracle.idf_fit(ip, ix, vv, 1 << 18, 2)
+        assert np.array_equal(got.indptr, ip) and np.array_equal(got.indices, ix)
+        np.testing.assert_allclose(got.values, oracle.idf_transform(ix, vv, idf_o, floor=1e-4), rtol=1e-15, atol=0)
+        assert np.array_equal(m.docFreq, df_o)
+        m.free()
+        d.free()
+        dt.free()
