@@ -217,7 +217,7 @@ def cpu_baseline(h, corpus, a, budget_s=12.0):
                       f"mean inner iters {iters / max(1, done):.1f}; {dt:.1f} s"}
 
 
-def featurization(stc, ctx, a, log, tokens, reps=3):
+def featurization(stc, ctx, a, log, tokens, reps=5):
     """HashingTF (2^18 buckets, Spark 2.4.3's murmur3 tail) → IDF(minDocFreq = 2) fit → TF·IDF transform
     with the reference's 1e-4 floor (LDAClustering.scala:154-192), all on the GPU over a token corpus
     already resident in HBM (stc_tokens_upload before timing).  One pass = the three calls, each
@@ -524,6 +524,14 @@ def main():
         r.update(elapsed=el, docs_all=d, entries_all=e, iters_all=it)
         return r
 
+    # the featurisation line first, as the pipeline runs (HashingTF → IDF precede the LDA training,
+    # LDAClustering.scala:154-192 → :61), on a device holding only the uploaded corpus
+    feat = None
+    if secondary:
+        log("featurisation")
+        feat = featurization(stc, ctx, a, log, tokens)
+        del tokens
+
     r = run_state(model, lam_head, barrier, log, a, a.dtype, a.steps, a.warmup)
     head = summarize(reduce_run(r), a, a.dtype, world, a.steps, a.corpus, kernel_name(a.dtype, a.k))
     h = model.h
@@ -544,9 +552,7 @@ def main():
                               dtype=dt, corpus="zipf-lda", **s3))
             dp.free()
         dcorp[other].free()
-        log("featurisation")
-        lines.append(featurization(stc, ctx, a, log, tokens))
-        del tokens
+        lines.append(feat)
 
     if rank != 0:
         if dist is not None:
