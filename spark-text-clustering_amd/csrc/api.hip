@@ -513,7 +513,8 @@ TeamChoice team_choice(const stc_lda& L, double mean_rows) {
   const double need = 1.05 * mean_rows;
   if (L.team_force == 1) return {1, false};
   if (L.k <= 512) {
-    int P = L.team_force > 1 ? L.team_force : (int)std::ceil(need / std::max(lda::wide_resident_rows<T>(L.k), 1));
+    if (L.team_force > 1) return {L.team_force, false};
+    const int P = (int)std::ceil(need / std::max(lda::wide_resident_rows<T>(L.k), 1));
     return {std::max(1, std::min(P, 4)), false};
   }
   if (L.team_force > 1) return {std::max(L.team_force, (L.k + 2047) / 2048), true};
@@ -1663,7 +1664,7 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     const char* sd = std::getenv("STC_SORT_DOCS");
     L->sort_docs = !(sd && sd[0] == '0');
     const char* wt = std::getenv("STC_WIDE_TEAM");
-    L->team_force = wt ? std::max(0, std::min(4, std::atoi(wt))) : 0;
+    L->team_force = wt ? std::max(0, std::min(8, std::atoi(wt))) : 0;
     const char* fc = std::getenv("STC_COLLECTIVE_MSTEP");
     L->force_coll = fc && fc[0] == '1';
     ensure_layout(*L);  // λ, Bp, stat, logscale, colpart for the current shard count
