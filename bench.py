@@ -113,6 +113,34 @@ def estep_sources_sha():
     return h.hexdigest()[:16]
 
 
+# the featurisation kernels' sources: its PMC entry counts only if measured on these exact files
+FEAT_SOURCES = ("hashing_tf.hip", "idf.hip", "stc_internal.h")
+FEAT_PMC = os.path.join(ROOT, "profiles", "r04_featurisation_pmc.json")
+
+
+def feat_sources_sha():
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in FEAT_SOURCES:
+        with open(os.path.join(ROOT, "spark-text-clustering_amd", "csrc", f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+def feat_traffic():
+    """HBM bytes per call of each featurisation stage from the committed PMC summary
+    (tools/gpu_featpmc.sh → tools/feat_pmc_summary.py), if measured on this tree's sources."""
+    try:
+        with open(FEAT_PMC) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return None, "no featurisation PMC summary committed"
+    if pm.get("feat_sources_sha") != feat_sources_sha():
+        return None, f"{os.path.basename(FEAT_PMC)} was measured on other featurisation sources"
+    return {k: v["bytes_per_call"] for k, v in pm["stages"].items()}, f"{os.path.basename(FEAT_PMC)} ({pm.get('note', '')})"
+
+
 def pmc_traffic(a, dtype, corpus):
     """HBM bytes per launch of the training E-step kernel from the committed PMC summary
     (tools/pmc_summary.py over tools/gpu_prof.sh's separate FETCH_SIZE / WRITE_SIZE passes), if it
@@ -260,6 +288,7 @@ def featurization(stc, ctx, a, log, tokens, reps=5):
     b_fit = nnz * 4 + 2 * 8.0 * V  # a HashingTF matrix's values are known > 0: df reads the ids only
     b_tr = nnz * (4 + 8 + 8) + 8.0 * V
     total = float(t.sum())
+    traffic, traffic_src = feat_traffic()
     return {
         "label": f"featurisation: HashingTF(2^{int(V).bit_length() - 1}, spark24 murmur3) -> IDF(2).fit -> "
                  "transform(1e-4 floor), tokens resident in HBM",
@@ -270,7 +299,8 @@ def featurization(stc, ctx, a, log, tokens, reps=5):
         "ms": {"hashing_tf": round(t[0] * 1e3, 3), "idf_fit": round(t[1] * 1e3, 3), "idf_transform": round(t[2] * 1e3, 3)},
         "roofline": {"bound": "hbm", "achieved": (b_hash + b_fit + b_tr) / total / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": (b_hash + b_fit + b_tr) / total / 1e9 / HBM_PEAK_GBS,
-                     "algorithmic_bytes": {"hashing_tf": b_hash, "idf_fit": b_fit, "idf_transform": b_tr}},
+                     "algorithmic_bytes": {"hashing_tf": b_hash, "idf_fit": b_fit, "idf_transform": b_tr},
+                     "traffic": traffic, "traffic_source": traffic_src},
     }
 
 
