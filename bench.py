@@ -100,7 +100,7 @@ def algorithmic_bytes(nnz, k, docs, dtype):
 
 
 # the E-step kernels' sources: a PMC entry counts only if it was measured on these exact files
-ESTEP_SOURCES = ("lda_rows64.hip", "lda_grid.hip", "lda_wide.hip", "lda.hip", "estep_common.h", "lda_kernels.h")
+ESTEP_SOURCES = ("lda_rows64.hip", "psi64.h", "lda_grid.hip", "lda_wide.hip", "lda.hip", "estep_common.h", "lda_kernels.h")
 
 
 def estep_sources_sha():
