@@ -16,6 +16,7 @@
 //   γ, ψ(γ), exp on the lane's own topics.  ψ(Σγ') from Σγ' = Σα + Σ_n r_n·(φ_n − ε'_n) (exact in
 //     real arithmetic), summed by the r lanes next to r — two barriers per iteration.
 #include "estep_common.h"
+#include "psi64.h"
 
 namespace stc {
 namespace lda {
@@ -69,7 +70,13 @@ struct WTr<double> {
   static __device__ __forceinline__ double wsum(double v) { return wave_sum_d(v); }
   static __device__ __forceinline__ double rcp(double x) { return rcp_nr(x); }
   // eθ' = exp(ψ(g) − cs − ψc): pc holds ψc
-  static __device__ __forceinline__ double eth(double g, double cs, double pc) { return exp_digamma_minus_d(g, cs + pc); }
+  static __device__ __forceinline__ double eth(double g, double cs, double pc) {
+#if WIDE_PSI_V2
+    return exp_digamma_minus_v2<2>(g, cs + pc);  // psi64.h: branch-free, constants as SGPR operands
+#else
+    return exp_digamma_minus_d(g, cs + pc);
+#endif
+  }
   static __device__ __forceinline__ double pcload(const double* psic, int k, int t) { (void)k; return psic[t]; }
   static __device__ __forceinline__ double psi(double x) { return digamma_fast_d(x); }
   static __device__ __forceinline__ double eps_floor() { return 0.0; }
@@ -204,6 +211,11 @@ __host__ __device__ constexpr size_t wide_lds_fixed() {
   return (sizeof(WLds<T>) + 255) / 256 * 256;
 }
 
+#ifndef WIDE_PSI_V2
+// fp64 γ update through psi64.h's chain (as k_estep_rows64) instead of exp_digamma_minus_d + libm exp:
+// config 4 E-step 301 → 286 ms, config 5 44.1 → 43.3 ms (r04), parity unchanged
+#define WIDE_PSI_V2 1
+#endif
 #ifndef WIDE_LB_BYTES
 #define WIDE_LB_BYTES 64  // streamed-row loads in flight per lane (bytes)
 #endif
