@@ -213,7 +213,8 @@ __host__ __device__ constexpr size_t wide_lds_fixed() {
 
 #ifndef WIDE_PSI_V2
 // fp64 γ update through psi64.h's chain (as k_estep_rows64) instead of exp_digamma_minus_d + libm exp:
-// config 4 E-step 301 → 286 ms, config 5 44.1 → 43.3 ms (r04), parity unchanged
+// one ψ/exp form across the fp64 E-step kernels; measured neutral at config 4 (277 ms either way over
+// 20 steps after 10 warm-up), parity unchanged
 #define WIDE_PSI_V2 1
 #endif
 #ifndef WIDE_LB_BYTES
