@@ -129,3 +129,23 @@ def test_traffic_is_null_with_a_reason_unless_measured_on_these_sources(tmp_path
                                           "estep_sources_sha": bench.estep_sources_sha()}]}))
     assert bench.pmc_traffic(A, "f64", "zipf")[0] == 4.6e9
     assert np.isfinite(bench.pmc_traffic(A, "f64", "zipf")[0])
+
+
+def test_featurisation_traffic_is_bound_to_its_sources(tmp_path, monkeypatch):
+    """The featurisation line's `traffic` comes from the committed PMC summary only when it was measured on
+    this tree's featurisation sources (bench.FEAT_SOURCES); otherwise null with the reason."""
+    p = tmp_path / "feat_pmc.json"
+    monkeypatch.setattr(bench, "FEAT_PMC", str(p))
+    t, why = bench.feat_traffic()
+    assert t is None and "no featurisation PMC" in why
+    stages = {"hashing_tf": {"bytes_per_call": 4.4e9}, "idf_fit": {"bytes_per_call": 0.8e9},
+              "idf_transform": {"bytes_per_call": 3.3e9}}
+    p.write_text(json.dumps({"feat_sources_sha": "0" * 16, "stages": stages}))
+    t, why = bench.feat_traffic()
+    assert t is None and "other featurisation sources" in why
+    p.write_text(json.dumps({"feat_sources_sha": bench.feat_sources_sha(), "stages": stages}))
+    t, _ = bench.feat_traffic()
+    assert t == {"hashing_tf": 4.4e9, "idf_fit": 0.8e9, "idf_transform": 3.3e9}
+    # the committed summary matches this tree
+    monkeypatch.undo()
+    assert bench.feat_traffic()[0] is not None
