@@ -23,7 +23,7 @@ roofline: the dominant kernel (the training E-step: k_estep_rows64 for fp64, k_e
 fp32; one launch per minibatch): SURVEY.md §8(d) algorithmic bytes per doc
 (nnz·(4 + s) + 2·nnz·k·s + s·k, s = 8 for fp64, 4 for fp32) × the launch's docs ÷ its HIP-event time
 on the library stream; traffic: the PMC FETCH_SIZE(×2, gfx950) + WRITE_SIZE per launch of that
-kernel from the committed rocprofv3 summary of this workload (profiles/, tools/gpu_prof.sh).
+kernel from the committed rocprofv3 summary of this workload (profiles/, tools/gpu.sh prof).
 roofline_compute: the same kernel's flops (4·nnz·k per inner iteration) against the dtype's peak.
 cpu_baseline: oracle/lda_oracle.c oracle_minibatch — one full submitMiniBatch + updateLambda +
 updateAlpha in Spark's structure (fp64, per-thread dense k×V stats, OpenMP on the host cores) —
@@ -80,6 +80,9 @@ def parse():
     p.add_argument("--featurisation-only", action="store_true",
                    help="only the HashingTF -> IDF line (for profiling its kernels)")
     p.add_argument("--no-hbm-copy", action="store_true", help="skip the device-copy HBM probe")
+    p.add_argument("--launch", default="auto", choices=["auto", "group"],
+                   help="group: drive the GPUs through one stc_group even at N = 1 (with STC_GROUP_RCCL=1 "
+                        "its RCCL communicator, ncclCommInitAll, and one host thread per member)")
     a = p.parse_args()
     for key, v in PRESETS[a.config].items():
         if getattr(a, key) is None:
@@ -130,7 +133,7 @@ def feat_sources_sha():
 
 def feat_traffic():
     """HBM bytes per call of each featurisation stage from the committed PMC summary
-    (tools/gpu_featpmc.sh → tools/feat_pmc_summary.py), if measured on this tree's sources."""
+    (tools/gpu.sh feat → tools/feat_pmc_summary.py), if measured on this tree's sources."""
     try:
         with open(FEAT_PMC) as f:
             pm = json.load(f)
@@ -143,7 +146,7 @@ def feat_traffic():
 
 def pmc_traffic(a, dtype, corpus):
     """HBM bytes per launch of the training E-step kernel from the committed PMC summary
-    (tools/pmc_summary.py over tools/gpu_prof.sh's separate FETCH_SIZE / WRITE_SIZE passes), if it
+    (tools/pmc_summary.py over tools/gpu.sh prof's separate FETCH_SIZE / WRITE_SIZE passes), if it
     was measured on this workload; FETCH_SIZE ×2 per the gfx950 correction (MI355X_MICROARCH.md)."""
     try:
         with open(PMC_SUMMARY) as f:
@@ -163,7 +166,10 @@ def pmc_traffic(a, dtype, corpus):
         if e.get("estep_sources_sha") != sha:
             return None, (f"PMC entry {e.get('tag', '?')} was measured on other E-step sources "
                           f"({e.get('estep_sources_sha')} vs HEAD {sha}): not a measurement of this code")
-        return b, f"{os.path.basename(PMC_SUMMARY)} ({e.get('note', '')})"
+        # the K6 window's bytes (E-step kernel + the sstats phase: sort, SpMM, stat clear) when the summary
+        # has them (round 5+), else the whole E-step phase per minibatch
+        return {"kernel": b, "window": e.get("k6_window_bytes_per_step") or e.get("estep_phase_bytes_per_step")}, \
+            f"{os.path.basename(PMC_SUMMARY)} ({e.get('note', '')})"
     return None, "no PMC summary committed for this workload"
 
 
@@ -391,14 +397,31 @@ def run_state(m, lam0, barrier, log, a, dtype, steps, warmup):
             "iters_local": l1["inner_iters"] - l0["inner_iters"]}
 
 
+# north-star parity of each dtype (tests/test_gpu_config1.py: configs[0] against the oracle)
+PARITY = {"f64": "north-star bars met: topicsMatrix 1e-9 (bar 1e-4), logPerplexity 1e-10 (bar 1e-5), identical "
+                 "top-10 terms on configs[0] (tests/test_gpu_config1.py)",
+          "f32": "north-star topicsMatrix bar NOT met: 4.8e-4 relative on configs[0] (bar 1e-4; one book's ~3300-"
+                 "iteration E-step stops at another iterate in fp32); logPerplexity 1e-5 and top-10 terms met "
+                 "(tests/test_gpu_config1.py) — a fast secondary mode, not a parity mode"}
+
+
 def summarize(r, a, dtype, world, steps, corpus_kind, kernel):
-    """value / roofline / roofline_compute of one run (rank-0 view of the reduced counters)."""
+    """value / roofline / roofline_compute of one run (rank-0 view of the reduced counters).
+
+    roofline window = SURVEY §8(d)'s K6: B_doc counts one gather of each entry's k-wide
+    expElogβ' row (the E-step kernel) AND one scatter of its k-wide sstats row, which the separate sstats
+    phase performs (radix sort of the (term, slot) keys + the term-sorted k_sstats SpMM), so the bytes are
+    divided by the E-step + sstats device time; `phase_split` gives each phase its own bytes and time."""
     estep_ms = r["phases"]["estep"]
+    sstats_ms = r["phases"].get("sstats", 0.0)
+    window_ms = estep_ms + sstats_ms
     per_step_docs = r["docs_local"] / max(1, steps)
     per_step_nnz = r["entries_local"] / max(1, steps)
     per_step_iters = r["iters_local"] / max(1, steps)
     alg = algorithmic_bytes(per_step_nnz, a.k, per_step_docs, dtype)
-    achieved = alg / (estep_ms * 1e-3) / 1e9
+    s_b = 8.0 if dtype == "f64" else 4.0
+    scatter = per_step_nnz * a.k * s_b  # the sstats rows written (K6's scatter half)
+    achieved = alg / (window_ms * 1e-3) / 1e9
     mean_nnz = per_step_nnz / max(1.0, per_step_docs)
     flops = 4.0 * mean_nnz * a.k * per_step_iters
     tflops = flops / (estep_ms * 1e-3) / 1e12
@@ -415,12 +438,21 @@ def summarize(r, a, dtype, world, steps, corpus_kind, kernel):
                             if r.get("estep_ms_slowest_member") is not None else {})),
         "estep_only_docs_per_s": per_step_docs * world / (estep_ms * 1e-3),
         "cold": r["cold"],
+        "parity": PARITY[dtype],
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic["window"] if traffic else None,
             "kernel": kernel, "algorithmic_bytes_per_launch": alg,
             "algorithmic_bytes_per_doc": f"nnz*(4+{s}) + 2*nnz*k*{s} + {s}*k",
-            "kernel_ms_per_launch": estep_ms, "traffic_source": traffic_note,
+            "window": "K6 = E-step kernel + sstats phase (radix sort + k_sstats): the gather and the scatter "
+                      "B_doc counts; kernel_ms_per_launch is their summed device time per minibatch",
+            "kernel_ms_per_launch": window_ms, "traffic_source": traffic_note,
+            "phase_split": {
+                "estep": {"ms": estep_ms, "algorithmic_bytes": alg - scatter,
+                          "traffic": traffic["kernel"] if traffic else None,
+                          "GBs": (alg - scatter) / (estep_ms * 1e-3) / 1e9 if estep_ms > 0 else None},
+                "sstats": {"ms": sstats_ms, "algorithmic_bytes": scatter,
+                           "GBs": scatter / (sstats_ms * 1e-3) / 1e9 if sstats_ms > 0 else None}},
         },
         "roofline_compute": {
             "bound": f"valu_{dtype}", "achieved": tflops, "peak": PEAK_TFS[dtype], "unit": "TFLOP/s",
@@ -442,21 +474,22 @@ def kernel_name(dtype, k):
     return "k_estep_grid (lda_grid.hip): the fp32 training E-step, one launch per minibatch"
 
 
-def launch_mode(gpus, env):
+def launch_mode(gpus, env, force_group=False):
     """How this process runs N GPUs: "ranks" — one process per GPU under torchrun (WORLD_SIZE set); "group"
-    — `python bench.py --gpus N` with no launcher: ONE process drives the N devices through stc_group (the
-    reference's own deployment, one JVM on Spark local[*], LDATraining.scala:7); "single" — N = 1."""
+    — `python bench.py --gpus N` with no launcher (or --launch group at any N): ONE process drives the N
+    devices through stc_group (the reference's own deployment, one JVM on Spark local[*],
+    LDATraining.scala:7); "single" — N = 1."""
     world = int(env.get("WORLD_SIZE", "1"))
     if world > 1:
         return "ranks", world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
-    if gpus > 1:
+    if gpus > 1 or force_group:
         return "group", gpus, 0, 0
     return "single", 1, 0, 0
 
 
 def main():
     a = parse()
-    mode, world, rank, local = launch_mode(a.gpus, os.environ)
+    mode, world, rank, local = launch_mode(a.gpus, os.environ, a.launch == "group")
     a.gpus = world
     log = (lambda msg: print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True))  # progress on stderr
     from stc import synth  # no GPU touched yet: the corpus pool may fork
@@ -490,7 +523,7 @@ def main():
         corpus = synth.make_corpus(a.corpus, a.docs, a.tokens, a.vocab, a.k, seed, lo, hi, workers)
     gen_s = time.perf_counter() - t0
     log(f"{mode}: corpus rows [{lo}, {hi}) generated in {gen_s:.1f} s")
-    secondary = world == 1 and not a.no_secondary
+    secondary = world == 1 and not a.no_secondary and mode != "group"  # (the secondary lines run on one context)
     planted = None
     if secondary:
         t0 = time.perf_counter()
@@ -629,6 +662,7 @@ def main():
             "cold": head["cold"], "phase_ms": head["phase_ms"],
             "estep_only_docs_per_s": head["estep_only_docs_per_s"], "cap_hits": head["cap_hits"],
         },
+        "parity": head["parity"],
         "roofline": roof,
         "roofline_compute": head["roofline_compute"],
         "cpu_baseline": cpu,

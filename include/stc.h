@@ -111,6 +111,9 @@ int stc_dcsr_shape(const stc_dcsr* m, int64_t* n_rows, int64_t* n_cols, int64_t*
 /* indptr[n_rows+1], indices[nnz], values[nnz] (any may be NULL to skip) */
 int stc_dcsr_download(stc_ctx* ctx, const stc_dcsr* m, int64_t* indptr, int32_t* indices,
                       double* values);
+/* Waits for the device to finish queued work, then hands the buffers back to the owning context for
+ * reuse.  Detach a training corpus from every stc_lda (stc_lda_set_corpus with another matrix, or
+ * stc_lda_destroy) before freeing it: the handle keeps a reference. */
 int stc_dcsr_free(stc_dcsr* m);
 
 /* ---- HashingTF (K1 murmur3 + nonNegativeMod, K2 per-doc count → sorted CSR) -----------
@@ -144,17 +147,19 @@ int stc_hash_tokens(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const in
  * Document d is the UTF-8 string text[text_off[d] .. text_off[d+1]).  Output: Spark's
  * Tokenizer result — lower-case, split on each Java \\s character ([ \t\n\x0B\f\r]), interior empty
  * tokens kept, trailing empty tokens dropped, a separator-free string is one token ("" → [""]) —
- * laid out as stc_hashing_tf's input: the separator-free lower-cased blob utf8_out (capacity
- * n_bytes + n_bytes / 2: lower-casing can grow a 2-byte character to 3 bytes), tok_off_out (capacity
- * n_bytes + n_docs + 1) and doc_off_out[n_docs+1].
+ * laid out as stc_hashing_tf's input: the separator-free lower-cased blob utf8_out (utf8_cap bytes;
+ * n_bytes + n_bytes / 2 always suffices: lower-casing can grow a 2-byte character to 3 bytes — when the
+ * text needs more than utf8_cap the call fails with STC_ERR_INVALID_ARG before writing any output and
+ * *n_out_bytes holds the size needed; utf8_out = NULL with utf8_cap = 0 is that size query), tok_off_out
+ * (capacity n_bytes + n_docs + 1) and doc_off_out[n_docs+1].
  * Lower-casing is Java 8's String.toLowerCase (root locale, Unicode 6.2) for every code point: the BMP
  * through a generated table, Deseret inline, characters Java 8 does not case passed through, and the 18
  * code points whose mapping is not a same-length 1:1 map by rule: U+0130 İ → "i̇" (2 → 3 bytes), U+03A3 Σ
  * → ς / σ by its Final_Sigma context, and the capitals whose lower case changes UTF-8 length (U+023A,
  * U+023E, U+1E9E, U+2126, U+212A, U+212B, U+2C62, U+2C64, U+2C6D–U+2C70, U+2C7E, U+2C7F, U+A78D, U+A7AA). */
 int stc_tokenize(stc_ctx* ctx, const uint8_t* text, int64_t n_bytes, const int64_t* text_off,
-                 int64_t n_docs, uint8_t* utf8_out, int64_t* n_out_bytes, int64_t* tok_off_out,
-                 int64_t* n_tok_out, int64_t* doc_off_out);
+                 int64_t n_docs, uint8_t* utf8_out, int64_t utf8_cap, int64_t* n_out_bytes,
+                 int64_t* tok_off_out, int64_t* n_tok_out, int64_t* doc_off_out);
 /* Tokenizer → HashingTF fused on device (no host round trip between the two stages) */
 int stc_tokenize_hashing_tf_dev(stc_ctx* ctx, const uint8_t* text, int64_t n_bytes,
                                 const int64_t* text_off, int64_t n_docs, int32_t num_features,
@@ -177,6 +182,8 @@ int stc_idf_fit_dev(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, stc_
 int stc_idf_get(stc_ctx* ctx, const stc_didf* model, double* idf_out /* n_cols */,
                 int64_t* df_out /* n_cols */, int64_t* m_out);
 int stc_idf_transform_dev(stc_ctx* ctx, stc_dcsr* tf, const stc_didf* model, double zero_floor);
+/* the model's vector size (numFeatures: stc_idf_get writes n_cols values to each output) and m */
+int stc_didf_shape(const stc_didf* model, int64_t* n_cols_out, int64_t* m_out);
 int stc_didf_free(stc_didf* model);
 
 /* ---- online LDA ----------------------------------------------------------------------- */
@@ -277,6 +284,16 @@ typedef struct stc_group stc_group;
 int stc_group_create(const int* device_ids, int n_devices, const stc_lda_config* cfg, stc_group** out);
 int stc_group_destroy(stc_group* g);
 int stc_group_size(const stc_group* g, int* n_out);
+/* How the members' collectives travel.  Debug knob: with STC_GROUP_RCCL=1 in the environment at
+ * stc_group_create, a group of distinct devices of any size (one included) builds its communicator with
+ * ncclCommInitAll, runs the sharded M-step's collectives over it and drives every member from its own
+ * host thread — the multi-GPU drop-in path on a one-GPU machine. */
+enum stc_transport {
+  STC_TRANSPORT_NONE = 0,       /* one member, no collectives */
+  STC_TRANSPORT_IN_PROCESS = 1, /* one device repeated: device pointers exchanged between member threads */
+  STC_TRANSPORT_RCCL = 2        /* an RCCL communicator over the members' devices (ncclCommInitAll) */
+};
+int stc_group_transport(const stc_group* g, int* transport_out);
 /* member i's handle (counters, timing); do not call its collective entry points directly */
 int stc_group_member(stc_group* g, int i, stc_lda** lda_out);
 /* the training corpus (rows = documents, values in the group's dtype on device) */

@@ -265,7 +265,7 @@ JNIEXPORT jlong JNICALL FN(hashingTfTokens)(JNIEnv* env, jclass c, jlong ctx, jl
 }
 
 /* ---- Tokenizer -------------------------------------------------------------------------- */
-/* outputs sized by the caller: utf8Out ≥ text.length, tokOffOut ≥ text.length + nDocs + 1,
+/* outputs sized by the caller: utf8Out ≥ text.length * 3 / 2, tokOffOut ≥ text.length + nDocs + 1,
  * docOffOut = nDocs + 1; returns {nOutBytes, nTok} */
 JNIEXPORT jlongArray JNICALL FN(tokenize)(JNIEnv* env, jclass c, jlong ctx, jbyteArray text, jlongArray text_off,
                                           jbyteArray utf8_out, jlongArray tok_off_out, jlongArray doc_off_out) {
@@ -280,7 +280,7 @@ JNIEXPORT jlongArray JNICALL FN(tokenize)(JNIEnv* env, jclass c, jlong ctx, jbyt
   jlong* to = PIN(jlong, Long, tok_off_out);
   jlong* dof = PIN(jlong, Long, doc_off_out);
   int st = stc_tokenize(CTX(ctx), (const uint8_t*)t, LEN(text), (const int64_t*)off, LEN(text_off) - 1,
-                        (uint8_t*)u, &nb, (int64_t*)to, &nt, (int64_t*)dof);
+                        (uint8_t*)u, LEN(utf8_out), &nb, (int64_t*)to, &nt, (int64_t*)dof);
   UNPIN(Long, doc_off_out, dof, 0);
   UNPIN(Long, tok_off_out, to, 0);
   UNPIN(Byte, utf8_out, u, 0);
@@ -343,8 +343,17 @@ JNIEXPORT jlong JNICALL FN(idfFitDev)(JNIEnv* env, jclass c, jlong ctx, jlong dc
 
 JNIEXPORT jlong JNICALL FN(idfGet)(JNIEnv* env, jclass c, jlong ctx, jlong model, jlong cols, jdoubleArray idf_out,
                                    jlongArray df_out) {
-  int64_t m = 0;
-  if ((idf_out && NEED(idf_out, cols, "idfGet idfOut")) || (df_out && NEED(df_out, cols, "idfGet dfOut"))) return 0;
+  int64_t m = 0, mcols = 0;
+  /* stc_idf_get writes the MODEL's column count into each output: size the checks from the model, and
+   * refuse a caller whose idea of numFeatures differs (a smaller `cols` overran the array) */
+  if (check(env, stc_didf_shape((const stc_didf*)(intptr_t)model, &mcols, NULL))) return 0;
+  if (cols != mcols) {
+    char msg[160];
+    snprintf(msg, sizeof msg, "idfGet: cols = %lld, the model has %lld columns", (long long)cols, (long long)mcols);
+    throw_iae(env, msg);
+    return 0;
+  }
+  if ((idf_out && NEED(idf_out, mcols, "idfGet idfOut")) || (df_out && NEED(df_out, mcols, "idfGet dfOut"))) return 0;
   jdouble* o = idf_out ? PIN(jdouble, Double, idf_out) : NULL;
   jlong* df = df_out ? PIN(jlong, Long, df_out) : NULL;
   int st = stc_idf_get(CTX(ctx), (const stc_didf*)(intptr_t)model, o, (int64_t*)df, &m);
@@ -357,6 +366,15 @@ JNIEXPORT jlong JNICALL FN(idfGet)(JNIEnv* env, jclass c, jlong ctx, jlong model
 JNIEXPORT void JNICALL FN(idfTransformDev)(JNIEnv* env, jclass c, jlong ctx, jlong dcsr, jlong model,
                                            jdouble zero_floor) {
   check(env, stc_idf_transform_dev(CTX(ctx), CSR(dcsr), (const stc_didf*)(intptr_t)model, zero_floor));
+}
+
+/* {numFeatures, m} of a device IDF model */
+JNIEXPORT jlongArray JNICALL FN(didfShape)(JNIEnv* env, jclass c, jlong model) {
+  int64_t s[2] = {0, 0};
+  if (check(env, stc_didf_shape((const stc_didf*)(intptr_t)model, &s[0], &s[1]))) return NULL;
+  jlongArray out = (*env)->NewLongArray(env, 2);
+  if (out) (*env)->SetLongArrayRegion(env, out, 0, 2, (const jlong*)s);
+  return out;
 }
 
 JNIEXPORT void JNICALL FN(didfFree)(JNIEnv* env, jclass c, jlong model) {
@@ -621,6 +639,13 @@ JNIEXPORT jint JNICALL FN(groupSize)(JNIEnv* env, jclass c, jlong g) {
   int n = 0;
   check(env, stc_group_size(GRP(g), &n));
   return n;
+}
+
+/* STC_TRANSPORT_NONE / _IN_PROCESS / _RCCL */
+JNIEXPORT jint JNICALL FN(groupTransport)(JNIEnv* env, jclass c, jlong g) {
+  int t = 0;
+  check(env, stc_group_transport(GRP(g), &t));
+  return t;
 }
 
 JNIEXPORT jlong JNICALL FN(groupMember)(JNIEnv* env, jclass c, jlong g, jint i) {

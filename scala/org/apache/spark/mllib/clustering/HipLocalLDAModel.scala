@@ -5,13 +5,15 @@ import org.apache.spark.rdd.RDD
 
 /**
  * The LocalLDAModel HipOnlineLDAOptimizer.getLDAModel returns: a stock [U] spark-mllib 2.4.3
- * LocalLDAModel (topicsMatrix, save/load, serialisation and ml.clustering.LocalLDAModel.transform are
- * Spark's own) whose inference calls run on the GPU group that trained it, where λ is still resident:
+ * LocalLDAModel (topicsMatrix, save/load and serialisation are Spark's own) whose inference calls run on
+ * the GPU group that trained it, where λ is still resident:
  *
  *   describeTopics      → stc_group_describe   (the reference's LDAClustering.scala describeTopics call)
  *   logLikelihood       → stc_group_bound      (LocalLDAModel.logLikelihoodBound: corpus part + topics part)
  *   logPerplexity       → stc_group_bound      (−bound / token count, one device pass instead of two RDD jobs)
  *   topicDistribution(s)→ stc_group_topic_distribution (zeros for empty documents, as Spark)
+ *   getTopicDistributionMethod (the row function of ml LocalLDAModel.transform)
+ *                       → stc_group_topic_distribution, via the JVM-local registry (token)
  *
  * The documents of an RDD call are collected to the driver (the reference runs local[*], one JVM:
  * LDATraining.scala:7) and sharded over the group's devices.  γ₀ of document i (its position in the
@@ -34,6 +36,15 @@ final class HipLocalLDAModel private[clustering] (
 
   @transient private lazy val lock = new Object
 
+  /**
+   * This model's key in the JVM-wide registry (serialised with the model and with the closures below): a
+   * task deserialised in the JVM that holds the group (Spark local[*], the reference's deployment,
+   * LDATraining.scala:7) finds the live model under it and runs on its GPUs; any other JVM finds nothing
+   * and runs Spark's CPU E-step.  The raw group pointer itself never leaves the driver.
+   */
+  private[clustering] val token: String = java.util.UUID.randomUUID().toString
+  HipLocalLDAModel.register(this)
+
   /** true while the model's λ is resident on the GPU group */
   def onDevice: Boolean = lock.synchronized(group != 0L)
 
@@ -41,7 +52,40 @@ final class HipLocalLDAModel private[clustering] (
   def close(): Unit = lock.synchronized {
     if (group != 0L) StcNative.groupDestroy(group)
     group = 0L
+    HipLocalLDAModel.unregister(token)
   }
+
+  /**
+   * θ = γ/Σγ of every document on this model's GPU group (one stc_group_topic_distribution call for the
+   * batch, documents sharded over the devices), or None when the group was released.  docIdBase keys γ₀.
+   */
+  private[clustering] def deviceTopicDistributions(docs: Array[Vector], docIdBase: Long): Option[Array[Vector]] =
+    lock.synchronized {
+      if (group == 0L) None
+      else {
+        docs.foreach(v => require(v.size == vocabSize, s"document of size ${v.size}, the model has $vocabSize terms"))
+        val csr = StcNative.toCsr(docs)
+        val out = new Array[Double](docs.length * k)
+        StcNative.groupTopicDistribution(group, docs.length, vocabSize, csr(0).asInstanceOf[Array[Long]],
+          csr(1).asInstanceOf[Array[Int]], csr(2).asInstanceOf[Array[Double]], getSeed, docIdBase, null, out)
+        Some(Array.tabulate(docs.length)(i => Vectors.dense(out.slice(i * k, (i + 1) * k))))
+      }
+    }
+
+  /**
+   * [U] LocalLDAModel.getTopicDistributionMethod: the per-row function ml.clustering.LocalLDAModel.transform
+   * wraps in its UDF (so the stock ml transform of a model wrapping this one reaches the GPU as well, one
+   * document per call — HipLDAModel.transform batches a whole partition per call instead).  The closure
+   * carries the registry token and Spark's own CPU function as the fallback for another JVM.
+   */
+  override private[spark] def getTopicDistributionMethod: Vector => Vector = {
+    val key = token
+    val cpu = cpuTopicDistributionMethod
+    (v: Vector) => HipLocalLDAModel.topicDistributionsLocal(key, Array(v), 0L).map(_(0)).getOrElse(cpu(v))
+  }
+
+  /** Spark's own CPU row function (the fallback the closures above carry to other JVMs) */
+  private[spark] def cpuTopicDistributionMethod: Vector => Vector = super.getTopicDistributionMethod
 
   override protected def finalize(): Unit = {
     try close() finally super.finalize()
@@ -106,6 +150,22 @@ final class HipLocalLDAModel private[clustering] (
 }
 
 object HipLocalLDAModel {
+  // the JVM's models that hold a GPU group, by token (weak: a model nobody references can still be collected)
+  private val live = new java.util.concurrent.ConcurrentHashMap[String, java.lang.ref.WeakReference[HipLocalLDAModel]]()
+
+  private def register(m: HipLocalLDAModel): Unit = live.put(m.token, new java.lang.ref.WeakReference(m))
+  private def unregister(token: String): Unit = live.remove(token)
+
+  /**
+   * θ of `docs` on the GPU group of the model registered under `token` in THIS JVM, or None (no such model
+   * here, or its group was released): the caller then uses Spark's CPU E-step.
+   */
+  private[spark] def topicDistributionsLocal(token: String, docs: Array[Vector], docIdBase: Long): Option[Array[Vector]] = {
+    val ref = live.get(token)
+    val m = if (ref == null) null else ref.get()
+    if (m == null) None else m.deviceTopicDistributions(docs, docIdBase)
+  }
+
   /**
    * A GPU copy of an already trained model, e.g. the reference's LDALoader.scala:108
    * `LDATrainedModel.toLocal.topicDistribution(v)` becomes

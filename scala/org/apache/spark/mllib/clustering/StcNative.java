@@ -68,6 +68,8 @@ public final class StcNative {
   public static native long idfFitDev(long ctx, long dcsr, long minDocFreq);
   public static native long idfGet(long ctx, long model, long cols, double[] idfOut, long[] dfOut);
   public static native void idfTransformDev(long ctx, long dcsr, long model, double zeroFloor);
+  // {numFeatures, m} of a device IDF model (idfGet's cols must equal numFeatures)
+  public static native long[] didfShape(long model);
   public static native void didfFree(long model);
 
   // ---- online LDA (alpha null ⇒ −1 ⇒ 1/k; eta −1 ⇒ 1/k)
@@ -129,6 +131,8 @@ public final class StcNative {
                                         int maxInnerIter);
   public static native void groupDestroy(long group);
   public static native int groupSize(long group);
+  // how the group's collectives travel: 0 none (one member), 1 in-process (one device repeated), 2 RCCL
+  public static native int groupTransport(long group);
   public static native long groupMember(long group, int i);
   public static native void groupSetCorpus(long group, long rows, long cols, long[] indptr, int[] indices,
                                            double[] values);

@@ -1236,6 +1236,10 @@ int stc_dcsr_free(stc_dcsr* m) {
     {  // hand the allocations back to the context that made it, if it still exists (Recycler)
       std::lock_guard<std::mutex> lk(g_live_mu);
       if (m->ctx && g_live.count(static_cast<stc_ctx*>(m->ctx)) && m->ctx->device == m->device) {
+        // every queued reader first — the context's stream and any other (an LDA handle's side stream
+        // sampling from this corpus): a recycled buffer is rewritten by the next taker, so the implicit
+        // device synchronisation hipFree used to give is kept
+        (void)hipDeviceSynchronize();
         m->ctx->recycle.put(m->indices);
         m->ctx->recycle.put(m->values);
         m->ctx->recycle.put(m->indptr);
@@ -1411,14 +1415,21 @@ void run_tokenizer(Ctx& c, Tokens& t, const uint8_t* text, int64_t n_bytes, cons
 }  // namespace
 
 int stc_tokenize(stc_ctx* ctx, const uint8_t* text, int64_t n_bytes, const int64_t* text_off,
-                 int64_t n_docs, uint8_t* utf8_out, int64_t* n_out_bytes, int64_t* tok_off_out,
-                 int64_t* n_tok_out, int64_t* doc_off_out) {
+                 int64_t n_docs, uint8_t* utf8_out, int64_t utf8_cap, int64_t* n_out_bytes,
+                 int64_t* tok_off_out, int64_t* n_tok_out, int64_t* doc_off_out) {
   return guard([&] {
-    STC_REQUIRE(ctx && n_out_bytes && n_tok_out && tok_off_out && doc_off_out && (utf8_out || n_bytes == 0),
+    STC_REQUIRE(ctx && n_out_bytes && n_tok_out && tok_off_out && doc_off_out && (utf8_out || utf8_cap == 0),
                 "ctx/outputs");
+    STC_REQUIRE(utf8_cap >= 0, "utf8_cap must be >= 0");
     ctx->use();
     Tokens t;
     run_tokenizer(*ctx, t, text, n_bytes, text_off, n_docs);
+    // the lower-cased blob can outgrow the input (İ → i̇, Ⱥ → ⱥ: 2 → 3 bytes); its size is known from the
+    // count pass, so a short buffer is refused before anything is copied (*n_out_bytes = the size needed)
+    *n_out_bytes = t.n_bytes;
+    if (t.n_bytes > utf8_cap)
+      throw Error(STC_ERR_INVALID_ARG, "utf8_out holds " + std::to_string(utf8_cap) + " bytes, the lower-cased text needs " +
+                                           std::to_string(t.n_bytes));
     hipStream_t s = ctx->stream;
     if (t.n_bytes) HIP_CHECK(hipMemcpyAsync(utf8_out, t.utf8.p, t.n_bytes, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(tok_off_out, t.tok_off.p, 8 * (t.n_tok + 1), hipMemcpyDeviceToHost, s));
@@ -1539,6 +1550,14 @@ int stc_idf_get(stc_ctx* ctx, const stc_didf* md, double* idf_out, int64_t* df_o
   });
 }
 
+int stc_didf_shape(const stc_didf* md, int64_t* cols_out, int64_t* m_out) {
+  return guard([&] {
+    STC_REQUIRE(md, "model");
+    if (cols_out) *cols_out = md->cols;
+    if (m_out) *m_out = md->m;
+  });
+}
+
 int stc_idf_transform_dev(stc_ctx* ctx, stc_dcsr* tf, const stc_didf* md, double zero_floor) {
   return guard([&] {
     STC_REQUIRE(ctx && tf && md, "ctx/tf/model");
@@ -1558,6 +1577,7 @@ int stc_didf_free(stc_didf* md) {
     {  // back to the context that made it, if it still exists (Recycler)
       std::lock_guard<std::mutex> lk(g_live_mu);
       if (md->ctx && g_live.count(static_cast<stc_ctx*>(md->ctx)) && md->ctx->device == md->device) {
+        (void)hipDeviceSynchronize();  // queued readers of the model first (as stc_dcsr_free)
         md->ctx->recycle.put(md->idf);
         md->ctx->recycle.put(md->df);
       }
@@ -1979,6 +1999,8 @@ struct stc_group {
   std::unique_ptr<LocalColl> local;
   int64_t rows = 0, cols = 0;
   int dtype = STC_F64;
+  int transport = STC_TRANSPORT_NONE;  // how the members' collectives travel (stc_group_transport)
+  bool threaded = false;               // run even a one-member call on its own host thread (STC_GROUP_RCCL)
   int n() const { return (int)ctx.size(); }
 };
 
@@ -2007,7 +2029,7 @@ void for_members(stc_group& g, F f) {
       if (g.local) g.local->fail();  // release the members waiting in a barrier
     }
   };
-  if (n == 1) {
+  if (n == 1 && !g.threaded) {
     run(0);
   } else {
     std::vector<std::thread> th;
@@ -2083,12 +2105,23 @@ int stc_group_create(const int* device_ids, int n_devices, const stc_lda_config*
       member_ok(stc_init(device_ids[i], &c));
       g->ctx.push_back(c);
     }
+    // debug knob STC_GROUP_RCCL=1: a group of distinct devices — one device included — builds its RCCL
+    // communicator with ncclCommInitAll, runs the collective (vocabulary-sliced) M-step even with one member,
+    // and drives every member from its own host thread: the configs[2] drop-in path (one JVM, N GPUs,
+    // LDATraining.scala:7) exercised end to end on a one-GPU box, where no two-device communicator exists
+    const char* gr = getenv("STC_GROUP_RCCL");
+    const bool rccl1 = gr && gr[0] == '1' && distinct;
     if (n_devices > 1 && same) {
       g->local = std::make_unique<LocalColl>(n_devices);
+      g->transport = STC_TRANSPORT_IN_PROCESS;
     }
-    if (n_devices > 1 || !same) {
+    if (n_devices > 1 || rccl1) {
       std::vector<ncclComm_t> comms((size_t)n_devices, nullptr);
-      if (!g->local) RCCL_CHECK(ncclCommInitAll(comms.data(), n_devices, device_ids));
+      if (!g->local) {
+        RCCL_CHECK(ncclCommInitAll(comms.data(), n_devices, device_ids));
+        g->transport = STC_TRANSPORT_RCCL;
+      }
+      g->threaded = rccl1;
       for (int i = 0; i < n_devices; ++i) {
         g->ctx[(size_t)i]->comm = comms[(size_t)i];
         g->ctx[(size_t)i]->local = g->local.get();
@@ -2099,6 +2132,7 @@ int stc_group_create(const int* device_ids, int n_devices, const stc_lda_config*
     for (int i = 0; i < n_devices; ++i) {
       stc_lda* l = nullptr;
       member_ok(stc_lda_create(g->ctx[(size_t)i], cfg, &l));
+      if (rccl1) l->force_coll = true;  // the sliced M-step and its collectives on a 1-rank communicator too
       g->lda.push_back(l);
     }
     g->dtype = g->lda[0]->dtype;
@@ -2125,6 +2159,13 @@ int stc_group_size(const stc_group* g, int* n_out) {
   return guard([&] {
     STC_REQUIRE(g && n_out, "group/n_out");
     *n_out = g->n();
+  });
+}
+
+int stc_group_transport(const stc_group* g, int* transport_out) {
+  return guard([&] {
+    STC_REQUIRE(g && transport_out, "group/transport_out");
+    *transport_out = g->transport;
   });
 }
 

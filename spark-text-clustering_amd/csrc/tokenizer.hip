@@ -78,8 +78,11 @@ __device__ __forceinline__ uint32_t cp_at(const uint8_t* __restrict__ text, int6
 }
 // Final_Sigma for the Σ at text[i] (2 bytes) of the document [s, e): preceded by a cased letter with only
 // case-ignorables between, and not followed by case-ignorables then a cased letter (the Unicode rule, as the
-// oracle's str.lower() applies it; Java 8's BreakIterator form agrees on letters, marks, digits, spaces
-// and punctuation around Σ).  A malformed byte ends a scan as a non-cased character.
+// oracle's str.lower() applies it).  A malformed byte ends a scan as a non-cased character.
+// KNOWN DIVERGENCE from Spark's JVM (parity unpinned: no artefact or test of the reference holds it): Java
+// 8's ConditionalSpecialCasing.isFinalCased scans the whole BreakIterator word instead, where letters AND
+// digits belong to one word, so a digit between Σ and a cased letter changes the answer — "Α1Σ" gives Java
+// ς but this rule σ, "ΑΣ1Β" Java σ but this rule ς.  Letters, marks, spaces and punctuation around Σ agree.
 __device__ bool final_sigma(const uint8_t* __restrict__ text, int64_t s, int64_t e, int64_t i) {
   bool pre = false;
   for (int64_t j = i; j > s;) {  // backwards, one character at a time

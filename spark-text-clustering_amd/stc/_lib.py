@@ -20,6 +20,7 @@ STC_OK, STC_ERR_INVALID_ARG, STC_ERR_HIP, STC_ERR_RCCL, STC_ERR_OOM, STC_ERR_STA
 STC_HASH_STANDARD, STC_HASH_SPARK24 = 0, 1
 STC_F32, STC_F64 = 0, 1
 STC_LAYOUT_VK, STC_LAYOUT_KV = 0, 1
+STC_TRANSPORT_NONE, STC_TRANSPORT_IN_PROCESS, STC_TRANSPORT_RCCL = 0, 1, 2
 
 _i32, _i64, _u64, _dbl, _int = C.c_int32, C.c_int64, C.c_uint64, C.c_double, C.c_int
 _p = C.c_void_p
@@ -86,7 +87,7 @@ SIGNATURES = {
     "stc_tokens_upload": (_int, [_p, _pu8, _i64, _pi64, _i64, _pi64, _i64, C.POINTER(_p)]),
     "stc_tokens_free": (_int, [_p]),
     "stc_hashing_tf_tokens": (_int, [_p, _p, _i32, _int, _int, _int, C.POINTER(_p)]),
-    "stc_tokenize": (_int, [_p, _pu8, _i64, _pi64, _i64, _pu8, _pi64, _pi64, _pi64, _pi64]),
+    "stc_tokenize": (_int, [_p, _pu8, _i64, _pi64, _i64, _pu8, _i64, _pi64, _pi64, _pi64, _pi64]),
     "stc_tokenize_hashing_tf_dev": (_int, [_p, _pu8, _i64, _pi64, _i64, _i32, _int, _int, _int,
                                            C.POINTER(_p)]),
     "stc_idf_fit": (_int, [_p, _p, _i64, _pdbl, _pi64, _pi64]),
@@ -94,6 +95,7 @@ SIGNATURES = {
     "stc_idf_fit_dev": (_int, [_p, _p, _i64, C.POINTER(_p)]),
     "stc_idf_get": (_int, [_p, _p, _pdbl, _pi64, _pi64]),
     "stc_idf_transform_dev": (_int, [_p, _p, _p, C.c_double]),
+    "stc_didf_shape": (_int, [_p, _pi64, _pi64]),
     "stc_didf_free": (_int, [_p]),
     "stc_lda_config_default": (None, [C.POINTER(LdaConfig)]),
     "stc_lda_create": (_int, [_p, C.POINTER(LdaConfig), C.POINTER(_p)]),
@@ -119,6 +121,7 @@ SIGNATURES = {
     "stc_group_create": (_int, [_pi32, _int, C.POINTER(LdaConfig), C.POINTER(_p)]),
     "stc_group_destroy": (_int, [_p]),
     "stc_group_size": (_int, [_p, _pi32]),
+    "stc_group_transport": (_int, [_p, _pi32]),
     "stc_group_member": (_int, [_p, _int, C.POINTER(_p)]),
     "stc_group_set_corpus": (_int, [_p, _i64, _i64, _pi64, _pi32, _pdbl]),
     "stc_group_init_random": (_int, [_p, _u64]),

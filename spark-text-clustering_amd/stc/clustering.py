@@ -283,6 +283,14 @@ class LdaGroup:
         """per member: cumulative docs / entries / inner iterations / cap hits"""
         return [_counters(self.lib, h) for h in self.members()]
 
+    def transport(self):
+        """how the members' collectives travel: "none" (one member), "in-process" (one device repeated) or
+        "rccl" (ncclCommInitAll over distinct devices — one included under STC_GROUP_RCCL=1)"""
+        t = C.c_int32()
+        L.check(self.lib.stc_group_transport(self.handle, C.byref(t)))
+        return {L.STC_TRANSPORT_NONE: "none", L.STC_TRANSPORT_IN_PROCESS: "in-process",
+                L.STC_TRANSPORT_RCCL: "rccl"}[t.value]
+
     def step(self, batch_ids, gamma0=None, stats=True):
         ids = L.as_i64(batch_ids)
         g0 = None if gamma0 is None else L.as_f64(gamma0)

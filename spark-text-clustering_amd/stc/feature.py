@@ -95,7 +95,7 @@ class Tokenizer:
         doc_off = np.zeros(n_docs + 1, np.int64)
         nb, nt = C.c_int64(), C.c_int64()
         L.check(self.ctx.lib.stc_tokenize(self.ctx.handle, L.ptr(text, C.c_uint8), text.size,
-                                          L.ptr(off, C.c_int64), n_docs, L.ptr(blob, C.c_uint8),
+                                          L.ptr(off, C.c_int64), n_docs, L.ptr(blob, C.c_uint8), blob.size,
                                           C.byref(nb), L.ptr(tok_off, C.c_int64), C.byref(nt),
                                           L.ptr(doc_off, C.c_int64)))
         return blob[:nb.value].copy(), tok_off[:nt.value + 1].copy(), doc_off
@@ -208,6 +208,13 @@ class IDFModel:
         self._m = None if numDocs is None else int(numDocs)
         self._ctx = ctx
         self._dev, self._cols = _dev, int(_cols)
+        # freeing the device model needs only the library, never a context (a __del__ at
+        # interpreter shutdown must not create or initialise one)
+        self._lib = L.load() if _dev is not None else None
+        if _dev is not None:
+            cols = C.c_int64()
+            L.check(self._lib.stc_didf_shape(_dev, C.byref(cols), None))
+            self._cols = cols.value
 
     @property
     def ctx(self):
@@ -265,13 +272,13 @@ class IDFModel:
         if self._dev is not None:
             if self._idf is None:
                 self._fetch()
-            self.ctx.lib.stc_didf_free(self._dev)
+            self._lib.stc_didf_free(self._dev)
             self._dev = None
 
     def __del__(self):
         try:
             if self._dev is not None:
-                self.ctx.lib.stc_didf_free(self._dev)
+                self._lib.stc_didf_free(self._dev)
                 self._dev = None
         except Exception:
             pass

@@ -69,9 +69,64 @@ static void report(const char* name) {
 }
 static jarray arr(jsize n, size_t esz) { return new_array(n, esz); }
 
-int main(void) {
+/* GPU mode (tests/test_gpu_jni_shim.py): a real context, IDF model and group behind the same wrappers */
+static int gpu_main(JNIEnv* env) {
+  jlong ctx = FN(init)(env, NULL, 0);
+  report("init");
+  if (!ctx) return 1;
+  /* 3 documents over 10 terms: {0:2, 3:1}, {3:4}, {1:1, 3:2, 9:5} */
+  jlongArray ip = arr(4, 8);
+  jintArray ix = arr(6, 4);
+  jdoubleArray vs = arr(6, 8);
+  jlong p4[4] = {0, 2, 3, 6};
+  jint i6[6] = {0, 3, 3, 1, 3, 9};
+  jdouble v6[6] = {2, 1, 4, 1, 2, 5};
+  memcpy(ip->data, p4, sizeof p4);
+  memcpy(ix->data, i6, sizeof i6);
+  memcpy(vs->data, v6, sizeof v6);
+  jlong m = FN(dcsrUpload)(env, NULL, ctx, 3, 10, ip, ix, vs, 1);
+  report("dcsrUpload");
+  jlong model = FN(idfFitDev)(env, NULL, ctx, m, 0);
+  report("idfFitDev");
+  FN(idfGet)(env, NULL, ctx, model, 9, arr(10, 8), NULL);
+  report("idfGet_wrong_cols");     /* the model has 10 columns */
+  FN(idfGet)(env, NULL, ctx, model, 10, arr(9, 8), NULL);
+  report("idfGet_short_idf");
+  {
+    jlongArray df = arr(10, 8);
+    jlong mm = FN(idfGet)(env, NULL, ctx, model, 10, arr(10, 8), df);
+    report("idfGet_sized");
+    const jlong* d = df->data;
+    printf("idfGet_result\t%lld\t%lld %lld %lld %lld\n", (long long)mm, (long long)d[0], (long long)d[1],
+           (long long)d[3], (long long)d[9]);
+  }
+  FN(didfFree)(env, NULL, model);
+  FN(dcsrFree)(env, NULL, m);
+  /* HipLDAModel.transform's call: a one-device group, λ set, θ of the 3 documents */
+  jintArray dev = arr(1, 4);
+  jlong g = FN(groupCreate)(env, NULL, dev, 3, 10, NULL, -1.0, 1024.0, 0.51, 0.05, 100.0, 0, 1, 1, 1, 0);
+  report("groupCreate");
+  if (!g) return 1;
+  jdoubleArray topics = arr(30, 8);
+  for (int j = 0; j < 30; ++j) ((jdouble*)topics->data)[j] = 0.5 + 0.37 * (double)((j * 7) % 11);
+  FN(groupSetTopics)(env, NULL, g, topics, 0);
+  report("groupSetTopics");
+  jdoubleArray theta = arr(9, 8);
+  FN(groupTopicDistribution)(env, NULL, g, 3, 10, ip, ix, vs, 7, 100, NULL, theta);
+  report("groupTopicDistribution");
+  printf("theta");
+  for (int j = 0; j < 9; ++j) printf("\t%.17g", ((jdouble*)theta->data)[j]);
+  printf("\n");
+  printf("transport\t%d\n", (int)FN(groupTransport)(env, NULL, g));
+  FN(groupDestroy)(env, NULL, g);
+  FN(destroy)(env, NULL, ctx);
+  return 0;
+}
+
+int main(int argc, char** argv) {
   JNIEnv env_ = &table;
   JNIEnv* env = &env_;
+  if (argc > 1 && strcmp(argv[1], "gpu") == 0) return gpu_main(env);
   /* 3 tokens "ab","c","" in 2 documents */
   jbyteArray utf8 = arr(3, 1);
   memcpy(utf8->data, "abc", 3);
@@ -114,5 +169,12 @@ int main(void) {
   report("ldaCounters_short");
   FN(ldaPhaseTimes)(env, NULL, 0, arr(4, 8));
   report("ldaPhaseTimes_short");
+  FN(idfGet)(env, NULL, 0, 0, 10, arr(10, 8), NULL);
+  report("idfGet_null_model");  /* the model's column count is looked up before anything is pinned */
+  {
+    jlongArray ip = arr(2, 8);
+    FN(groupTopicDistribution)(env, NULL, 0, 1, 10, ip, arr(0, 4), arr(0, 8), 7, 0, NULL, arr(3, 8));
+    report("groupTopicDistribution_null_group");  /* HipLDAModel.transform's call reaches the library */
+  }
   return 0;
 }

@@ -24,6 +24,8 @@ def test_launch_mode():
     assert bench.launch_mode(8, {}) == ("group", 8, 0, 0)
     assert bench.launch_mode(2, {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1"}) == ("ranks", 2, 1, 1)
     assert bench.launch_mode(1, {"WORLD_SIZE": "4", "RANK": "0", "LOCAL_RANK": "0"})[0] == "ranks"
+    # --launch group: one stc_group even at N = 1 (its RCCL communicator under STC_GROUP_RCCL=1)
+    assert bench.launch_mode(1, {}, True) == ("group", 1, 0, 0)
 
 
 class FakeGroup:
@@ -89,10 +91,25 @@ def test_gpus_n_without_launcher_drives_a_group(monkeypatch, capsys):
     assert line["config"]["parallelism"] == "group2"
     assert line["config"]["baseline_config"] == "configs[2]"
     assert line["cpu_baseline"] is None and line["secondary"] == []
-    # value = docs of all members / wall time; the roofline uses member 0's launch
+    # value = docs of all members / wall time; the roofline uses member 0's K6 window (E-step + sstats)
     assert line["value"] > 0
     assert line["config"]["phase_ms"]["estep_slowest_member"] == 2.0
-    assert line["roofline"]["kernel_ms_per_launch"] == 1.0
+    assert line["roofline"]["kernel_ms_per_launch"] == pytest.approx(1.2)
+    split = line["roofline"]["phase_split"]
+    assert split["estep"]["ms"] == 1.0 and split["sstats"]["ms"] == 0.2
+    # the split's bytes add up to the window's
+    assert split["estep"]["algorithmic_bytes"] + split["sstats"]["algorithmic_bytes"] == pytest.approx(
+        line["roofline"]["algorithmic_bytes_per_launch"])
+    assert line["parity"].startswith("north-star bars met")  # the fp64 headline
+
+
+def test_group_launch_at_one_gpu(monkeypatch, capsys):
+    """--launch group at N = 1: the group path (group1) on device 0, reported as such."""
+    line = _run_bench(monkeypatch, capsys, ["--launch", "group", "--steps", "2", "--warmup", "0", "--docs", "800",
+                                            "--tokens", "10", "--vocab", "1024", "--k", "4", "--workers", "1",
+                                            "--no-hbm-copy", "--no-cpu-baseline"], n_dev=1)
+    (g,) = FakeGroup.made
+    assert g.devices == [0] and line["n_gpus"] == 1 and line["config"]["parallelism"] == "group1"
 
 
 def test_gpus_n_fails_loudly_when_fewer_devices_are_visible(monkeypatch, capsys):
@@ -127,8 +144,13 @@ def test_traffic_is_null_with_a_reason_unless_measured_on_these_sources(tmp_path
     assert b is None and "other E-step sources" in why
     p.write_text(json.dumps({"entries": [{"workload": wl, "estep_kernel": ["k"], "estep_kernel_bytes_per_launch": 4.6e9,
                                           "estep_sources_sha": bench.estep_sources_sha()}]}))
-    assert bench.pmc_traffic(A, "f64", "zipf")[0] == 4.6e9
-    assert np.isfinite(bench.pmc_traffic(A, "f64", "zipf")[0])
+    t = bench.pmc_traffic(A, "f64", "zipf")[0]
+    assert t["kernel"] == 4.6e9 and t["window"] is None  # no window / phase bytes in this entry
+    p.write_text(json.dumps({"entries": [{"workload": wl, "estep_kernel": ["k"], "estep_kernel_bytes_per_launch": 4.6e9,
+                                          "k6_window_bytes_per_step": 6.1e9,
+                                          "estep_sources_sha": bench.estep_sources_sha()}]}))
+    t = bench.pmc_traffic(A, "f64", "zipf")[0]
+    assert t == {"kernel": 4.6e9, "window": 6.1e9} and np.isfinite(t["window"])
 
 
 def test_featurisation_traffic_is_bound_to_its_sources(tmp_path, monkeypatch):

@@ -195,3 +195,120 @@ def test_failed_set_corpus_leaves_every_member_on_its_shard(ctx, monkeypatch):
     t1, a1 = run(True)
     np.testing.assert_array_equal(t1, t0)
     np.testing.assert_array_equal(a1, a0)
+
+
+# ---- the group's RCCL path (ncclCommInitAll + one host thread per member) on a one-GPU box.
+# STC_GROUP_RCCL=1: a group of distinct devices — here the one device — builds a real communicator with
+# ncclCommInitAll, runs the sliced (multi-rank) M-step's reduce-scatter / all-reduce / all-gathers over it
+# and drives its member from a spawned host thread, exactly as configs[2]'s one-JVM, N-GPU drop-in does.
+
+def test_rccl_group_matches_a_single_handle(ctx, monkeypatch):
+    """Injected membership and γ₀ through a one-member RCCL group: λ, α, iteration count, describeTopics,
+    the bound and topicDistribution bit-identical to a plain single handle (a one-rank reduce-scatter /
+    all-gather is a copy and the slice is the whole vocabulary)."""
+    import stc
+
+    monkeypatch.setenv("STC_GROUP_RCCL", "1")
+    rng = np.random.default_rng(211)
+    D, V, k = 240, 3000, 40
+    corpus = random_corpus(rng, D, V, 1, 160, empty_every=17)
+    lam = rng.gamma(100.0, 0.01, size=(V, k))
+    kw = dict(mini_batch_fraction=0.3, optimize_doc_concentration=True)
+    h, d = _single(ctx, corpus, k, lam, **kw)
+    with stc.LdaGroup([0], k, V, dtype="f64", **kw) as g:
+        assert g.transport() == "rccl"
+        g.set_corpus(corpus)
+        g.set_topics(lam)
+        for _ in range(3):
+            ids = rng.integers(0, D, size=90)
+            g0 = rng.gamma(100.0, 0.01, size=(ids.size, k))
+            sh, sg = h.step(ids, g0), g.step(ids, g0)
+            assert sg["inner_iters"] == sh["inner_iters"] and sg["nonempty_docs"] == sh["nonempty_docs"]
+        np.testing.assert_array_equal(g.topics(), h.topics())
+        np.testing.assert_array_equal(g.alpha(), h.alpha())
+        assert g.iteration() == h.iteration() == 3
+        ig, wg = g.describe(10)
+        ih, wh = h.describe(10)
+        assert np.array_equal(ig, ih) and np.array_equal(wg, wh)
+        held = random_corpus(rng, 70, V, 0, 120, empty_every=11)
+        dh = stc.DeviceCsr.upload(ctx, held, stc.STC_F64)
+        assert g.bound(held, gamma_seed=7, doc_id_base=1000)["bound"] == h.bound(dh, gamma_seed=7, doc_id_base=1000)["bound"]
+        np.testing.assert_array_equal(g.topic_distribution(held, gamma_seed=7, doc_id_base=1000),
+                                      h.topic_distribution(dh, gamma_seed=7, doc_id_base=1000))
+        dh.free()
+        # device-sampled next() through the same communicator, then the sharded λ gathered back
+        g.next()
+        g.next(stats=False)
+        g.synchronize()
+        assert g.iteration() == 5 and np.all(np.isfinite(g.topics()))
+
+
+def test_rccl_group_next_matches_the_oracle_replay(ctx, oracle, monkeypatch, dtype="f64"):
+    """The device-sampled next() path over the real communicator against the single-process oracle replaying
+    the same membership (as test_group_next_matches_the_oracle_replay for the in-process transport)."""
+    import stc
+    from test_gpu_comm import _members
+
+    monkeypatch.setenv("STC_GROUP_RCCL", "1")
+    rng = np.random.default_rng(170)
+    D, V, k, seed, frac, steps = 90, 700, 6, 77, 0.05, 8
+    corpus = random_corpus(rng, D, V, 1, 30, empty_every=11)
+    lam0 = rng.gamma(100.0, 0.01, size=(V, k))
+    with stc.LdaGroup([0], k, V, dtype=dtype, mini_batch_fraction=frac, seed=seed,
+                      optimize_doc_concentration=True) as g:
+        assert g.transport() == "rccl"
+        g.set_corpus(corpus)
+        g.set_topics(lam0)
+        for _ in range(steps):
+            g.next()
+        lam, alpha, iters = g.topics(), g.alpha(), g.iteration()
+    alpha0, eta = oracle.resolve_alpha_eta(k)
+    st = oracle.OnlineLDAState(lam=lam0.T.copy(), alpha=alpha0, eta=eta, corpus_size=D, mini_batch_fraction=frac,
+                               optimize_doc_concentration=True)
+    for draw in range(1, steps + 1):
+        it = st.iteration + 1
+        mem = _members(corpus.indptr, frac, seed, draw, 0, oracle)
+        if not mem:
+            continue
+        oracle.submit_minibatch(st, [corpus.row(dd) for dd in mem],
+                                [oracle.gamma_init(seed, oracle.train_doc_key(it, 0, pos), k) for pos in range(len(mem))])
+    assert iters == st.iteration and st.iteration > 0
+    rel = np.max(np.abs(lam - st.lam.T) / st.lam.T)
+    assert rel < 1e-9, rel
+    np.testing.assert_allclose(alpha, st.alpha, rtol=1e-9)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_rccl_group_next_bitwise_equals_the_plain_group(ctx, monkeypatch, dtype):
+    """next() steps through the one-member RCCL group (sliced M-step, collectives, member thread) are
+    bit-identical to the same steps through a plain one-member group, in both dtypes."""
+    import stc
+
+    rng = np.random.default_rng(5)
+    D, V, k = 400, 3000, 9
+    corpus = random_corpus(rng, D, V, 1, 50, empty_every=9)
+    runs = []
+    for knob in ("0", "1"):
+        monkeypatch.setenv("STC_GROUP_RCCL", knob)
+        with stc.LdaGroup([0], k, V, dtype=dtype, mini_batch_fraction=0.2, seed=4,
+                          optimize_doc_concentration=True) as g:
+            assert g.transport() == ("rccl" if knob == "1" else "none")
+            g.set_corpus(corpus)
+            g.init_random(6)
+            for _ in range(6):
+                g.next(stats=False)
+            runs.append((g.topics(), g.alpha(), g.iteration()))
+    (t0, a0, i0), (t1, a1, i1) = runs
+    assert i0 == i1 == 6
+    np.testing.assert_array_equal(t1, t0)
+    np.testing.assert_array_equal(a1, a0)
+
+
+def test_group_transport_kinds(ctx, monkeypatch):
+    import stc
+
+    monkeypatch.delenv("STC_GROUP_RCCL", raising=False)
+    with stc.LdaGroup([0], 8, 100) as g:
+        assert g.transport() == "none"
+    with stc.LdaGroup([0, 0], 8, 100) as g:
+        assert g.transport() == "in-process"

@@ -2,9 +2,11 @@
 reference's known answers (tests/golden/en_topicdist.json, en_describe.json).
 
 Tolerances: f64 mode (the default and the benchmark headline) restates Spark's double arithmetic, so
-λ/γ/bound agree to ~1e-9 relative; f32 mode (the fast secondary) is checked against the north-star
-bars: topicsMatrix within 1e-4 relative, logPerplexity within 1e-5 relative, identical top-10 terms
-per topic.
+λ/γ/bound agree to ~1e-9 relative and meets the north-star bars (topicsMatrix 1e-4, logPerplexity 1e-5,
+identical top-10 terms) everywhere.  f32 mode (the fast secondary) is held to those bars on the synthetic
+cases here, but it does NOT meet the topicsMatrix bar on configs[0]: one book's E-step takes ≈3300
+iterations there and the fp32 trajectory stops at another iterate (4.8e-4 relative,
+test_gpu_config1.py), so fp32 is not a north-star-parity mode and every fp32 bench line says so.
 """
 import numpy as np
 import pytest

@@ -53,3 +53,7 @@ def test_short_java_arrays_throw_before_the_library_is_called(tmp_path):
     assert rows["hashingTf_sized"][0] == iae and rows["hashingTf_sized"][1].startswith("requirement failed: ctx")
     # the handle's shape is looked up (and fails on a null handle) before any array is touched
     assert rows["ldaGetTopics_null_handle"] == (iae, "requirement failed: lda")
+    # idfGet sizes its checks from the model (stc_didf_shape), not from the caller's cols
+    assert rows["idfGet_null_model"] == (iae, "requirement failed: model")
+    # the ml transform's batched call (HipLDAModel → groupTopicDistribution) reaches stc_group_topic_distribution
+    assert rows["groupTopicDistribution_null_group"] == (iae, "requirement failed: group/member index")

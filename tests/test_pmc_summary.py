@@ -66,3 +66,24 @@ def test_summary_without_an_estep_kernel_is_refused(tmp_path, monkeypatch):
         P.main()
     assert "refusing" in str(e.value)
     assert not (tmp_path / "profiles" / "pmc_traffic.json").exists()
+
+
+def test_steady_window_keeps_the_last_dispatches(tmp_path):
+    """--steady: only the last fraction of each kernel's dispatches (the timed minibatches) is averaged,
+    both in the kernel-trace stats table and in the counter passes (config 4's average
+    included the cold launches)."""
+    trace = tmp_path / "t.csv"
+    with open(trace, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writeheader()
+        for i in range(10):  # 5 cold launches of 1000 ns, then 5 of 100 ns
+            w.writerow({"Dispatch_Id": i + 1, "Kernel_Name": "k_estep", "Start_Timestamp": 0,
+                        "End_Timestamp": 1000 if i < 5 else 100})
+    out = tmp_path / "s.csv"
+    P.steady_stats(str(trace), str(out), 0.5)
+    (row,) = list(csv.DictReader(open(out)))
+    assert int(float(row["Calls"])) == 5 and float(row["AverageNs"]) == 100.0
+    rows = [{"Dispatch_Id": str(i), "v": i} for i in (3, 1, 2, 4)]
+    assert [r["v"] for r in P._last(rows, 0.5)] == [3, 4]
+    assert P.WINDOW.search("k_sstats<double, 2>") and P.WINDOW.search("k_estep_rows64<RShape<13, 5, 6>, true, false>")
+    assert not P.WINDOW.search("k_lambda_eeb<double, 2, true>") and not P.WINDOW.search("k_sample")

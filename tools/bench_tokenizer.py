@@ -27,7 +27,7 @@ ctx = stc.Context(0)
 lib = ctx.lib
 import ctypes as C  # noqa: E402
 from stc import _lib as L  # noqa: E402
-out = np.zeros(n, np.uint8)
+out = np.zeros(n + n // 2, np.uint8)  # stc_tokenize's bound: lower-casing may grow text by half
 tok = np.zeros(n + a.docs + 1, np.int64)
 doc = np.zeros(a.docs + 1, np.int64)
 nb, nt = C.c_int64(), C.c_int64()
@@ -35,7 +35,7 @@ ts = []
 for r in range(a.reps + 1):
     t0 = time.perf_counter()
     L.check(lib.stc_tokenize(ctx.handle, L.ptr(text, C.c_uint8), n, L.ptr(off, C.c_int64), a.docs,
-                             L.ptr(out, C.c_uint8), C.byref(nb), L.ptr(tok, C.c_int64), C.byref(nt),
+                             L.ptr(out, C.c_uint8), out.size, C.byref(nb), L.ptr(tok, C.c_int64), C.byref(nt),
                              L.ptr(doc, C.c_int64)))
     ts.append(time.perf_counter() - t0)
 print(json.dumps({"docs": a.docs, "bytes": n, "tokens": nt.value, "kept_bytes": nb.value,

@@ -1,4 +1,4 @@
-"""Summarise tools/gpu_featpmc.sh's FETCH_SIZE / WRITE_SIZE passes of the featurisation line into
+"""Summarise tools/gpu.sh feat's FETCH_SIZE / WRITE_SIZE passes of the featurisation line into
 profiles/<tag>_featurisation_pmc.json (read by bench.py's featurisation line as `traffic`).
 
   python tools/feat_pmc_summary.py gpurun_out/featpmc --tag r04
