@@ -653,8 +653,8 @@ def main():
             "subsampling_rate": a.fraction, "corpus": a.corpus, "parallelism": parallelism,
             "launch": {"single": "one process, one GPU",
                        "ranks": f"{world} processes (torchrun), one GPU each, RCCL communicator via stc_comm_init",
-                       "group": f"one process, {world} GPUs through stc_group (one host thread per device, "
-                                f"ncclCommInitAll)"}[mode],
+                       "group": f"one process, {world} GPU(s) through stc_group (one host thread per device), "
+                                f"collectives: {model.h.transport() if mode == 'group' else ''}"}[mode],
             "mean_nnz_per_doc": head["mean_nnz_per_doc"], "mean_inner_iters": head["mean_inner_iters"],
             "model_state": (f"after {a.state_minibatches} minibatches from lambda0 (Gamma(100,1/100))"
                             if a.state == "burn-in" else

@@ -57,6 +57,9 @@ class FakeGroup:
     def enable_timing(self, on=True):
         pass
 
+    def transport(self):
+        return "rccl" if len(self.devices) > 1 else "none"
+
     def counters(self):
         n = len(self.devices)
         return [{"docs": 10 * self.steps, "entries": 1000 * self.steps, "inner_iters": 50 * self.steps,
