@@ -103,7 +103,8 @@ def algorithmic_bytes(nnz, k, docs, dtype):
 
 
 # the E-step kernels' sources: a PMC entry counts only if it was measured on these exact files
-ESTEP_SOURCES = ("lda_rows64.hip", "psi64.h", "lda_grid.hip", "lda_wide.hip", "lda.hip", "estep_common.h", "lda_kernels.h")
+ESTEP_SOURCES = ("lda_rows64.hip", "psi64.h", "lda_grid.hip", "lda_wide.hip", "lda_team64.hip", "team_exchange.h", "lda.hip",
+                 "estep_common.h", "lda_kernels.h")
 
 
 def estep_sources_sha():
@@ -465,6 +466,10 @@ def summarize(r, a, dtype, world, steps, corpus_kind, kernel):
 def kernel_name(dtype, k):
     """The training E-step kernel libstc dispatches (api.hip use_wide: grid kernels up to their topic
     capacity, fp32 k <= 128 / fp64 k <= 104, the many-topic kernel past it)."""
+    if dtype == "f64" and 104 < k <= 832:
+        return ("k_estep_tgrid64 (lda_team64.hip): the fp64 many-topic training E-step, a team of "
+                f"{-(-k // 104)} CUs per document with the topics split (rows64 grid in each member), one launch "
+                "per minibatch (documents past 448 rows: k_estep_wide / _mc)")
     if k > (128 if dtype == "f32" else 104):
         return ("k_estep_wide / k_estep_wide_mc (lda_wide.hip): the many-topic training E-step (k <= 512: a "
                 "team of CUs per document), one launch per minibatch")

@@ -84,6 +84,8 @@ struct stc_lda {
   // many-topic documents larger than one CU: a team of P CUs per document (lda_wide.hip
   // k_estep_wide_mc); STC_WIDE_TEAM=n forces P = n (1: the one-CU kernel)
   int team_force = 0;
+  bool tgrid = true;  // fp64 many-topic documents: the topic-split grid team kernel when they fit (STC_TGRID=0: off)
+  bool tgrid_require = false;  // STC_TGRID=2 (tests): a many-topic fp64 launch that cannot take it is an error
   DevBuf team_words, team_x;
   unsigned* htmo = nullptr;  // pinned copy of the team kernel's timeout word
   int64_t team_fallbacks = 0;  // team launches re-run on the one-CU kernel after a timeout
@@ -507,11 +509,22 @@ void ensure_order(stc_lda& L) {
 struct TeamChoice {
   int P = 1;
   bool topics = false;
+  bool grid = false;  // the fp64 topic-split grid kernel (lda_team64.hip k_estep_tgrid64)
 };
 template <typename T>
-TeamChoice team_choice(const stc_lda& L, double mean_rows) {
+TeamChoice team_choice(const stc_lda& L, double mean_rows, int64_t max_row) {
   const double need = 1.05 * mean_rows;
   if (L.team_force == 1) return {1, false};
+  // fp64: the topic-split team with the rows64 grid in every member (members of 104 topics) when every
+  // document of the corpus fits its 448 rows (config 4: k = 500, P = 5, 371 ± 10 rows); STC_TGRID=0: off
+  if constexpr (std::is_same<T, double>::value) {
+    const int P = lda::tgrid64_members(L.kp);
+    if (L.tgrid && L.team_force == 0 && P >= 2 && P <= 8 && max_row >= 0 && max_row <= lda::tgrid64_row_cap())
+      return {P, true, true};
+    if (L.tgrid_require)
+      throw Error(STC_ERR_STATE, "STC_TGRID=2: the fp64 grid team kernel cannot take this launch (k " + std::to_string(L.k) +
+                                     ", longest document " + std::to_string(max_row) + " rows)");
+  }
   if (L.k <= 512) {
     if (L.team_force > 1) return {L.team_force, false};
     const int P = (int)std::ceil(need / std::max(lda::wide_resident_rows<T>(L.k), 1));
@@ -552,7 +565,7 @@ bool launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamCh
   if (wt.blocks <= 0) return false;  // fewer CUs than one team per XCD group: the one-CU kernel
   const int teams = wt.blocks / P;
   // granules per member: rows split, the s partials + Σ r·φ; topics split, the φ partials + Σ|Δγ| + Σγ
-  wt.xstride = std::max<int64_t>(L.kp + 1, 512 + 2);
+  wt.xstride = tc.grid ? lda::tgrid64_xstride() : std::max<int64_t>(L.kp + 1, 512 + 2);
   const size_t xbytes = 16 * (size_t)teams * 2 * P * (size_t)wt.xstride;
   L.team_words.reserve(16);
   L.team_x.reserve(xbytes);
@@ -568,8 +581,15 @@ bool launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamCh
   // (a tag left by an earlier launch could equal an epoch this launch waits for)
   HIP_CHECK(hipMemsetAsync(L.team_words.p, 0, 16, s));
   HIP_CHECK(hipMemsetAsync(L.team_x.p, 0, xbytes, s));
-  const bool ok = tc.topics ? lda::launch_estep_wide_tc<T>(s, w, stats, wt) : lda::launch_estep_wide_mc<T>(s, w, stats, wt);
+  bool ok;
+  if constexpr (std::is_same<T, double>::value) {
+    ok = tc.grid ? lda::launch_estep_tgrid64(s, w, stats, wt)
+                 : tc.topics ? lda::launch_estep_wide_tc<T>(s, w, stats, wt) : lda::launch_estep_wide_mc<T>(s, w, stats, wt);
+  } else {
+    ok = tc.topics ? lda::launch_estep_wide_tc<T>(s, w, stats, wt) : lda::launch_estep_wide_mc<T>(s, w, stats, wt);
+  }
   if (ok) HIP_CHECK(hipMemcpyAsync(L.htmo, wt.tmo, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  if (!ok && tc.grid && L.tgrid_require) throw Error(STC_ERR_STATE, "STC_TGRID=2: the grid team could not be resident");
   return ok;
 }
 
@@ -584,7 +604,7 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
     lda::EStepArgs<T> w = a;
     w.slot0 = 0;
     w.n = n_short;
-    const TeamChoice tc = use_wide(L.k, L.dtype) && !bound ? team_choice<T>(L, mean_rows) : TeamChoice{};
+    const TeamChoice tc = use_wide(L.k, L.dtype) && !bound ? team_choice<T>(L, mean_rows, m.max_row) : TeamChoice{};
     const bool team = tc.P > 1 && launch_wide_team<T>(L, w, stats, tc);
     if (team) {  // launched (a grid that could not be resident falls through to the one-CU kernel)
       HIP_CHECK(hipStreamSynchronize(s));
@@ -1685,6 +1705,9 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->sort_docs = !(sd && sd[0] == '0');
     const char* wt = std::getenv("STC_WIDE_TEAM");
     L->team_force = wt ? std::max(0, std::min(8, std::atoi(wt))) : 0;
+    const char* tg = std::getenv("STC_TGRID");
+    L->tgrid = !(tg && tg[0] == '0');
+    L->tgrid_require = tg && tg[0] == '2';
     const char* fc = std::getenv("STC_COLLECTIVE_MSTEP");
     L->force_coll = fc && fc[0] == '1';
     ensure_layout(*L);  // λ, Bp, stat, logscale, colpart for the current shard count

@@ -126,6 +126,13 @@ template <typename T>
 bool launch_estep_wide_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt);
 template <typename T>
 void launch_estep_wide(hipStream_t s, const EStepArgs<T>& a, bool stats, bool bound);
+// fp64 many-topic team E-step with the TOPICS split over P = tgrid64_members(kp) CUs and the rows64 grid
+// inside a member (lda_team64.hip k_estep_tgrid64): nnz ≤ tgrid64_row_cap(); wt.xstride ≥ tgrid64_xstride();
+// false: the grid could not be resident at once (nothing launched)
+int tgrid64_row_cap();
+int tgrid64_members(int kp);
+int64_t tgrid64_xstride();
+bool launch_estep_tgrid64(hipStream_t s, const EStepArgs<double>& a, bool stats, const WideTeam& wt);
 
 // Batch partition: slots [0, n_short) = members with nnz <= cap (wave kernel), then the rest.
 void launch_part_flags(hipStream_t s, const int64_t* indptr, const int32_t* batch, int64_t n,

@@ -24,11 +24,13 @@ TRAINING = [
     "k_estep_grid64<DShape<13, 5>, true, false, true>",
     "k_estep<double, true, false>",
     "k_estep_wide<float, 4, 32, true, false>",
+    "k_estep_tgrid64<13, true>",
 ]
 NOT_TRAINING = [
     "k_estep_rows64<RShape<13, 5, 6>, false, true>",   # the bound's E-step
     "k_estep_grid<GShape<2, 26, 6, 2>, false, false, true>",  # inference
     "k_estep_wide_mc<double, 1, 64, false>",
+    "k_estep_tgrid64<13, false>",
     "k_sstats<double, 8>",
     "k_lambda_eeb<double, 4, true>",
 ]

@@ -43,6 +43,7 @@ ESTEP = re.compile(r"k_estep_grid64<DShape<[^>]*>, true, false, (true|false)>$" 
                    r"|k_estep_rows64(_long)?<RShape<[^>]*>, true, false(, (true|false))?>$"
                    r"|k_estep_grid(_long)?<GShape<[^>]*>, true, false(, (true|false))?>$"
                    r"|k_estep_wide_(mc|tc)<\w+, \d+, \d+, true>$"
+                   r"|k_estep_tgrid64<\d+, true>$"
                    r"|k_estep(_wave|_wide)?<(?!DShape|RShape|GShape).*, true, false>$")
 
 
