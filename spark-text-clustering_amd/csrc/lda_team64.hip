@@ -40,6 +40,10 @@ constexpr int kTSbPitch = 66;           // s-partial row pitch (doubles): 64 par
 constexpr int kTSlotD = 64 * kTSets;    // granule slot of a member's Σ|Δγ| partial (rows: [0, nnz))
 constexpr int kTSlotG = kTSlotD + 1;    // … of its final Σγ partial
 constexpr int kTXStride = kTSlotG + 1;  // granules per member and parity
+constexpr int kTMaxP = 8;               // members at most (k ≤ 832)
+#ifndef TG_LOAD_BATCH
+#define TG_LOAD_BATCH 2                 // row sets whose block loads are in flight together
+#endif
 
 template <int KL>
 struct TLds {
@@ -206,7 +210,13 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
   constexpr int KT = TLds<KL>::KT, KLP = TLds<KL>::KLP;
   constexpr int RG = R < kTReg ? R : kTReg;  // row sets in VGPRs; [RG, R) in sm.ovf
   static_assert(R >= 1 && R <= kTSets && R - RG <= 1, "row sets");
-  const int lane = t.lane, w = t.w, tl = t.tl, rl = t.rl;
+  STAMP_DECL
+  // the lane index laundered per document: every lane-derived index below (the block loads' piece
+  // offsets and worker-lane permutes, the LDS addresses) is then computed per document instead of being
+  // hoisted out of the persistent document loop and held — spilled — across every fixed point
+  int lane = t.lane;
+  asm volatile("" : "+v"(lane));
+  const int w = t.w, tl = lane & 7, rl = lane >> 3;
   const int kp = a.kp, nnz = d.nnz, m0 = t.m0;
   const int qn = d.qn;
   const bool wv = d.wv;
@@ -224,34 +234,49 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
     double* const stg = &sm.u.stage[w][0][0];
     constexpr int SP = KT + 2;
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
-      double2 pcs[NP];
+    for (int j0 = 0; j0 < R; j0 += TG_LOAD_BATCH) {
+      // TG_LOAD_BATCH row sets' loads in flight together; the scheduling barriers keep the compiler from
+      // hoisting every set's loads to the top (all in flight at once they took 168 VGPRs and spilled B)
+      __builtin_amdgcn_sched_barrier(0);
+      double2 pcs[TG_LOAD_BATCH][NP];
 #pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const int c = lane + 64 * i;
-        const int srow = c / C2, q = c - srow * C2;
-        const int id = __builtin_amdgcn_ds_bpermute((8 * j + (srow & 7)) << 2, d.qid);  // its worker lane
-        const bool keep = c < 8 * C2 && q < c2v && 64 * j + 8 * w + srow < nnz;
-        const double2 x = *reinterpret_cast<const double2*>(a.Bp + (int64_t)(keep ? id : 0) * kp + (keep ? m0 + 2 * q : 0));
-        pcs[i] = keep ? x : make_double2(0.0, 0.0);
+      for (int jj = 0; jj < TG_LOAD_BATCH; ++jj) {
+        const int j = j0 + jj;
+        if (j >= R) break;
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const int c = lane + 64 * i;
+          const int srow = c / C2, q = c - srow * C2;
+          const int id = __builtin_amdgcn_ds_bpermute((8 * j + (srow & 7)) << 2, d.qid);  // its worker lane
+          const bool keep = c < 8 * C2 && q < c2v && 64 * j + 8 * w + srow < nnz;
+          const double2 x = *reinterpret_cast<const double2*>(a.Bp + (int64_t)(keep ? id : 0) * kp + (keep ? m0 + 2 * q : 0));
+          pcs[jj][i] = keep ? x : make_double2(0.0, 0.0);
+        }
       }
 #pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const int c = lane + 64 * i;
-        const int srow = c / C2, q = c - srow * C2;
-        if (c < 8 * C2) *reinterpret_cast<double2*>(stg + srow * SP + 2 * q) = pcs[i];
-      }
-      __builtin_amdgcn_wave_barrier();  // one wave writes and reads its stage; LDS is in order per wave
+      for (int jj = 0; jj < TG_LOAD_BATCH; ++jj) {
+        const int j = j0 + jj;
+        if (j >= R) break;
 #pragma unroll
-      for (int p = 0; p < KL; ++p) {
-        const double v = stg[rl * SP + KL * tl + p];
-        if (j < RG) B[j < RG ? j : 0][p] = v;
-        else ovf[64 * p] = v;
+        for (int i = 0; i < NP; ++i) {
+          const int c = lane + 64 * i;
+          const int srow = c / C2, q = c - srow * C2;
+          if (c < 8 * C2) *reinterpret_cast<double2*>(stg + srow * SP + 2 * q) = pcs[jj][i];
+        }
+        __builtin_amdgcn_wave_barrier();  // one wave writes and reads its stage; LDS is in order per wave
+#pragma unroll
+        for (int p = 0; p < KL; ++p) {
+          const double v = stg[rl * SP + KL * tl + p];
+          if (j < RG) B[j < RG ? j : 0][p] = v;
+          else ovf[64 * p] = v;
+        }
+        __builtin_amdgcn_wave_barrier();
       }
-      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   __syncthreads();  // the staging area is the loop's partial arrays; (also publishes the first eθ, γ, α/ψc)
+  STAMP(0);  // block loads and their barrier
 
   double* const pa = &sm.u.l.pa[w][0][0];
   double* const sb = &sm.u.l.sb[0][0];
@@ -285,6 +310,7 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
       const double2 x0 = pr[0], x1 = pr[1], x2 = pr[2], x3 = pr[3];
       part = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
     }
+    STAMP(1);  // eθ reads, φ FMAs, partial stores, worker sums
     // ---- exchange: the member's φ partials and Σ|Δγ| partial out, the team's sums in member order
     ++epoch;
     {
@@ -292,8 +318,40 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
       if (t.pub_ok && wv) put_granule<double>(t.rs, base + qn, epoch, part);
       if (t.pub_ok && threadIdx.x == 0) put_granule<double>(t.rs, base + kTSlotD, epoch, dmine);
     }
-    const double phi = team_sum(t, epoch, qn, part, wv, s_abort);
-    const double dsum = team_sum(t, epoch, kTSlotD, dmine, true, s_abort);
+    // every partner's row partial and Σ|Δγ| partial requested together (one L2 round trip per poll, not
+    // one per member and value), then summed in member order
+    double phi = 0.0, dsum = 0.0;
+    {
+      const int base = (int)(epoch & 1) * t.P * t.xstride;
+      double vr[kTMaxP], vd[kTMaxP];
+      for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (int m = 0; m < kTMaxP; ++m) {
+          vr[m] = 0.0;
+          vd[m] = 0.0;
+          if (m < t.P && m != t.member) {
+            if (wv) ok &= get_granule<double>(t.rs, base + m * t.xstride + qn, epoch, vr[m]);
+            ok &= get_granule<double>(t.rs, base + m * t.xstride + kTSlotD, epoch, vd[m]);
+          }
+        }
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        if (spin_give_up(spins, t.tmo, t.spin_limit)) {
+          *s_abort = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int m = 0; m < kTMaxP; ++m) {
+        if (m < t.P) {
+          phi += m == t.member ? part : vr[m];
+          dsum += m == t.member ? dmine : vd[m];
+        }
+      }
+      if (!wv) phi = 0.0;
+    }
+    STAMP(2);  // exchange: publish, poll, member-order sums
     bool live = false;
     if (lane < 8 * R) {
       const double ph = fma(qe2, 0x1p-53, phi);
@@ -313,6 +371,7 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
     // Spark: while (meanGammaChange > 1e-3); dsum is identical in every wave of every member unless a
     // wave timed out, which every wave sees after the barrier below
     const bool stop = (it > 0 && dsum <= a.stop_thr) || it >= a.max_iter;
+    STAMP(3);  // r, ε' ballot, r reads
 
     // Phase B: s partials over the lane's R rows, one row lane's slot per topic
     if (!stop) {
@@ -324,7 +383,9 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
         sb[(KL * tl + p) * kTSbPitch + 8 * w + rl] = x;
       }
     }
+    STAMP(4);  // s FMAs + partial stores
     __syncthreads();  // (1) s partials, esum and any give-up published
+    STAMP(5);  // barrier 1
     if (*s_abort) return -1;
     if (stop) break;
     const bool psi = (w >> 2) == (it & 1);
@@ -362,11 +423,14 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
       if (lane == 0) sm.dpart[w & 3] = dw;
       __builtin_amdgcn_s_setprio(0);
     }
+    STAMP(psi ? 6 : 8);  // ψ phase (ψ waves; the others: nothing)
     __syncthreads();  // (2) eθ, γ, Σ|Δγ| partials published
+    STAMP(psi ? 7 : 9);  // barrier 2 (ψ waves / the others)
     dmine = (sm.dpart[0] + sm.dpart[1]) + (sm.dpart[2] + sm.dpart[3]);
     ++it;
   }
 #undef BV
+  STAMP_FLUSH
   return it;
 }
 
@@ -489,6 +553,8 @@ __global__ __launch_bounds__(kTThreads, 1) void k_estep_tgrid64(EStepArgs<double
 }
 
 }  // namespace
+
+STC_STAMP_READER(stc_debug_stamps_team64)
 
 int tgrid64_row_cap() { return 64 * kTSets; }
 int tgrid64_members(int kp) { return (kp + 8 * kTKL - 1) / (8 * kTKL); }

@@ -1,4 +1,5 @@
-"""Where the team E-step (lda_wide.hip k_estep_wide_mc) spends its cycles: per-phase s_memtime stamps.
+"""Where the team E-step spends its cycles: per-phase s_memtime stamps of lda_wide.hip k_estep_wide_mc
+(--kernel mc, with STC_WIDE_TEAM=P) or lda_team64.hip k_estep_tgrid64 (--kernel tgrid, the fp64 default).
 
     make -C spark-text-clustering_amd/csrc stamp
     STC_LIB=spark-text-clustering_amd/stc/libstc_stamp.so python tools/stamp_team.py [--dtype f64 ...]
@@ -18,8 +19,11 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "spark-text-clustering_amd"))
 
-PHASES = ["per-doc preamble + block loads", "A: phi rows + reduce", "barriers, r, sum r*phi", "B: s partial",
-          "exchange: publish + wait + sums", "gamma, psi/exp", "outputs"]
+PHASES = {"mc": ["per-doc preamble + block loads", "A: phi rows + reduce", "barriers, r, sum r*phi", "B: s partial",
+                 "exchange: publish + wait + sums", "gamma, psi/exp", "outputs"],
+          "tgrid": ["block loads", "A: phi FMAs + worker sums", "exchange: publish + poll + sums", "r, eps ballot, r reads",
+                    "B: s FMAs + stores", "barrier 1", "psi phase (psi waves)", "barrier 2 (psi waves)",
+                    "psi phase (others: empty)", "barrier 2 (others)"]}
 
 
 def main():
@@ -33,7 +37,9 @@ def main():
     p.add_argument("--burn", type=int, default=5)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--seed", type=int, default=20261015)
+    p.add_argument("--kernel", default="tgrid", choices=sorted(PHASES))
     a = p.parse_args()
+    phases = PHASES[a.kernel]
     assert "stamp" in os.environ.get("STC_LIB", ""), "set STC_LIB to the stamp build"
     import stc
     from stc import synth
@@ -42,7 +48,7 @@ def main():
     print("corpus generated", file=sys.stderr, flush=True)
     ctx = stc.Context(0)
     lib = stc._lib.load()
-    reader = lib.stc_debug_stamps_wide
+    reader = lib.stc_debug_stamps_team64 if a.kernel == "tgrid" else lib.stc_debug_stamps_wide
     reader.restype = C.c_int
     reader.argtypes = [C.POINTER(C.c_ulonglong), C.c_int, C.c_int]
     buf = (C.c_ulonglong * 12)()
@@ -65,12 +71,12 @@ def main():
     cyc = np.array(buf[:], dtype=np.float64)
     docs = c1["docs"] - c0["docs"]
     iters = c1["inner_iters"] - c0["inner_iters"]
-    tot = cyc[:len(PHASES)].sum()
-    P = int(os.environ.get("STC_WIDE_TEAM", "0")) or None
+    tot = cyc[:len(phases)].sum()
+    P = int(os.environ.get("STC_WIDE_TEAM", "0")) or (-(-a.k // 104) if a.kernel == "tgrid" else None)
     out = {"k": a.k, "dtype": a.dtype, "team": P or "auto", "docs": int(docs),
            "mean_inner_iters": iters / max(1, docs), "share": {}, "cycles_per_block_wave_iter": {}}
     waves = 8 * (P or 1)
-    for i, name in enumerate(PHASES):
+    for i, name in enumerate(phases):
         out["share"][name] = round(cyc[i] / tot, 4)
         out["cycles_per_block_wave_iter"][name] = round(cyc[i] / (waves * max(1, iters)), 1)
     out["note"] = "per-iteration cycles assume `team` blocks per document (set STC_WIDE_TEAM)"
