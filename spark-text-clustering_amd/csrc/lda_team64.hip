@@ -12,8 +12,9 @@
 //   exchange     : every member publishes its nnz partials (and its Σ|Δγ| partial) as epoch granules and
 //     sums the P partials of its rows in member order, so φ, r = cts/φ, the ψ(Σγ') identity and the stop
 //     rule are bit-identical in every member and the team leaves the loop together;
-//   s = Bᵀr      : R lane-local FMAs per topic, 64 partials per topic to LDS, one block barrier;
-//   ψ phase      : four waves (one per SIMD, alternating wave sets by iteration parity) add a topic's 64
+//   s = Bᵀr      : R lane-local FMAs per topic, the eight row lanes' partials reduce-scattered inside the
+//     wave, eight partials per topic (one per wave) to LDS, one block barrier;
+//   ψ phase      : four waves (one per SIMD, alternating wave sets by iteration parity) add a topic's 8
 //     partials, update γ and eθ = exp(ψ(γ) − ψ(Σγ') − ψc) for their KT/4 topics, second barrier.
 // Against k_estep_wide_mc (the rows split: one topic per lane, every row's φ a 512-lane reduction, the
 // s partials of all k topics exchanged, ψ of all k topics in every member, registers spilled in the loop)
@@ -36,7 +37,7 @@ constexpr int kTSets = 7;               // row sets of 64 rows (8 waves × 8 row
 constexpr int kTReg = 6;                // row sets in VGPRs (the seventh in LDS)
 constexpr int kTKL = 13;                // topics per topic lane: KT = 104 per member
 constexpr int kTPaPitch = 10;           // φ-partial row pitch (doubles): conflict-free 16-B worker reads
-constexpr int kTSbPitch = 66;           // s-partial row pitch (doubles): 64 partials + pad, 16-B aligned rows
+constexpr int kTSbPitch = 10;           // s-partial row pitch (doubles): one per wave + pad, 16-B aligned rows
 constexpr int kTSlotD = 64 * kTSets;    // granule slot of a member's Σ|Δγ| partial (rows: [0, nnz))
 constexpr int kTSlotG = kTSlotD + 1;    // … of its final Σγ partial
 constexpr int kTXStride = kTSlotG + 1;  // granules per member and parity
@@ -61,7 +62,7 @@ struct TLds {
   union {
     struct {
       double pa[kTW][8 * kTSets][kTPaPitch];        // φ partials (wave, worker row, topic lane)
-      double sb[KT][kTSbPitch];                     // s partials (topic, row lane 8·w + rl)
+      double sb[KT][kTSbPitch];                     // s partials (topic, wave): each wave's eight row lanes summed
     } l;
     double stage[kTW][8][KT + 2];                   // block loads: eight rows per wave at a time
   } u __attribute__((aligned(16)));
@@ -373,14 +374,32 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
     const bool stop = (it > 0 && dsum <= a.stop_thr) || it >= a.max_iter;
     STAMP(3);  // r, ε' ballot, r reads
 
-    // Phase B: s partials over the lane's R rows, one row lane's slot per topic
+    // Phase B: s partials over the lane's R rows, summed over the wave's eight row lanes by a
+    // reduce-scatter (lane bits 5, 4, 3: permlane32 / permlane16 swaps, then row_ror:8), so each lane
+    // stores two topics' wave sums and a ψ lane reads eight partials (one per wave) instead of 64
     if (!stop) {
+      static_assert(KL == 13, "the reduce-scatter below is laid out for 13 topics per topic lane");
+      double x[14];
 #pragma unroll
       for (int p = 0; p < KL; ++p) {
-        double x = 0.0;
+        double acc = 0.0;
 #pragma unroll
-        for (int j = 0; j < R; ++j) x = fma(BV(j, p), rr[j], x);
-        sb[(KL * tl + p) * kTSbPitch + 8 * w + rl] = x;
+        for (int j = 0; j < R; ++j) acc = fma(BV(j, p), rr[j], acc);
+        x[p] = acc;
+      }
+      x[13] = 0.0;
+      double a7[7], b4[4];
+      swap_add_nd<true, 7>(x, x + 7, a7);           // bit 5: p [0, 7) | [7, 14)
+      const double a8[8] = {a7[0], a7[1], a7[2], a7[3], a7[4], a7[5], a7[6], 0.0};
+      swap_add_nd<false, 4>(a8, a8 + 4, b4);        // bit 4: entries [0, 4) | [4, 8)
+      const bool h3 = (lane & 8) != 0;
+      const double c0 = rs_dpp_d<DPP_ROW_ROR8>(b4[0], b4[2], h3);  // bit 3: entries {0, 1} | {2, 3}
+      const double c1 = rs_dpp_d<DPP_ROW_ROR8>(b4[1], b4[3], h3);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int jb = ((lane & 16) ? 4 : 0) + (h3 ? 2 : 0) + i;  // entry of the bit-5 list
+        const int p = ((lane & 32) ? 7 : 0) + jb;
+        if (jb < 7 && p < KL) sb[(KL * tl + p) * kTSbPitch + w] = i == 0 ? c0 : c1;
       }
     }
     STAMP(4);  // s FMAs + partial stores
@@ -394,18 +413,8 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
       double dg = 0.0;
       if (t.town) {
         const double2* const sp = reinterpret_cast<const double2*>(sb + t.tt * kTSbPitch);
-        // the 64 partials in a fixed order, a quarter in flight at a time (a rolled loop: unrolled, the
-        // compiler issues all 32 loads at once and the block's registers spill)
-        double s = 0.0;
-#pragma unroll 1
-        for (int hh = 0; hh < 4; ++hh) {
-          double2 xs[8];
-#pragma unroll
-          for (int i = 0; i < 8; ++i) xs[i] = sp[8 * hh + i];
-          const double g = (((xs[0].x + xs[0].y) + (xs[1].x + xs[1].y)) + ((xs[2].x + xs[2].y) + (xs[3].x + xs[3].y))) +
-                           (((xs[4].x + xs[4].y) + (xs[5].x + xs[5].y)) + ((xs[6].x + xs[6].y) + (xs[7].x + xs[7].y)));
-          s = hh == 0 ? g : s + g;
-        }
+        const double2 x0 = sp[0], x1 = sp[1], x2 = sp[2], x3 = sp[3];  // the eight waves' sums, fixed order
+        const double s = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
         const double g = sm.gam[t.tt], eo = sm.eth[t.ttl][t.ttp];
         const double2 ap = *reinterpret_cast<const double2*>(&sm.apc[t.tt][0]);  // α_t, ψc_t
         const double2 e01 = *reinterpret_cast<const double2*>(&sm.esum[0]);
