@@ -69,6 +69,19 @@ __device__ __forceinline__ void swap_add_nd(const double* xs, const double* ys, 
 #pragma unroll
   for (int i = 0; i < N; ++i) out[i] = mkd(xl[i], xh[i]) + mkd(yl[i], yh[i]);
 }
+// The s-partial reduce-scatter of the grid E-steps (lda_rows64.hip, lda_team64.hip): lane = tl + 8·rl holds
+// x[p] for its topic lane's KL ≤ 16 topics (zero-padded to 16); the eight row lanes rl (lane bits 3, 4, 5)
+// are summed in a fixed order — bit 5 by permlane32 swaps, bit 4 by permlane16 swaps, bit 3 by row_ror:8 —
+// so that lane (tl, rl) returns the wave sums of topics 2·rl and 2·rl + 1 of its topic lane.
+__device__ __forceinline__ void rs_rows8(const double (&x)[16], int lane, double& s0, double& s1) {
+  double a[8], b[4];
+  swap_add_nd<true, 8>(x, x + 8, a);   // bit 5: topics [0, 8) | [8, 16)
+  swap_add_nd<false, 4>(a, a + 4, b);  // bit 4: [0, 4) | [4, 8) of those
+  const bool h3 = (lane & 8) != 0;     // bit 3: {0, 1} | {2, 3}
+  s0 = rs_dpp_d<DPP_ROW_ROR8>(b[0], b[2], h3);
+  s1 = rs_dpp_d<DPP_ROW_ROR8>(b[1], b[3], h3);
+}
+
 // fp64 wave64 all-reduce (sum) without LDS
 __device__ __forceinline__ double wave_sum_d(double v) {
   {

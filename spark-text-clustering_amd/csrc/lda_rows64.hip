@@ -45,6 +45,9 @@
 #define R64_MIRROR 0  // 1 (k > 64): the idle wave of the ψ wave's topic set computes Σ|Δγ| off the ψ chain —
                       // measured +1.3 % E-step on the headline (r04: 31.96 vs 31.54 ms), so off
 #endif
+#ifndef R64_SB_RS
+#define R64_SB_RS 1  // Phase B's s partials reduce-scattered over the wave's row lanes (4 per topic, not 32)
+#endif
 #ifndef R64_LONG_OCC
 #define R64_LONG_OCC 1  // long-document kernel workgroups per CU the register budget is cut for
 #endif
@@ -55,7 +58,8 @@ namespace lda {
 namespace {
 
 constexpr int kW = 4;          // waves per document
-constexpr int kSbPitch = 34;   // s-partial row pitch (doubles): conflict-free 8-B stores, 16-B reads
+constexpr int kSbPitch = R64_SB_RS ? 4 : 34;  // s-partial row pitch (doubles): per wave (R64_SB_RS) or per row lane
+                                               // (conflict-free 8-B stores, 16-B reads)
 constexpr int kPaPitch = 10;   // φ-partial row pitch (doubles): conflict-free 16-B worker reads
 constexpr int kOnChipSets = 6; // row sets the common kernel holds (5 in VGPRs + 1 in LDS)
 constexpr int kMaxSets = 8;    // one worker lane per wave row: 8 row lanes × 8 sets = 64 lanes
@@ -372,6 +376,25 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
     if ((it > 0 && dsum <= a.stop_thr) || it >= a.max_iter) break;
 
     // Phase B: s partials over the lane's R rows, one row lane's slot per topic
+#if R64_SB_RS
+    {  // the eight row lanes summed inside the wave (estep_common.h rs_rows8): lane (tl, rl) stores the wave
+       // sums of its topic lane's topics 2·rl, 2·rl + 1, so a ψ lane reads 4 partials instead of 32
+      double x[16];
+#pragma unroll
+      for (int p = 0; p < 16; ++p) {
+        double acc = 0.0;
+        if (p < KL) {
+#pragma unroll
+          for (int j = 0; j < R; ++j) acc = fma(BV(j, p < KL ? p : 0), rr[j], acc);
+        }
+        x[p] = acc;
+      }
+      double s0, s1;
+      rs_rows8(x, lane, s0, s1);
+      if (2 * rl < KL) sb[(KL * tl + 2 * rl) * kSbPitch + w] = s0;
+      if (2 * rl + 1 < KL) sb[(KL * tl + 2 * rl + 1) * kSbPitch + w] = s1;
+    }
+#else
 #pragma unroll
     for (int p = 0; p < KL; ++p) {
       double x = 0.0;
@@ -379,6 +402,7 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
       for (int j = 0; j < R; ++j) x = fma(BV(j, p), rr[j], x);
       sb[(KL * tl + p) * kSbPitch + 8 * w + rl] = x;
     }
+#endif
     STAMP(3);  // s FMAs + partial stores
     __syncthreads();  // (1) s partials and esum published
     STAMP(4);  // barrier 1
@@ -387,15 +411,22 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
       if (R64_PRIO >= 1) __builtin_amdgcn_s_setprio(3);
       double dg = 0.0;
       if (town) {
-        // every LDS read of the phase issued together: the 32 partials, γ, eθ, the four ε' sums
+        // every LDS read of the phase issued together: the partials, γ, eθ, the four ε' sums
         const double2* const sp = reinterpret_cast<const double2*>(sb + tt * kSbPitch);
+#if R64_SB_RS
+        const double2 x0 = sp[0], x1 = sp[1];  // the four waves' sums
+#else
         double2 xs[16];
 #pragma unroll
         for (int h = 0; h < 16; ++h) xs[h] = sp[h];
+#endif
         const double g = mir ? gm : sm.gam[tt], eo = sm.eth[ttl][ttp];
         const double2 ap = *reinterpret_cast<const double2*>(&sm.apc[tt][0]);  // α_t, ψc_t
         const double2 e01 = *reinterpret_cast<const double2*>(&sm.esum[0]);
         const double2 e23 = *reinterpret_cast<const double2*>(&sm.esum[2]);
+#if R64_SB_RS
+        const double s = (x0.x + x0.y) + (x1.x + x1.y);
+#else
         double c4[4];
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
@@ -403,6 +434,7 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
           c4[h] = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
         }
         const double s = (c4[0] + c4[1]) + (c4[2] + c4[3]);
+#endif
         const double et = (e01.x + e01.y) + (e23.x + e23.y);
         const double csn = et != 0.0 ? digamma_fast_d(sm.ac[0] + sm.ac[1] - et) : sm.ac[2];
         const double gn = fma(eo, s, ap.x);  // γ ← eθ ⊙ s + α
@@ -425,10 +457,14 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
       double dg = 0.0;
       if (town) {
         const double2* const sp = reinterpret_cast<const double2*>(sb + tt * kSbPitch);
+        const double al = sm.apc[tt][0];
+#if R64_SB_RS
+        const double2 y0 = sp[0], y1 = sp[1];
+        const double s = (y0.x + y0.y) + (y1.x + y1.y);
+#else
         double2 xs[16];
 #pragma unroll
         for (int h = 0; h < 16; ++h) xs[h] = sp[h];
-        const double al = sm.apc[tt][0];
         double c4[4];
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
@@ -436,6 +472,7 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
           c4[h] = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
         }
         const double s = (c4[0] + c4[1]) + (c4[2] + c4[3]);
+#endif
         const double gn = fma(em, s, al);
         dg = fabs(gn - gm);
         gm = gn;  // (its eθ: the ψ wave's, from LDS, when this wave is next the ψ wave)
