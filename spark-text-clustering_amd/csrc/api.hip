@@ -96,6 +96,12 @@ struct stc_lda {
   // collectives (STC_VIRTUAL_SHARDS, for testing the slicing).
   int shards = 1, virt = 1;
   bool force_coll = false;  // STC_COLLECTIVE_MSTEP=1: the RCCL slice path even on a 1-rank communicator (tests)
+  // sharded steps: stat reduce-scattered in rs_chunks vocabulary sub-chunks on cstream, each as soon as
+  // its sstats launch is done, and the M-step of sub-chunk j under the reduce-scatter of j+1
+  // (STC_RS_CHUNKS, 1: one reduce-scatter after the whole stat)
+  int rs_chunks = 4;
+  hipStream_t cstream = nullptr;
+  hipEvent_t ev_ss[16] = {}, ev_rs[16] = {};
   int64_t Vs = 0, vpad = 0;
   bool lam_stale = false;  // rows outside this rank's slice are out of date (sharded M-step)
 
@@ -130,6 +136,11 @@ struct stc_lda {
     if (ev_fill) (void)hipEventDestroy(ev_fill);
     if (ev_samp) (void)hipEventDestroy(ev_samp);
     if (side) (void)hipStreamDestroy(side);
+    for (int j = 0; j < 16; ++j) {
+      if (ev_ss[j]) (void)hipEventDestroy(ev_ss[j]);
+      if (ev_rs[j]) (void)hipEventDestroy(ev_rs[j]);
+    }
+    if (cstream) (void)hipStreamDestroy(cstream);
   }
 };
 
@@ -651,10 +662,34 @@ const T* upload_gamma0(stc_lda& L, const double* gamma0, int64_t n) {
   return L.g0.as<T>();
 }
 
-// E-step over the n partitioned slots (L.batch / L.orig / L.bptr), then the term-sorted sstats
-// SpMM into L.stat (V×kp, row-scaled) and logphat / non-empty count into L.small.
+// a step's M-step is sharded over the ranks (reduce-scatter, slice update, all-gather)
+bool sharded(const stc_lda& L) { return L.ctx->coll() && (L.ctx->n_ranks > 1 || L.force_coll); }
+
+// the stat sub-chunk layout of a sharded step (lda_kernels.h StatMap; nsub = 1: one reduce-scatter):
+// at most rs_chunks sub-chunks of whole λ-update blocks, the last one the rest of the slice
+lda::StatMap stat_layout(const stc_lda& L) {
+  lda::StatMap m;
+  const int64_t nb = L.Vs / lda::kRowsPerBlock;
+  if (!sharded(L) || L.rs_chunks <= 1 || nb < 2) return m;
+  const int64_t per = ceil_div(nb, (int64_t)L.rs_chunks);
+  m.vs = (uint32_t)L.Vs;
+  m.vsj = (uint32_t)(per * lda::kRowsPerBlock);
+  m.n = L.shards;
+  m.nsub = (int)ceil_div(nb, per);
+  return m;
+}
+// sub-chunk j: (first canonical row within a slice, rows)
+std::pair<int64_t, int64_t> stat_sub_rows(const lda::StatMap& m, int j) {
+  const int64_t w = j < m.nsub - 1 ? (int64_t)m.vsj : (int64_t)m.vs - (int64_t)(m.nsub - 1) * m.vsj;
+  return {(int64_t)j * m.vsj, w};
+}
+
+// E-step over the n partitioned slots (L.batch / L.orig / L.bptr), then logphat / non-empty count into
+// L.small and the term-sorted sstats SpMM into L.stat (V×kp, row-scaled).  split: a training step of a
+// sharded handle — stat in the sub-chunk layout, one sstats launch per sub-chunk (ev_ss[j] after each).
 template <typename T>
-void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T* g0, int64_t iteration) {
+void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T* g0, int64_t iteration,
+                     bool split = false) {
   hipStream_t s = L.ctx->stream;
   lda::EStepArgs<T> a = estep_args<T>(L);
   a.indptr = L.corpus->indptr.as<int64_t>();
@@ -678,16 +713,7 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   record(L, 1);
   launch_split<T>(L, *L.corpus, a, n, n_short, true, false, n > 0 ? (double)E / (double)n : 0.0);
   record(L, 2);
-  HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.vpad * L.kp, s));  // padded rows stay zero
-  if (E > 0) {
-    size_t tb = L.sort_tmp.bytes;
-    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(L.sort_tmp.p, tb, L.keys.as<uint32_t>(),
-                                                 L.skeys.as<uint32_t>(), L.vals.as<uint64_t>(),
-                                                 L.svals.as<uint64_t>(), (int)E, 0, bits_for(L.V), s));
-    lda::launch_sstats<T>(s, L.skeys.as<uint32_t>(), L.svals.as<uint64_t>(), E, L.r.as<T>(),
-                          L.eth.as<T>(), L.kp, L.stat.as<T>(),
-                          L.headbuf.as<T>(), L.tailbuf.as<T>());
-  }
+  // logphat first: its all-reduce rides with the first stat sub-chunk of a sharded step
   if (n > 0) {
     lda::launch_logphat<T>(s, L.elogth.as<T>(), L.nonempty.as<int32_t>(), n, L.k, L.small.as<double>(),
                              L.lpart.as<double>());
@@ -696,6 +722,27 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   } else {
     HIP_CHECK(hipMemsetAsync(L.small.p, 0, sizeof(double) * (L.k + 1), s));
     HIP_CHECK(hipMemsetAsync(L.stats4.p, 0, sizeof(int64_t) * 4, s));
+  }
+  HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.vpad * L.kp, s));  // padded rows stay zero
+  if (E > 0) {
+    size_t tb = L.sort_tmp.bytes;
+    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(L.sort_tmp.p, tb, L.keys.as<uint32_t>(),
+                                                 L.skeys.as<uint32_t>(), L.vals.as<uint64_t>(),
+                                                 L.svals.as<uint64_t>(), (int)E, 0, bits_for(L.V), s));
+  }
+  const lda::StatMap lay = split ? stat_layout(L) : lda::StatMap{};
+  if (lay.nsub <= 1) {
+    lda::launch_sstats<T>(s, L.skeys.as<uint32_t>(), L.svals.as<uint64_t>(), E, L.r.as<T>(), L.eth.as<T>(), L.kp,
+                          L.stat.as<T>(), L.headbuf.as<T>(), L.tailbuf.as<T>());
+  } else {
+    for (int j = 0; j < lay.nsub; ++j) {
+      lda::StatMap m = lay;
+      m.sub = j;
+      lda::launch_sstats<T>(s, L.skeys.as<uint32_t>(), L.svals.as<uint64_t>(), E, L.r.as<T>(), L.eth.as<T>(),
+                            L.kp, L.stat.as<T>(), L.headbuf.as<T>(), L.tailbuf.as<T>(), m);
+      if (!L.ev_ss[j]) HIP_CHECK(hipEventCreateWithFlags(&L.ev_ss[j], hipEventDisableTiming));
+      HIP_CHECK(hipEventRecord(L.ev_ss[j], s));
+    }
   }
   record(L, 3);
 }
@@ -711,6 +758,18 @@ void mstep_slice(stc_lda& L, int r, double rho, double scale, const double* gate
                             L.Bp.as<T>() + v0 * L.kp, L.logscale.as<double>() + v0, vn, L.k, L.kp, rho, scale,
                             L.eta, gate, L.colpart.as<double>() + (int64_t)r * nbs * L.k, nbs);
 }
+// the same pass over sub-chunk j of slice r, whose summed stat rows sit at the sub-chunk layout's
+// physical rows (stat_layout); λ / expElogβ' / logscale / colsum partials at their canonical rows
+template <typename T>
+void mstep_sub(stc_lda& L, const lda::StatMap& m, int r, int j, double rho, double scale, const double* gate) {
+  const auto [off, w] = stat_sub_rows(m, j);
+  const int64_t v0 = (int64_t)r * L.Vs + off, vn = std::max<int64_t>(0, std::min(L.V - v0, w));
+  const int64_t phys = (int64_t)m.n * j * m.vsj + (int64_t)r * w;
+  lda::launch_lambda_eeb<T>(L.ctx->stream, true, L.lam.as<double>() + v0 * L.k, L.stat.as<T>() + phys * L.kp,
+                            L.Bp.as<T>() + v0 * L.kp, L.logscale.as<double>() + v0, vn, L.k, L.kp, rho, scale,
+                            L.eta, gate, L.colpart.as<double>() + (v0 / lda::kRowsPerBlock) * L.k,
+                            w / lda::kRowsPerBlock);
+}
 
 // [U] submitMiniBatch tail: the stats merge (treeReduce ≙ RCCL), updateLambda, updateAlpha.
 //  * one GPU: the fused λ update + expElogβ' pass over all rows, then colsum and ψ(colsum).
@@ -721,13 +780,32 @@ void mstep_slice(stc_lda& L, int r, double rho, double scale, const double* gate
 //    λ stays sharded (lam_stale) until a reader gathers it.  Per rank: stat (N−1)/N·V·kp·T bytes
 //    out, expElogβ' the same in, against 2(N−1)/N for an all-reduce, and 1/N of the M-step work.
 template <typename T>
+void train_tail_split(stc_lda& L, const lda::StatMap& lay, bool had_samp, int64_t n, int64_t E,
+                      stc_step_stats* st);
+template <typename T>
+void train_finish(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st);
+
+//  * N ranks with rs_chunks > 1 (stat_layout: nsub sub-chunks): sstats ran once per sub-chunk
+//    (estep_and_stats split) and recorded ev_ss[j]; the reduce-scatter of sub-chunk j (one contiguous
+//    buffer in that layout) runs on cstream as soon as ev_ss[j] fires — under the sstats launches of
+//    j+1… — with the logphat / count all-reduce in sub-chunk 0's group, and the main stream runs the
+//    M-step of sub-chunk j under the reduce-scatter of j+1.  Each element is summed over the same
+//    ranks in the same way as by the single reduce-scatter, and sstats builds every row exactly as
+//    the single launch does, so the result is the unchunked step's.
+template <typename T>
 void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
   Ctx& c = *L.ctx;
   hipStream_t s = c.stream;
-  const bool ranks = c.coll() && (c.n_ranks > 1 || L.force_coll);
+  const bool ranks = sharded(L);
+  const lda::StatMap lay = stat_layout(L);
+  const bool had_samp = L.samp_pending;
   if (L.samp_pending) {  // the next draw's counts (side stream) feed this step's collective / readback
     HIP_CHECK(hipStreamWaitEvent(s, L.ev_samp, 0));
     L.samp_pending = false;
+  }
+  if (ranks && lay.nsub > 1) {
+    train_tail_split<T>(L, lay, had_samp, n, E, st);
+    return;
   }
   if (c.coll()) {
     coll_group_start(c);
@@ -772,6 +850,64 @@ void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
   }
   if (L.cfg.optimize_doc_concentration)
     lda::launch_update_alpha(s, L.alpha.as<double>(), L.small.as<double>(), L.k, rho);
+  train_finish<T>(L, n, E, st);
+}
+
+template <typename T>
+void train_tail_split(stc_lda& L, const lda::StatMap& lay, bool had_samp, int64_t n, int64_t E,
+                      stc_step_stats* st) {
+  Ctx& c = *L.ctx;
+  hipStream_t s = c.stream;
+  if (!L.cstream) HIP_CHECK(hipStreamCreateWithFlags(&L.cstream, hipStreamNonBlocking));
+  hipStream_t cs = L.cstream;
+  if (had_samp) HIP_CHECK(hipStreamWaitEvent(cs, L.ev_samp, 0));  // the next draw's count (side stream)
+  for (int j = 0; j < lay.nsub; ++j) {
+    if (!L.ev_rs[j]) HIP_CHECK(hipEventCreateWithFlags(&L.ev_rs[j], hipEventDisableTiming));
+    HIP_CHECK(hipStreamWaitEvent(cs, L.ev_ss[j], 0));
+    const int64_t w = stat_sub_rows(lay, j).second;
+    T* chunk = L.stat.as<T>() + (int64_t)lay.n * j * lay.vsj * L.kp;
+    coll_group_start(c);
+    coll_reduce_scatter(c, chunk, chunk + (int64_t)c.rank * w * L.kp, (size_t)(w * L.kp), RcclType<T>::v, cs);
+    if (j == 0) {
+      coll_all_reduce(c, L.small.p, (size_t)(L.k + 1), ncclFloat64, cs);
+      if (L.pre_inflight) coll_all_reduce(c, L.dcnt.as<int64_t>() + 3, 1, ncclInt64, cs);
+    }
+    coll_group_end(c);
+    if (j == 0 && L.pre_inflight) {
+      HIP_CHECK(hipMemcpyAsync(L.hpre, L.dcnt.p, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, cs));
+      HIP_CHECK(hipEventRecord(L.ev_pre, cs));
+      L.pre_inflight = false;
+      L.pre_valid = true;
+    }
+    HIP_CHECK(hipEventRecord(L.ev_rs[j], cs));
+  }
+  L.iteration += 1;
+  const double rho = std::pow(L.cfg.tau0 + (double)L.iteration, -L.cfg.kappa);
+  const double batch_size = std::ceil(L.cfg.mini_batch_fraction * (double)L.corpus_total);
+  const double scale = (double)L.corpus_total / batch_size;
+  const double* gate = L.small.as<double>() + L.k;
+  for (int j = 0; j < lay.nsub; ++j) {
+    HIP_CHECK(hipStreamWaitEvent(s, L.ev_rs[j], 0));
+    if (j == 0) record(L, 4);  // the statistics of sub-chunk 0 and the logphat / count sums are in
+    mstep_sub<T>(L, lay, c.rank, j, rho, scale, gate);
+  }
+  const size_t nbs = (size_t)(L.Vs / lda::kRowsPerBlock), cnt = (size_t)(L.Vs * L.kp);
+  coll_group_start(c);
+  coll_all_gather(c, L.colpart.as<double>() + (size_t)c.rank * nbs * L.k, L.colpart.p, nbs * L.k, ncclFloat64, s);
+  coll_all_gather(c, L.Bp.as<T>() + (size_t)c.rank * cnt, L.Bp.p, cnt, RcclType<T>::v, s);
+  coll_all_gather(c, L.logscale.as<double>() + (size_t)c.rank * L.Vs, L.logscale.p, (size_t)L.Vs, ncclFloat64, s);
+  coll_group_end(c);
+  lda::launch_colsum_reduce(s, L.colpart.as<double>(), L.shards * (int64_t)nbs, L.k, gate, L.colsum.as<double>(),
+                            L.psic.as<double>());
+  L.lam_stale = true;
+  if (L.cfg.optimize_doc_concentration)
+    lda::launch_update_alpha(s, L.alpha.as<double>(), L.small.as<double>(), L.k, rho);
+  train_finish<T>(L, n, E, st);
+}
+
+template <typename T>
+void train_finish(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
+  hipStream_t s = L.ctx->stream;
   record(L, 5);
   if (L.timing) {
     L.ev_pending[L.ev_set] = true;
@@ -791,7 +927,7 @@ void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
     st->inner_iters_max = (int32_t)h4[1];
     st->cap_hits = (int32_t)h4[2];
     st->nonempty_docs = (int64_t)ne;
-    st->rho = rho;
+    st->rho = std::pow(L.cfg.tau0 + (double)L.iteration, -L.cfg.kappa);
   }
 }
 
@@ -827,7 +963,7 @@ void step_ids(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, s
   const Part p = upload_members<T>(L, ids, n);
   if (L.timing) harvest_all(L);  // partition() drained the stream
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
-  estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1);
+  estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1, true);
   train_tail<T>(L, n, p.E, st);
 }
 
@@ -931,7 +1067,7 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
   L.samp_pending = true;
   L.pre_inflight = true;
   L.pre_draw = draw + 1;
-  estep_and_stats<T>(L, n, ns32, E, nullptr, L.iteration + 1);
+  estep_and_stats<T>(L, n, ns32, E, nullptr, L.iteration + 1, true);
   train_tail<T>(L, n, E, st);
 }
 
@@ -1710,6 +1846,8 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->tgrid_require = tg && tg[0] == '2';
     const char* fc = std::getenv("STC_COLLECTIVE_MSTEP");
     L->force_coll = fc && fc[0] == '1';
+    const char* rc = std::getenv("STC_RS_CHUNKS");
+    L->rs_chunks = rc ? std::max(1, std::min(16, std::atoi(rc))) : 4;
     ensure_layout(*L);  // λ, Bp, stat, logscale, colpart for the current shard count
     L->colsum.reserve(8 * L->k);
     L->psic.reserve(16 * L->k);  // ψ(colsum), exp(−ψ(colsum))

@@ -381,7 +381,7 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
                                                 const T* __restrict__ r,
                                                 const T* __restrict__ eth, int kp, T* __restrict__ stat,
                                                 T* __restrict__ headbuf, T* __restrict__ tailbuf,
-                                                int64_t nchunks) {
+                                                int64_t nchunks, StatMap map) {
   const int c0 = (int)blockIdx.y * 64 * Q;  // this slab's first topic column
   // kU entries in flight per wave: their (term, r, doc) are read out of the lanes that loaded them
   // (v_readlane: wave-uniform, so the eθ' row address is scalar) and their eθ' rows are all requested
@@ -394,6 +394,9 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
   const int64_t p0 = chunk * kChunk;
   const int64_t p1 = (p0 + kChunk < E) ? p0 + kChunk : E;
   const uint32_t first = skeys[p0], last = skeys[p1 - 1];
+  const bool part = map.sub >= 0;  // a sub-chunk launch: only its terms' rows (StatMap)
+  // a chunk inside one (rank, sub-chunk) term range of another launch has nothing of this one's
+  if (part && stat_group(map, first) == stat_group(map, last) && stat_sub(map, first) != map.sub) return;
   const bool start_mid = p0 > 0 && skeys[p0 - 1] == first;
   const bool cont = p1 < E && skeys[p1] == last;
   T acc[Q];
@@ -402,9 +405,14 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
   uint32_t cur = first;
   auto flush = [&](uint32_t v) {
     T* dst;
+    if (part && stat_sub(map, v) != map.sub) {  // another launch's row: drop it
+#pragma unroll
+      for (int q = 0; q < Q; ++q) acc[q] = T(0);
+      return;
+    }
     if (v == first && start_mid) dst = headbuf + chunk * kp;
     else if (v == last && cont) dst = tailbuf + chunk * kp;
-    else dst = stat + (int64_t)v * kp;
+    else dst = stat + stat_row(map, v) * kp;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int col = c0 + lane + 64 * q;
@@ -417,8 +425,11 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
     uint32_t kv = cur;
     T rv = T(0);
     int32_t dv = 0;
-    if (p < p1) {  // (slot, r) travel with the sorted keys (entry_val); fp64 gathers r[e]
-      kv = skeys[p];
+    if (p < p1) kv = skeys[p];
+    // this launch's entries (a sub-chunk launch gathers nothing for the other terms)
+    const bool mine = p < p1 && (!part || stat_sub(map, kv) == map.sub);
+    const uint64_t mmask = part ? __ballot(mine) : ~0ull;
+    if (mine) {  // (slot, r) travel with the sorted keys (entry_val); fp64 gathers r[e]
       const uint64_t pv = svals[p];
       dv = (int32_t)(pv >> 32);
       if constexpr (sizeof(T) == 4) rv = __builtin_bit_cast(T, (uint32_t)pv);
@@ -435,10 +446,11 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
         vk[u] = (uint32_t)__builtin_amdgcn_readlane((int)kv, jj);
         rk[u] = readlane_t(rv, jj);
         const T* er = eth + (int64_t)__builtin_amdgcn_readlane(dv, jj) * kp;
+        const bool mu = (mmask >> jj) & 1;  // wave-uniform
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
           const int col = c0 + lane + 64 * q;
-          e[u][q] = col < kp ? er[col] : T(0);
+          e[u][q] = col < kp && mu ? er[col] : T(0);
         }
       }
 #pragma unroll
@@ -461,7 +473,8 @@ template <typename T, int Q>
 __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skeys, int64_t E,
                                                int kp, T* __restrict__ stat,
                                                const T* __restrict__ headbuf,
-                                               const T* __restrict__ tailbuf, int64_t nchunks) {
+                                               const T* __restrict__ tailbuf, int64_t nchunks,
+                                               StatMap map) {
   // the run's owner (the chunk where it starts) adds the head partials of the chunks the run covers,
   // in chunk order; kG chunks are fetched at a time (keys and partials), so a run over hundreds of
   // chunks (the most frequent terms) costs hundreds / kG dependent round trips, not hundreds
@@ -476,6 +489,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
   const bool start_mid = p0 > 0 && skeys[p0 - 1] == first;
   const bool cont = p1 < E && skeys[p1] == last;
   if (!cont || (first == last && start_mid)) return;  // owner = chunk where the run starts
+  if (map.sub >= 0 && stat_sub(map, last) != map.sub) return;  // another sub-chunk launch's row
   T acc[Q];
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
@@ -512,33 +526,36 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     const int col = c0 + lane + 64 * q;
-    if (col < kp) stat[(int64_t)last * kp + col] = acc[q];
+    if (col < kp) stat[stat_row(map, last) * kp + col] = acc[q];
   }
 }
 
 template <typename T, int Q>
 static void sstats_q(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, int64_t E,
-                     const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf) {
+                     const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf, const StatMap& map) {
   const int64_t nchunks = ceil_div(E, kChunk);
   const dim3 grid((unsigned)ceil_div(nchunks, 4), (unsigned)ceil_div(kp, 64 * Q));
-  k_sstats<T, Q><<<grid, 256, 0, s>>>(skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, nchunks);
+  k_sstats<T, Q><<<grid, 256, 0, s>>>(skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, nchunks, map);
   KERNEL_CHECK();
-  k_fixup<T, Q><<<grid, 256, 0, s>>>(skeys, E, kp, stat, headbuf, tailbuf, nchunks);
+  k_fixup<T, Q><<<grid, 256, 0, s>>>(skeys, E, kp, stat, headbuf, tailbuf, nchunks, map);
   KERNEL_CHECK();
 }
 
 template <typename T>
 void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, int64_t E,
-                   const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf) {
+                   const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf, const StatMap& map) {
   if (E == 0) return;
   if (kp > 4096) throw Error(STC_ERR_INVALID_ARG, "k > 4096 topics is not supported");
+  if (map.sub >= 0 && (map.vs == 0 || map.vsj == 0 || map.nsub < 1 || map.sub >= map.nsub ||
+                       (uint64_t)(map.nsub - 1) * map.vsj >= map.vs))
+    throw Error(STC_ERR_INVALID_ARG, "sstats: bad sub-chunk map");
   // slab width: ≤ 4 (fp64) / 8 (fp32) columns per lane — the whole row when it is that narrow
   const int q = (kp + 63) / 64;
   constexpr int QMAX = sizeof(T) == 8 ? 4 : 8;
-  if (q <= 1) sstats_q<T, 1>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 2) sstats_q<T, 2>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
-  else if (q <= 4 || QMAX == 4) sstats_q<T, 4>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
-  else sstats_q<T, QMAX>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf);
+  if (q <= 1) sstats_q<T, 1>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, map);
+  else if (q <= 2) sstats_q<T, 2>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, map);
+  else if (q <= 4 || QMAX == 4) sstats_q<T, 4>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, map);
+  else sstats_q<T, QMAX>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, map);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1227,7 +1244,7 @@ void launch_unscale_stat(hipStream_t s, const T* stat, const double* logscale, c
   template int estep_lds_rows<T>(int, int, int);                                                  \
   template void launch_estep<T>(hipStream_t, const EStepArgs<T>&, bool, bool);                    \
   template void launch_sstats<T>(hipStream_t, const uint32_t*, const uint64_t*, int64_t, const T*, \
-                                 const T*, int, T*, T*, T*);                                      \
+                                 const T*, int, T*, T*, T*, const StatMap&);                      \
   template void launch_lambda_eeb<T>(hipStream_t, bool, double*, const T*, T*, double*, int64_t, int, \
                                      int, double, double, double, const double*, double*, int64_t);    \
   template void launch_logphat<T>(hipStream_t, const T*, const int32_t*, int64_t, int, double*, double*);  \

@@ -141,9 +141,36 @@ void launch_part_scatter(hipStream_t s, const int32_t* batch, const int64_t* nnz
                          const int32_t* short_flag, const int32_t* short_incl, int32_t* batch_p,
                          int32_t* orig_p, int64_t* nnz_p);
 
+// The multi-GPU stat layout for a reduce-scatter per vocabulary sub-chunk (api.hip train_tail): rank
+// r's slice [r·vs, (r+1)·vs) is cut into nsub sub-chunks of vsj rows (the last one the rest), and
+// sub-chunk j of every slice is stored together, in rank order, at physical rows [n·j·vsj, …) — so
+// sub-chunk j is ONE contiguous reduce-scatter of n pieces.  sub ≥ 0 restricts an sstats launch to the
+// terms of sub-chunk j (the entries, their sort order and the chunk grid are the whole launch's, so
+// every row's fp64 sum associates exactly as in the single launch); sub < 0: canonical rows, every term.
+struct StatMap {
+  uint32_t vs = 0, vsj = 0;
+  int n = 1, nsub = 1, sub = -1;
+};
+__host__ __device__ __forceinline__ int stat_sub(const StatMap& m, uint32_t v) {
+  const uint32_t j = (v % m.vs) / m.vsj;
+  return j < (uint32_t)(m.nsub - 1) ? (int)j : m.nsub - 1;
+}
+// (rank, sub-chunk) group of a term: the groups are contiguous term ranges, in term order
+__host__ __device__ __forceinline__ uint32_t stat_group(const StatMap& m, uint32_t v) {
+  return (v / m.vs) * (uint32_t)m.nsub + (uint32_t)stat_sub(m, v);
+}
+__host__ __device__ __forceinline__ int64_t stat_row(const StatMap& m, uint32_t v) {
+  if (m.sub < 0) return (int64_t)v;
+  const uint32_t r = v / m.vs, rem = v - r * m.vs;
+  const int j = stat_sub(m, v);
+  const int64_t w = j < m.nsub - 1 ? (int64_t)m.vsj : (int64_t)m.vs - (int64_t)(m.nsub - 1) * m.vsj;
+  return (int64_t)m.n * j * m.vsj + (int64_t)r * w + (rem - (int64_t)j * m.vsj);
+}
+
 template <typename T>
 void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, int64_t E,
-                   const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf);
+                   const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf,
+                   const StatMap& map = StatMap{});
 
 // the fused M-step pass (update = true: λ update; both: expElogβ' rows, logscale, colsum partials)
 template <typename T>

@@ -312,3 +312,38 @@ def test_group_transport_kinds(ctx, monkeypatch):
         assert g.transport() == "none"
     with stc.LdaGroup([0, 0], 8, 100) as g:
         assert g.transport() == "in-process"
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_chunked_reduce_scatter_is_bitwise_the_single_one(ctx, monkeypatch, dtype):
+    """The sharded step with the stat reduce-scatter split into vocabulary sub-chunks (api.hip
+    train_tail_split: one sstats launch per sub-chunk, each sub-chunk's reduce-scatter on the collective
+    stream under the next sstats launch, the M-step of sub-chunk j under the reduce-scatter of j+1)
+    against STC_RS_CHUNKS=1 (one reduce-scatter after the whole stat): λ, α, expElogβ'-dependent
+    topicDistribution and the step statistics bit-identical over sampled steps (next(): the draw-count
+    all-reduce rides on sub-chunk 0) and injected ones.  V = 5000 over 3 members: 27 blocks of 64 rows
+    per slice, cut 7+7+7+6 (STC_RS_CHUNKS=4) and 6+6+6+6+3 (=5)."""
+    import stc
+
+    rng = np.random.default_rng(31)
+    D, V, k = 400, 5000, 24
+    corpus = random_corpus(rng, D, V, 1, 120, empty_every=13)
+    ids = rng.integers(0, D, size=150)
+    g0 = rng.gamma(100.0, 0.01, size=(ids.size, k))
+    out = {}
+    for chunks in ("1", "4", "5"):
+        monkeypatch.setenv("STC_RS_CHUNKS", chunks)
+        with stc.LdaGroup([0, 0, 0], k, V, dtype=dtype, mini_batch_fraction=0.25, seed=8,
+                          optimize_doc_concentration=True) as g:
+            g.set_corpus(corpus)
+            g.init_random(3)
+            stats = [g.next() for _ in range(3)]
+            stats.append(g.step(ids, g0))
+            td = g.topic_distribution(corpus)
+            out[chunks] = (g.topics(), g.alpha(), td, stats)
+    ref = out["1"]
+    for chunks in ("4", "5"):
+        got = out[chunks]
+        for a, b in zip(got[:3], ref[:3]):
+            np.testing.assert_array_equal(a, b)
+        assert got[3] == ref[3]
