@@ -72,6 +72,11 @@ struct stc_lda {
   hipStream_t side = nullptr;
   hipEvent_t ev_fill = nullptr, ev_samp = nullptr;
   bool samp_pending = false;
+  // next(): the prefetched draw's batch (fill, slot order, offsets) is built on the side stream once the
+  // previous step's E-step has read the batch buffers (ev_est), under that step's M-step and all-gathers.
+  // prep_side: the last user of the batch buffers was next() (any other call's ensure_batch clears it).
+  hipEvent_t ev_est = nullptr;
+  bool prep_side = false;
   DevBuf side_scan_tmp;
   DevBuf long_list;  // rows / grid kernels: the launch's long documents (count word + slot offsets)
   DevBuf o_keys, o_keys2, o_idx, o_idx2, o_batch, o_orig, o_nnz, o_tmp;  // slot ordering (order_slots)
@@ -135,6 +140,7 @@ struct stc_lda {
     if (ev_pre) (void)hipEventDestroy(ev_pre);
     if (ev_fill) (void)hipEventDestroy(ev_fill);
     if (ev_samp) (void)hipEventDestroy(ev_samp);
+    if (ev_est) (void)hipEventDestroy(ev_est);
     if (side) (void)hipStreamDestroy(side);
     for (int j = 0; j < 16; ++j) {
       if (ev_ss[j]) (void)hipEventDestroy(ev_ss[j]);
@@ -369,7 +375,8 @@ void refresh(stc_lda& L) {
 }
 
 template <typename T>
-void ensure_batch(stc_lda& L, int64_t n, int64_t E) {
+void ensure_batch(stc_lda& L, int64_t n, int64_t E, bool from_next = false) {
+  if (!from_next) L.prep_side = false;
   const size_t ts = sizeof(T);
   L.batch_raw.reserve(4 * (n + 1));
   L.batch.reserve(4 * (n + 1));
@@ -413,9 +420,10 @@ void incl_scan(stc_lda& L, const X* in, X* out, int64_t n, hipStream_t s = nullp
 }
 
 // bptr[0] = 0, bptr[i+1] = Σ_{j<=i} nnz_p[j]  (entry offsets of the partitioned slots)
-void slot_offsets(stc_lda& L, int64_t n) {
-  HIP_CHECK(hipMemsetAsync(L.bptr.p, 0, sizeof(int64_t), L.ctx->stream));
-  incl_scan<int64_t>(L, L.nnzp.as<int64_t>(), L.bptr.as<int64_t>() + 1, n);
+void slot_offsets(stc_lda& L, int64_t n, hipStream_t s = nullptr, DevBuf* tmp = nullptr) {
+  if (!s) s = L.ctx->stream;
+  HIP_CHECK(hipMemsetAsync(L.bptr.p, 0, sizeof(int64_t), s));
+  incl_scan<int64_t>(L, L.nnzp.as<int64_t>(), L.bptr.as<int64_t>() + 1, n, s, tmp);
 }
 
 struct Part {
@@ -468,12 +476,12 @@ bool use_wide(int k, int dtype) { return dtype == STC_F32 ? lda::grid_row_cap(k)
 // launch does not end on a few long documents started late (longest-processing-time-first).  Each
 // slot keeps its member index (orig: γ₀ keys, outputs), so results only change in the summation
 // order of sstats within a term.
-void order_slots(stc_lda& L, int64_t n_short) {
+void order_slots(stc_lda& L, int64_t n_short, hipStream_t s = nullptr) {
   // measured: no gain at 50k docs per launch (≈ 100 documents per workgroup slot, the tail is
   // short), +0.13 ms of sorting; kept for small per-rank minibatches (strong scaling), where a
   // launch is only a few documents deep
   if (!L.sort_docs || n_short < 2 || n_short > 16384) return;
-  hipStream_t s = L.ctx->stream;
+  if (!s) s = L.ctx->stream;
   L.o_keys.reserve(8 * n_short);
   L.o_keys2.reserve(8 * n_short);
   L.o_idx.reserve(4 * n_short);
@@ -712,6 +720,7 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   a.nonempty = L.nonempty.as<int32_t>();
   record(L, 1);
   launch_split<T>(L, *L.corpus, a, n, n_short, true, false, n > 0 ? (double)E / (double)n : 0.0);
+  if (L.ev_est) HIP_CHECK(hipEventRecord(L.ev_est, s));  // the batch buffers are free (next_impl)
   record(L, 2);
   // logphat first: its all-reduce rides with the first stat sub-chunk of a sharded step
   if (n > 0) {
@@ -1029,7 +1038,11 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
   claim_event_set(L);
   record(L, 0);
   int64_t cnt[4];
-  if (L.pre_valid && L.pre_draw == draw) {
+  // the prefetched draw's batch is built on the side stream (behind its sampling, and behind the previous
+  // step's E-step — ev_est), under the previous step's M-step and all-gathers
+  const bool prefetched = L.pre_valid && L.pre_draw == draw;
+  const bool on_side = prefetched && L.prep_side && L.side && L.ev_est;
+  if (prefetched) {
     HIP_CHECK(hipEventSynchronize(L.ev_pre));
     std::copy(L.hpre, L.hpre + 4, cnt);
   } else {
@@ -1047,21 +1060,25 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
     if (st) *st = stc_step_stats{};
     return;
   }
-  ensure_batch<T>(L, n, E);
+  ensure_batch<T>(L, n, E, true);
+  const hipStream_t ps = on_side ? L.side : s;
+  if (on_side) HIP_CHECK(hipStreamWaitEvent(ps, L.ev_est, 0));
   if (n > 0)
-    lda::launch_fill_batch(s, L.corpus->indptr.as<int64_t>(), D, L.wave_cap, L.s_counts.as<int32_t>(),
+    lda::launch_fill_batch(ps, L.corpus->indptr.as<int64_t>(), D, L.wave_cap, L.s_counts.as<int32_t>(),
                            L.s_cincl.as<int32_t>(), L.s_sincl.as<int32_t>(), ns32, L.batch.as<int32_t>(),
                            L.orig.as<int32_t>(), L.nnzp.as<int64_t>());
-  order_slots(L, ns32);
-  slot_offsets(L, n);
+  order_slots(L, ns32, ps);
+  slot_offsets(L, n, ps, on_side ? &L.side_scan_tmp : &L.scan_tmp);
   // the next draw, on the side stream beside this step's E-step, counted with this step's collective
   if (!L.side) {
     HIP_CHECK(hipStreamCreateWithFlags(&L.side, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&L.ev_fill, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&L.ev_samp, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&L.ev_est, hipEventDisableTiming));
   }
-  HIP_CHECK(hipEventRecord(L.ev_fill, s));  // this draw's counts consumed (fill_batch, slot order)
-  HIP_CHECK(hipStreamWaitEvent(L.side, L.ev_fill, 0));
+  HIP_CHECK(hipEventRecord(L.ev_fill, ps));  // this draw's counts consumed and its batch built
+  if (on_side) HIP_CHECK(hipStreamWaitEvent(s, L.ev_fill, 0));
+  else HIP_CHECK(hipStreamWaitEvent(L.side, L.ev_fill, 0));
   sample_draw(L, draw + 1, L.side, &L.side_scan_tmp);
   HIP_CHECK(hipEventRecord(L.ev_samp, L.side));
   L.samp_pending = true;
@@ -1069,6 +1086,7 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
   L.pre_draw = draw + 1;
   estep_and_stats<T>(L, n, ns32, E, nullptr, L.iteration + 1, true);
   train_tail<T>(L, n, E, st);
+  L.prep_side = true;
 }
 
 template <typename T>
