@@ -66,6 +66,7 @@ struct stc_lda {
   DevBuf batch_raw, batch, orig, flags, sincl, bptr, bnnz, nnzp, g0, gamma, eth, elogth, iters,
       nonempty, r, keys, vals, skeys, svals, stat, headbuf, tailbuf, sort_tmp, scan_tmp,
       stats4, cum2, bound, dtmp, lpart;
+  DevBuf g0gen;  // γ₀ drawn ahead of the E-step (lda::launch_gamma0) when the caller injects none
   DevBuf s_counts, s_weights, s_short, s_cincl, s_wincl, s_sincl;
   // the next draw is sampled on a side stream, concurrently with this step's E-step (it reads only
   // indptr and writes only the s_* buffers, which this step's fill_batch has consumed)
@@ -692,6 +693,18 @@ std::pair<int64_t, int64_t> stat_sub_rows(const lda::StatMap& m, int j) {
   return {(int64_t)j * m.vsj, w};
 }
 
+// γ₀ of the n partitioned slots' members from the counter RNG, keyed as the E-step kernels key it
+// (key_mode 0: train_doc_key(iteration, rank, member); 1: doc_id_base + row), into L.g0gen
+template <typename T>
+const T* gen_gamma0(stc_lda& L, hipStream_t s, int64_t n, uint64_t seed, int64_t iteration, int key_mode,
+                    int64_t base) {
+  if (n == 0) return nullptr;
+  L.g0gen.reserve(sizeof(T) * n * L.k);
+  lda::launch_gamma0<T>(s, L.batch.as<int32_t>(), L.orig.as<int32_t>(), n, L.k, seed, iteration, L.ctx->rank,
+                        key_mode, base, L.cfg.gamma_shape, L.g0gen.as<T>());
+  return L.g0gen.as<T>();
+}
+
 // E-step over the n partitioned slots (L.batch / L.orig / L.bptr), then logphat / non-empty count into
 // L.small and the term-sorted sstats SpMM into L.stat (V×kp, row-scaled).  split: a training step of a
 // sharded handle — stat in the sub-chunk layout, one sstats launch per sub-chunk (ev_ss[j] after each).
@@ -972,6 +985,7 @@ void step_ids(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, s
   const Part p = upload_members<T>(L, ids, n);
   if (L.timing) harvest_all(L);  // partition() drained the stream
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
+  if (!g0) g0 = gen_gamma0<T>(L, L.ctx->stream, n, L.cfg.seed, L.iteration + 1, 0, 0);
   estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1, true);
   train_tail<T>(L, n, p.E, st);
 }
@@ -1069,6 +1083,7 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
                            L.orig.as<int32_t>(), L.nnzp.as<int64_t>());
   order_slots(L, ns32, ps);
   slot_offsets(L, n, ps, on_side ? &L.side_scan_tmp : &L.scan_tmp);
+  const T* g0 = gen_gamma0<T>(L, ps, n, L.cfg.seed, L.iteration + 1, 0, 0);
   // the next draw, on the side stream beside this step's E-step, counted with this step's collective
   if (!L.side) {
     HIP_CHECK(hipStreamCreateWithFlags(&L.side, hipStreamNonBlocking));
@@ -1084,7 +1099,7 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
   L.samp_pending = true;
   L.pre_inflight = true;
   L.pre_draw = draw + 1;
-  estep_and_stats<T>(L, n, ns32, E, nullptr, L.iteration + 1, true);
+  estep_and_stats<T>(L, n, ns32, E, g0, L.iteration + 1, true);
   train_tail<T>(L, n, E, st);
   L.prep_side = true;
 }
@@ -1098,6 +1113,7 @@ void estep_only(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0,
   hipStream_t s = L.ctx->stream;
   const Part p = upload_members<T>(L, ids, n);
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
+  if (!g0) g0 = gen_gamma0<T>(L, s, n, L.cfg.seed, L.iteration + 1, 0, 0);
   const bool t = L.timing;
   L.timing = false;
   estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1);
@@ -1134,6 +1150,7 @@ void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const
   L.scal.reserve(sizeof(double) * 8);
   const Part p = partition(L, docs.indptr.as<int64_t>(), nullptr, n);
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
+  if (!g0) g0 = gen_gamma0<T>(L, s, n, seed, 0, 1, base);
   lda::EStepArgs<T> a = estep_args<T>(L);
   a.indptr = docs.indptr.as<int64_t>();
   a.indices = docs.indices.as<int32_t>();

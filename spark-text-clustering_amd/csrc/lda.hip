@@ -1239,7 +1239,36 @@ void launch_unscale_stat(hipStream_t s, const T* stat, const double* logscale, c
   KERNEL_CHECK();
 }
 
+// γ₀ of a launch's members ahead of the E-step: one thread per (slot, topic), the counter RNG each
+// E-step kernel would otherwise run in its prologue (the same gamma_sample, key and stream), written
+// member-major for EStepArgs::gamma0.  The E-step prologues are latency-bound per document and the team
+// kernels drew every topic of the document in every member; here the draws fill the chip.
+template <typename T>
+__global__ __launch_bounds__(256) void k_gamma0(const int32_t* __restrict__ batch, const int32_t* __restrict__ orig,
+                                                int64_t n, int k, uint64_t seed, int64_t iteration, int rank,
+                                                int key_mode, int64_t doc_id_base, double shape, T* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * k) return;
+  const int64_t slot = i / k;
+  const int t = (int)(i - slot * k);
+  const int64_t mem = orig ? (int64_t)orig[slot] : slot;
+  const int64_t row = batch ? (int64_t)batch[slot] : slot;
+  const uint64_t key = key_mode == 0 ? train_doc_key(iteration, rank, mem) : (uint64_t)(doc_id_base + row);
+  out[mem * k + t] = (T)gamma_sample(doc_stream(seed, key), t, shape);
+}
+
+template <typename T>
+void launch_gamma0(hipStream_t s, const int32_t* batch, const int32_t* orig, int64_t n, int k, uint64_t seed,
+                   int64_t iteration, int rank, int key_mode, int64_t doc_id_base, double shape, T* out) {
+  if (n <= 0) return;
+  k_gamma0<T><<<(unsigned)ceil_div(n * k, (int64_t)256), 256, 0, s>>>(batch, orig, n, k, seed, iteration, rank,
+                                                                      key_mode, doc_id_base, shape, out);
+  KERNEL_CHECK();
+}
+
 #define STC_INSTANTIATE(T)                                                                        \
+  template void launch_gamma0<T>(hipStream_t, const int32_t*, const int32_t*, int64_t, int, uint64_t, int64_t, \
+                                 int, int, int64_t, double, T*);                                  \
   template size_t estep_lds_bytes<T>(int, int, int);                                              \
   template int estep_lds_rows<T>(int, int, int);                                                  \
   template void launch_estep<T>(hipStream_t, const EStepArgs<T>&, bool, bool);                    \

@@ -172,6 +172,11 @@ void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, 
                    const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf,
                    const StatMap& map = StatMap{});
 
+// γ₀ of n slots' members (gamma_sample, keyed as the E-step kernels key it) into out[member·k + t]
+template <typename T>
+void launch_gamma0(hipStream_t s, const int32_t* batch, const int32_t* orig, int64_t n, int k, uint64_t seed,
+                   int64_t iteration, int rank, int key_mode, int64_t doc_id_base, double shape, T* out);
+
 // the fused M-step pass (update = true: λ update; both: expElogβ' rows, logscale, colsum partials)
 template <typename T>
 void launch_lambda_eeb(hipStream_t s, bool update, double* lam, const T* stat, T* Bp, double* logscale,

@@ -165,11 +165,8 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
   const int64_t qe = d.wv ? d.s0 + qn : 0;
   d.qid = d.wv ? a.indices[qe] : 0;
   d.qc = d.wv ? a.values[qe] : 0.0;
-  d.qls = a.logscale[d.qid];
-  // ε'_q = 1e-100·e^{-m_v} held as 2^53·ε' (the test 2^53·ε' ≥ φ is then direct), capped at 1e300
-  // where e^{-m_v} overflows (Spark's unscaled row is 0 there; r ≈ cts·1e-284 reproduces that).
-  // Padding rows hold −2^53 (φ = −1, r = −0, never live).
-  d.qe2 = d.wv ? fmin(0x1p53 * exp(kLogEps - d.qls), 1e300) : -0x1p53;
+  // (m_v = logscale[id] and ε' are loaded in rows64_iterate beside the block's B rows: a third dependent
+  // round trip here would sit on the prologue's chain)
 
   // ---- γ₀ / α partials (the first npsi waves hold the topics), Σcts, eθ pads, α and ψc to LDS
   double g0 = 0.0;
@@ -242,7 +239,7 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
 // the document block (R row sets) and the fixed point; returns the iteration count, the worker's φ
 // (without ε') in qdt; the final r sits in sm.rrow
 template <class S, int R>
-__device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S>& sm, const RDoc& d, double& qdt) {
+__device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S>& sm, RDoc& d, double& qdt) {
   constexpr int KL = S::KL, KLP = S::KLP;
   constexpr int RG = R < S::RREG ? R : S::RREG;  // row sets in VGPRs; [RG, R) in sm.ovf
   static_assert(R >= 1 && R <= S::RMAX && R - RG <= S::NOVF, "row sets");
@@ -254,7 +251,9 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
   const int k = a.k, kp = a.kp, nnz = d.nnz, npsi = d.npsi, pw = d.pw, tt = d.tt, ttl = d.ttl, ttp = d.ttp;
   const bool town = d.town;
   const int qid = d.qid;
-  const double qc = d.qc, qe2 = d.qe2;
+  const double qc = d.qc;
+  // the worker row's m_v, issued before the B gather so the two round trips overlap
+  d.qls = a.logscale[qid];
   // mirror mode (k > 64): the waves w and w ^ 2 share a topic set and take turns as its ψ wave and as
   // its Σ|Δγ| wave; each keeps γ / eθ of its lane's topic as it last computed them (read once below)
   const bool mir = R64_MIRROR && npsi == 2;
@@ -314,6 +313,11 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
     }
   }
 
+  // ε'_q = 1e-100·e^{-m_v} held as 2^53·ε' (the test 2^53·ε' ≥ φ is then direct), capped at 1e300
+  // where e^{-m_v} overflows (Spark's unscaled row is 0 there; r ≈ cts·1e-284 reproduces that).
+  // Padding rows hold −2^53 (φ = −1, r = −0, never live).
+  const double qe2 = d.wv ? fmin(0x1p53 * exp(kLogEps - d.qls), 1e300) : -0x1p53;
+  d.qe2 = qe2;
   __syncthreads();  // the staging area is the loop's partial arrays; (also publishes the first eθ)
   if (mir && town) {  // γ₀ / eθ₀ of the lane's topic (no ψ phase has overwritten them before barrier 1)
     gm = sm.gam[tt];

@@ -63,7 +63,7 @@ r_configs() {
 r_cab() {  # r_cab CONFIG
   local B="python bench.py --config $1 --steps ${STEPS:-6} --warmup ${WARMUP:-2} $FAST"
   for n in $LIBS; do step c$1_$n 500 env STC_LIB=$(lib $n) $B; done
-  step c$1_base 500 $B
+  step c$1_new 500 $B
 }
 r_feat() {
   step feat 300 python bench.py --featurisation-only --steps 5
