@@ -38,6 +38,12 @@
 #ifndef R64_PSI_V2
 #define R64_PSI_V2 1  // the ψ phase's chain: psi64.h exp_digamma_minus_v2 (0: the round-3 form)
 #endif
+#ifndef R64_PSI_V3
+#define R64_PSI_V3 0  // the v2 chain with its constants read from an LDS table (psi64.h exp_digamma_minus_v3)
+#endif
+#ifndef R64_PSI_V4
+#define R64_PSI_V4 1  // the v2 chain with its exp() constants in VGPRs across the fixed point (exp_digamma_minus_v4)
+#endif
 #ifndef R64_RCP_NR
 #define R64_RCP_NR 2  // Newton steps after v_rcp_f64 in that chain
 #endif
@@ -78,10 +84,14 @@ using RCommon = RShape<KL, 5, kOnChipSets>;
 template <int KL>
 using RLong = RShape<KL, kMaxSets, kMaxSets>;
 
-__device__ __forceinline__ double exp_digamma_minus_r64(double x, double cst) {
-#if R64_PSI_V2
+__device__ __forceinline__ double exp_digamma_minus_r64(double x, double cst, const PsiK& tab) {
+#if R64_PSI_V3
+  return exp_digamma_minus_v3<R64_RCP_NR>(x, cst, tab);
+#elif R64_PSI_V2
+  (void)tab;
   return exp_digamma_minus_v2<R64_RCP_NR>(x, cst);
 #else
+  (void)tab;
   return exp_digamma_minus_s(x, cst);
 #endif
 }
@@ -98,6 +108,7 @@ struct RLds {
   double cs;                       // ψ(Σγ') of the current eθ (the bound's scale)
   double apc[S::KT][2] __attribute__((aligned(16)));  // α_t, ψc_t of the ψ lanes' topics (not in VGPRs)
   double ac[4] __attribute__((aligned(16)));  // Σα, Σcts, ψ(Σα + Σcts) (the flat ψ(Σγ'))
+  PsiK psik;                       // the ψ/exp chain's constants (R64_PSI_V3)
   union {
     struct {
       double pa[kW][8 * S::RMAX][kPaPitch];  // φ partials (wave, wave row, topic lane)
@@ -192,6 +203,9 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
     if (d.tval) sm.gam[tt] = g0;
   }
   for (int i = tid; i < 8 * KLP; i += 64 * kW) (&sm.eth[0][0])[i] = 0.0;
+#if R64_PSI_V3 || R64_PSI_V4
+  psik_fill(sm.psik, tid, 64 * kW);  // (published by the barrier below)
+#endif
   {
     const double gs = wave_sum_d(g0), as = wave_sum_d(alp), cts = wave_sum_d(d.qc);
     if (lane == 0) {
@@ -230,7 +244,7 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
   // eθ' = exp(ψ(γ) − ψ(Σγ) − ψc_t): Spark's exp(E[log θ]) times expElogβ's per-topic factor
   {
     const double cs0 = digamma_fast_d(gsum0);
-    if (w < npsi && d.town) sm.eth[d.ttl][d.ttp] = exp_digamma_minus_r64(g0, cs0 + pc);
+    if (w < npsi && d.town) sm.eth[d.ttl][d.ttp] = exp_digamma_minus_r64(g0, cs0 + pc, sm.psik);
     if (tid == 0) sm.cs = cs0;
   }
   return true;  // (the block loads' barrier publishes eθ)
@@ -326,6 +340,9 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
 
   double* const pa = &sm.u.l.pa[w][0][0];
   double* const sb = &sm.u.l.sb[0][0];
+#if R64_PSI_V4
+  const PsiExpK expk = psi_expk_load(sm.psik);
+#endif
   double rr[R];
   double qr = 0.0;  // worker: r of its row (φ without ε' in qdt)
   qdt = 0.0;
@@ -444,7 +461,11 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
         const double gn = fma(eo, s, ap.x);  // γ ← eθ ⊙ s + α
         dg = fabs(gn - g);
         sm.gam[tt] = gn;
-        const double en = exp_digamma_minus_r64(gn, csn + ap.y);
+#if R64_PSI_V4
+        const double en = exp_digamma_minus_v4<R64_RCP_NR>(gn, csn + ap.y, expk);
+#else
+        const double en = exp_digamma_minus_r64(gn, csn + ap.y, sm.psik);
+#endif
         sm.eth[ttl][ttp] = en;
         gm = gn;
         em = en;
