@@ -4,6 +4,10 @@
 
 #include "estep_common.h"
 
+#ifndef PSI_V4_SERIES
+#define PSI_V4_SERIES 0  // 1: v4 also holds Breeze's series coefficients in VGPRs (12 more VGPRs; measured 30.10 vs 29.97 ms headline, so off)
+#endif
+
 namespace stc {
 namespace lda {
 namespace psi64 {
@@ -293,6 +297,9 @@ __device__ __forceinline__ double exp_digamma_minus_v3(double x, double cst, con
 // to v2 (same instructions, operands from VGPRs).
 struct PsiExpK {
   double log2e, ln2hi, ln2lo, e0, e1, e2, e3, e4, o0, o1, o2, o3, o5, o4;  // o5 = 1/5!
+#if PSI_V4_SERIES
+  double s0, s1, s2, s3, s4, s5;  // Breeze's series: 3617/8160, −1/12, 691/32760, −1/132, 1/240, −1/252 (1/120 = o5)
+#endif
 };
 __device__ __forceinline__ PsiExpK psi_expk_load(const PsiK& T) {
   const double* K = T.k;
@@ -300,6 +307,15 @@ __device__ __forceinline__ PsiExpK psi_expk_load(const PsiK& T) {
             K[PK_O0],    K[PK_O1],    K[PK_O2],    K[PK_O3], K[PK_S6], K[PK_O4]};
   asm volatile("" : "+v"(c.log2e), "+v"(c.ln2hi), "+v"(c.ln2lo), "+v"(c.e0), "+v"(c.e1), "+v"(c.e2), "+v"(c.e3));
   asm volatile("" : "+v"(c.e4), "+v"(c.o0), "+v"(c.o1), "+v"(c.o2), "+v"(c.o3), "+v"(c.o5), "+v"(c.o4));
+#if PSI_V4_SERIES
+  c.s0 = K[PK_S0];
+  c.s1 = K[PK_S1];
+  c.s2 = K[PK_S2];
+  c.s3 = K[PK_S3];
+  c.s4 = K[PK_S4];
+  c.s5 = K[PK_S5];
+  asm volatile("" : "+v"(c.s0), "+v"(c.s1), "+v"(c.s2), "+v"(c.s3), "+v"(c.s4), "+v"(c.s5));
+#endif
   return c;
 }
 __device__ __forceinline__ double exp_vk(double z, const PsiExpK& C) {
@@ -322,6 +338,18 @@ __device__ __forceinline__ double exp_vk(double z, const PsiExpK& C) {
   o = __builtin_fma(o, r2, 1.0);
   return __builtin_ldexp(__builtin_fma(r, o, e), (int)fmax(n, -1100.0));  // n < -1100: 0
 }
+#if PSI_V4_SERIES
+__device__ __forceinline__ double series_vk(double f, const PsiExpK& C) {
+#pragma clang fp contract(off)
+  double t = f * C.s0 + C.s1;
+  t = __builtin_fma(t, f, C.s2);
+  t = __builtin_fma(t, f, C.s3);
+  t = __builtin_fma(t, f, C.s4);
+  t = __builtin_fma(t, f, C.s5);
+  t = __builtin_fma(t, f, C.o5);
+  return __builtin_fma(t, f, C.s1) * f;
+}
+#endif
 template <int RCP_STEPS>
 __device__ __forceinline__ double exp_digamma_minus_v4(double x, double cst, const PsiExpK& C) {
   const bool sh = x <= 5.0;
@@ -335,6 +363,9 @@ __device__ __forceinline__ double exp_digamma_minus_v4(double x, double cst, con
   const double y = sh ? add_s(x, 6.0) : x;
   const double iy = rcp_n<RCP_STEPS>(y);
   const double f = iy * iy;
+#if PSI_V4_SERIES
+  const double t = series_vk(f, C);
+#else
   double t = add_s(mul_s(f, 3617.0 / 8160.0), -1.0 / 12.0);
   t = fma_s(t, f, 691.0 / 32760.0);
   t = fma_s(t, f, -1.0 / 132.0);
@@ -342,6 +373,7 @@ __device__ __forceinline__ double exp_digamma_minus_v4(double x, double cst, con
   t = fma_s(t, f, -1.0 / 252.0);
   t = fma_s(t, f, 1.0 / 120.0);
   t = fma_s(t, f, -1.0 / 12.0) * f;
+#endif
   const double shift = sh ? trunc_fix_pk(f, xs) - c : 0.0;
   const double z = (fma(-0.5, iy, shift) + t) - cst;
   return y * exp_vk(z, C);
