@@ -54,6 +54,9 @@
 #ifndef R64_SB_RS
 #define R64_SB_RS 1  // Phase B's s partials reduce-scattered over the wave's row lanes (4 per topic, not 32)
 #endif
+#ifndef R64_PERSIST
+#define R64_PERSIST 1  // the common documents on a resident grid taking tickets (1) or one workgroup per slot (0)
+#endif
 #ifndef R64_LONG_OCC
 #define R64_LONG_OCC 1  // long-document kernel workgroups per CU the register budget is cut for
 #endif
@@ -602,10 +605,11 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
 }
 
 // one document (slot, row, member and extent set by the caller): open → iterate<R> → close
-template <class S, bool STATS, bool BOUND, bool LONG>
+// LONG: the 7–8-row-set documents; RES: a resident kernel (d.tid laundered per document)
+template <class S, bool STATS, bool BOUND, bool LONG, bool RES = LONG>
 __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& sm, RDoc& d) {
   d.e0 = a.bptr ? a.bptr[d.slot] : d.s0;
-  if (!rows64_open<S, STATS, BOUND, LONG>(a, sm, d)) return;
+  if (!rows64_open<S, STATS, BOUND, RES>(a, sm, d)) return;
   double qdt = 0.0;
   int it;
   if constexpr (LONG) {
@@ -620,7 +624,7 @@ __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& 
       default: it = rows64_iterate<S, 6>(a, sm, d, qdt); break;
     }
   }
-  rows64_close<S, STATS, BOUND, LONG>(a, sm, d, it, qdt);
+  rows64_close<S, STATS, BOUND, RES>(a, sm, d, it, qdt);
 }
 
 // the documents with ≤ kOnChipSets row sets: one workgroup per slot (the long documents exit at once)
@@ -640,6 +644,41 @@ __global__ __launch_bounds__(64 * kW, 2) void k_estep_rows64(EStepArgs<double> a
   d.rsets = (d.nnz + 31) >> 5;
   if (d.rsets > kOnChipSets) return;  // the long-document kernel's
   rows64_doc<S, STATS, BOUND, false>(a, sm, d);
+}
+
+// The same documents on a resident grid (R64_PERSIST): every workgroup takes the next slot from a ticket
+// counter and walks until the tickets run out (no dependency between workgroups: any residency drains).
+// A workgroup per slot paid a dispatch and its own prologue start per document; here the next ticket is
+// requested at the start of a document and read at its end, and the per-document lane maps are laundered
+// (as in the long-document kernel) so they are not hoisted and held across the fixed point.
+template <class S, bool STATS, bool BOUND>
+__global__ __launch_bounds__(64 * kW, 2) void k_estep_rows64_pers(EStepArgs<double> a, int32_t* ticket) {
+  __shared__ RLds<S> sm;
+  __shared__ int s_tk;
+  if (threadIdx.x == 0) s_tk = atomicAdd(ticket, 1);
+  __syncthreads();
+  int cur = s_tk;
+  while (cur < a.n) {
+    __syncthreads();  // every thread has read s_tk
+    int nxt = 0;
+    if (threadIdx.x == 0) nxt = atomicAdd(ticket, 1);  // the next document's ticket, stored after this one
+    RDoc d;
+#ifdef STC_STAMP
+    d.st0 = stamp_now();
+#endif
+    d.tid = threadIdx.x;
+    asm volatile("" : "+v"(d.tid));
+    d.slot = a.slot0 + cur;
+    d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
+    d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
+    d.s0 = a.indptr[d.row];
+    d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
+    d.rsets = (d.nnz + 31) >> 5;
+    if (d.rsets <= kOnChipSets) rows64_doc<S, STATS, BOUND, false, true>(a, sm, d);
+    if (threadIdx.x == 0) s_tk = nxt;
+    __syncthreads();  // LDS is the next document's; s_tk published
+    cur = s_tk;
+  }
 }
 
 // the launch's 7–8-set documents into a.long_list: word 0 the count, then their slot offsets (in any
@@ -680,7 +719,29 @@ __global__ __launch_bounds__(64 * kW, R64_LONG_OCC) void k_estep_rows64_long(ESt
 }
 
 template <class S>
+bool launch_persist(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound) {
+  if (!R64_PERSIST || !a.long_list) return false;
+  int32_t* ticket = a.long_list + a.n + 1;  // the word past the long-document list (api.hip reserves it)
+  auto go = [&](const void* kern) {
+    int dev = 0, cus = 0, per_cu = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kW, 0));
+    if (per_cu < 1) return false;
+    HIP_CHECK(hipMemsetAsync(ticket, 0, sizeof(int32_t), s));
+    EStepArgs<double> aa = a;
+    void* args[] = {&aa, &ticket};
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(a.n, (int64_t)per_cu * cus));
+    HIP_CHECK(hipLaunchKernel(kern, dim3((unsigned)blocks), dim3(64 * kW), args, 0, s));
+    return true;
+  };
+  if (stats) return go((const void*)k_estep_rows64_pers<S, true, false>);
+  if (bound) return go((const void*)k_estep_rows64_pers<S, false, true>);
+  return go((const void*)k_estep_rows64_pers<S, false, false>);
+}
+template <class S>
 void launch_common(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound) {
+  if (launch_persist<S>(s, a, stats, bound)) return;
   const dim3 grid((unsigned)a.n);
   const int threads = 64 * kW;
   if (stats) k_estep_rows64<S, true, false><<<grid, threads, 0, s>>>(a);
