@@ -636,10 +636,9 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
     } else if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
     else if constexpr (std::is_same<T, float>::value) {
       const bool long_docs = m.max_row < 0 || m.max_row > lda::grid_onchip_rows(L.k);
-      if (long_docs) {
-        L.long_list.reserve(4 * (size_t)(n_short + 1));
-        w.long_list = L.long_list.as<int32_t>();
-      }
+      // the long-document list (count word + slots) and, past it, the resident grid's ticket word
+      L.long_list.reserve(4 * (size_t)(n_short + 2));
+      w.long_list = L.long_list.as<int32_t>();
       lda::launch_estep_grid(s, w, stats, bound, long_docs);
     } else {
       const bool long_docs = m.max_row < 0 || m.max_row > lda::rows64_onchip_rows(L.k);

@@ -489,6 +489,28 @@ __global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_grid(EStepArgs<floa
   grid_doc<S, STATS, BOUND, SKIPLONG>(a, sm, a.slot0 + blockIdx.x, (int)threadIdx.x);
 }
 
+// the same on a resident grid taking tickets (as lda_rows64.hip k_estep_rows64_pers): the next ticket is
+// requested at a document's start and read at its end; tid laundered per document
+template <class S, bool STATS, bool BOUND, bool SKIPLONG>
+__global__ __launch_bounds__(64 * S::W, S::OCC) void k_estep_grid_pers(EStepArgs<float> a, int32_t* ticket) {
+  __shared__ GLds<S> sm;
+  __shared__ int s_tk;
+  if (threadIdx.x == 0) s_tk = atomicAdd(ticket, 1);
+  __syncthreads();
+  int cur = s_tk;
+  while (cur < a.n) {
+    __syncthreads();  // every thread has read s_tk
+    int nxt = 0;
+    if (threadIdx.x == 0) nxt = atomicAdd(ticket, 1);
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    grid_doc<S, STATS, BOUND, SKIPLONG>(a, sm, a.slot0 + cur, tid);
+    if (threadIdx.x == 0) s_tk = nxt;
+    __syncthreads();  // LDS is the next document's; s_tk published
+    cur = s_tk;
+  }
+}
+
 // the launch's documents past `rows` rows into a.long_list (word 0 the count, then slot offsets)
 __global__ void k_grid_long_list(EStepArgs<float> a, int rows) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -521,8 +543,32 @@ size_t lds_pad() {
   return v;
 }
 
+#ifndef GRID_PERSIST
+#define GRID_PERSIST 1  // the documents on a resident grid taking tickets (1) or one workgroup per slot (0)
+#endif
+template <class S, bool SKIPLONG>
+bool launch_g_persist(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound) {
+  if (!GRID_PERSIST || !a.long_list || lds_pad() != 0 || bound) return false;  // (the bound kernels spill resident)
+  int32_t* ticket = a.long_list + a.n + 1;  // the word past the long-document list (api.hip reserves it)
+  auto go = [&](const void* kern) {
+    int dev = 0, cus = 0, per_cu = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * S::W, 0));
+    if (per_cu < 1) return false;
+    HIP_CHECK(hipMemsetAsync(ticket, 0, sizeof(int32_t), s));
+    EStepArgs<float> aa = a;
+    void* args[] = {&aa, &ticket};
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(a.n, (int64_t)per_cu * cus));
+    HIP_CHECK(hipLaunchKernel(kern, dim3((unsigned)blocks), dim3(64 * S::W), args, 0, s));
+    return true;
+  };
+  if (stats) return go((const void*)k_estep_grid_pers<S, true, false, SKIPLONG>);
+  return go((const void*)k_estep_grid_pers<S, false, false, SKIPLONG>);
+}
 template <class S, bool SKIPLONG = false>
 void launch_g(hipStream_t s, const EStepArgs<float>& a, bool stats, bool bound) {
+  if (launch_g_persist<S, SKIPLONG>(s, a, stats, bound)) return;
   const dim3 grid((unsigned)a.n);
   const int threads = 64 * S::W;
   const size_t pad = lds_pad();
