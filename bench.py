@@ -474,9 +474,10 @@ def kernel_name(dtype, k):
         return ("k_estep_wide / k_estep_wide_mc (lda_wide.hip): the many-topic training E-step (k <= 512: a "
                 "team of CUs per document), one launch per minibatch")
     if dtype == "f64":
-        return ("k_estep_rows64 (lda_rows64.hip): the fp64 training E-step, one launch per minibatch (plus "
-                "the 7-8-row-set launch when a document has > 192 rows)")
-    return "k_estep_grid (lda_grid.hip): the fp32 training E-step, one launch per minibatch"
+        return ("k_estep_rows64_pers (lda_rows64.hip): the fp64 training E-step, one launch per minibatch on a "
+                "resident grid taking document tickets (plus the 7-8-row-set launch when a document has > 192 rows)")
+    return ("k_estep_grid_pers (lda_grid.hip): the fp32 training E-step, one launch per minibatch on a resident "
+            "grid taking document tickets")
 
 
 def launch_mode(gpus, env, force_group=False):

@@ -16,6 +16,8 @@ import pmc_summary as P  # noqa: E402
 TRAINING = [
     "k_estep_rows64<RShape<13, 5, 6>, true, false>",
     "k_estep_rows64_long<RShape<13, 8, 8>, true, false>",
+    "k_estep_rows64_pers<RShape<13, 5, 6>, true, false>",
+    "k_estep_grid_pers<GShape<2, 26, 6, 2>, true, false, false>",
     "k_estep_grid<GShape<2, 26, 6, 2>, true, false, true>",
     "k_estep_grid<GShape<2, 26, 6, 2>, true, false, false>",
     "k_estep_grid_long<GShape<2, 26, 8, 1>, true, false>",
@@ -28,6 +30,7 @@ TRAINING = [
 ]
 NOT_TRAINING = [
     "k_estep_rows64<RShape<13, 5, 6>, false, true>",   # the bound's E-step
+    "k_estep_rows64_pers<RShape<13, 5, 6>, false, false>",  # inference on the resident grid
     "k_estep_grid<GShape<2, 26, 6, 2>, false, false, true>",  # inference
     "k_estep_wide_mc<double, 1, 64, false>",
     "k_estep_tgrid64<13, false>",

@@ -38,10 +38,10 @@ WINDOW = re.compile(r"k_estep|k_rows64_long_list|k_sstats|k_fixup|k_logphat|k_it
 # minibatch — the grid kernel plus the workgroup kernel for the few docs past its row capacity, the
 # same launches the bench's HIP-event "estep" phase brackets
 # (STATS = true, BOUND = false): k_estep / k_estep_grid / k_estep_wave / k_estep_wide <..., true, false>;
-# k_estep_grid64 / k_estep_rows64 <shape, true, false, LONG>; k_estep_wide_mc / _tc <T, Q, NR, true>
+# k_estep_grid64 / k_estep_rows64[_long|_pers] / k_estep_grid[_long|_pers] <shape, true, false, LONG>; k_estep_wide_mc / _tc <T, Q, NR, true>
 ESTEP = re.compile(r"k_estep_grid64<DShape<[^>]*>, true, false, (true|false)>$"  # round-2 profiles
-                   r"|k_estep_rows64(_long)?<RShape<[^>]*>, true, false(, (true|false))?>$"
-                   r"|k_estep_grid(_long)?<GShape<[^>]*>, true, false(, (true|false))?>$"
+                   r"|k_estep_rows64(_long|_pers)?<RShape<[^>]*>, true, false(, (true|false))?>$"
+                   r"|k_estep_grid(_long|_pers)?<GShape<[^>]*>, true, false(, (true|false))?>$"
                    r"|k_estep_wide_(mc|tc)<\w+, \d+, \d+, true>$"
                    r"|k_estep_tgrid64<\d+, true>$"
                    r"|k_estep(_wave|_wide)?<(?!DShape|RShape|GShape).*, true, false>$")
