@@ -57,6 +57,11 @@
 #ifndef R64_PERSIST
 #define R64_PERSIST 1  // the common documents on a resident grid taking tickets (1) or one workgroup per slot (0)
 #endif
+#ifndef R64_PREFETCH
+#define R64_PREFETCH 0  // 1: the resident grid fetches the next document's identity and entries to LDS (LDS-DMA)
+                        // during this one — correct, but measured slower (headline 27.8 vs 27.0 ms, planted
+                        // 4.40 vs 4.36 ms: wave 0's DMA steps and drains, 256 VGPRs)
+#endif
 #ifndef R64_LONG_OCC
 #define R64_LONG_OCC 1  // long-document kernel workgroups per CU the register budget is cut for
 #endif
@@ -120,6 +125,15 @@ struct RLds {
     double stage[kW][8][S::KT + 2];          // load phase: eight B rows per wave at a time
   } u __attribute__((aligned(16)));
   double ovf[S::NOVF > 0 ? S::NOVF * kW * S::KL * 64 : 1];  // row sets past RREG ([set][w][p][lane])
+  // resident grid (R64_PREFETCH): the next document's row / member / entry offset, its CSR extent and its
+  // ≤ 192 (term id, count) pairs, loaded by LDS-DMA in the idle waits of this document's fixed point
+  struct {
+    double vals[32 * kOnChipSets];
+    int32_t ids[32 * kOnChipSets];
+    int32_t rme[4];   // batch[slot], orig[slot], bptr[slot] (two words)
+    int32_t ext[4];   // indptr[row], indptr[row + 1] (two words each)
+    int32_t slot, valid;
+  } pf __attribute__((aligned(16)));
 };
 
 // Per-lane document context: set up once per document by rows64_open, outside the row-set
@@ -132,6 +146,10 @@ struct RLds {
 struct RDoc {
   int64_t slot, row, mem, s0, e0;
   int nnz, rsets;
+  int nxt;                           // resident grid: the next ticket (valid in thread 0)
+  int pfs;                           // prefetch steps issued during this document (wave 0)
+  bool pfon;                         // resident grid with batch / orig / bptr: prefetch the next document
+  bool pfv;                          // this document's identity and entries came from the prefetch
   int tid;                           // the resident long kernel's threadIdx.x, laundered per document
   int lane, w, tl, rl;
   int npsi, half, pw, tt, ttl, ttp;  // ψ-lane topic map
@@ -177,8 +195,13 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
   const int qn = 32 * (lane >> 3) + 8 * w + (lane & 7);
   d.wv = lane < 8 * d.rsets && qn < d.nnz;
   const int64_t qe = d.wv ? d.s0 + qn : 0;
-  d.qid = d.wv ? a.indices[qe] : 0;
-  d.qc = d.wv ? a.values[qe] : 0.0;
+  if (d.pfv) {  // prefetched into LDS during the previous document
+    d.qid = d.wv ? sm.pf.ids[qn] : 0;
+    d.qc = d.wv ? sm.pf.vals[qn] : 0.0;
+  } else {
+    d.qid = d.wv ? a.indices[qe] : 0;
+    d.qc = d.wv ? a.values[qe] : 0.0;
+  }
   // (m_v = logscale[id] and ε' are loaded in rows64_iterate beside the block's B rows: a third dependent
   // round trip here would sit on the prologue's chain)
 
@@ -251,6 +274,54 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
     if (tid == 0) sm.cs = cs0;
   }
   return true;  // (the block loads' barrier publishes eθ)
+}
+
+// One step of the next document's prefetch (resident grid, wave 0, in the wait of an iteration in which it
+// is not a ψ wave): (0) its row, member and entry offset; (1) its CSR extent; (2) its ≤ 192 ids and counts —
+// each an LDS-DMA (global_load_lds: no register destination) whose source address depends only on the
+// previous step's result, read back from LDS after a vmcnt drain that finds it long complete.  A document
+// that converges first leaves the chain unfinished: the next one then loads for itself.
+template <class S>
+__device__ __forceinline__ void rows64_prefetch_step(const EStepArgs<double>& a, RLds<S>& sm, RDoc& d, int lane) {
+  typedef __attribute__((address_space(3))) void* lds_t;
+  if (d.pfs >= 3) return;  // done, or given up (no next document / a long one)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the previous step's DMA (issued two iterations ago)
+  const int nxt = __builtin_amdgcn_readfirstlane(d.nxt);
+  const int64_t slot = a.slot0 + nxt;
+  if (d.pfs == 0) {
+    if (nxt >= a.n) {  // no next document
+      d.pfs = 9;
+      return;
+    }
+    if (lane < 4) {
+      const int32_t* src = lane == 0 ? a.batch + slot
+                         : lane == 1 ? a.orig + slot
+                                     : reinterpret_cast<const int32_t*>(a.bptr + slot) + (lane - 2);
+      __builtin_amdgcn_global_load_lds(src, (lds_t)&sm.pf.rme[0], 4, 0, 0);
+    }
+  } else if (d.pfs == 1) {
+    const int64_t row = sm.pf.rme[0];
+    if (lane < 4) __builtin_amdgcn_global_load_lds(reinterpret_cast<const int32_t*>(a.indptr + row) + lane,
+                                                   (lds_t)&sm.pf.ext[0], 4, 0, 0);
+  } else {
+    const int64_t s0 = (int64_t)(((uint64_t)(uint32_t)sm.pf.ext[1] << 32) | (uint32_t)sm.pf.ext[0]);
+    const int64_t s1 = (int64_t)(((uint64_t)(uint32_t)sm.pf.ext[3] << 32) | (uint32_t)sm.pf.ext[2]);
+    const int64_t nnz64 = s1 - s0;
+    if (nnz64 < 0 || nnz64 > 32 * kOnChipSets) {  // the long-document kernel's: no prefetch
+      d.pfs = 9;
+      return;
+    }
+    const int nnz = (int)nnz64;
+#pragma unroll
+    for (int i = 0; i < kOnChipSets / 2; ++i)  // ids: 64 dwords per instruction
+      if (64 * i + lane < nnz) __builtin_amdgcn_global_load_lds(a.indices + s0 + 64 * i + lane, (lds_t)&sm.pf.ids[64 * i], 4, 0, 0);
+#pragma unroll
+    for (int i = 0; i < kOnChipSets; ++i)  // counts: two dwords each, 64 dwords per instruction
+      if (64 * i + lane < 2 * nnz)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const int32_t*>(a.values + s0) + 64 * i + lane,
+                                         (lds_t)(reinterpret_cast<int32_t*>(sm.pf.vals) + 64 * i), 4, 0, 0);
+  }
+  d.pfs += 1;
 }
 
 // the document block (R row sets) and the fixed point; returns the iteration count, the worker's φ
@@ -507,6 +578,8 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
       }
       const double d = wave_sum_d(dg);
       if (lane == 0) sm.dsum[pw] = d;
+    } else if (R64_PREFETCH && d.pfon && w == 0 && (it & 1) && it <= 5) {
+      rows64_prefetch_step<S>(a, sm, d, lane);  // wave 0 waits at barrier 2 here anyway
     }
     STAMP(psi ? 5 : 8);  // ψ phase (ψ waves; non-ψ waves: nothing)
     __syncthreads();  // (2) eθ, γ, Σ|Δγ| published
@@ -608,7 +681,7 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
 // LONG: the 7–8-row-set documents; RES: a resident kernel (d.tid laundered per document)
 template <class S, bool STATS, bool BOUND, bool LONG, bool RES = LONG>
 __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& sm, RDoc& d) {
-  d.e0 = a.bptr ? a.bptr[d.slot] : d.s0;
+  if (!d.pfv) d.e0 = a.bptr ? a.bptr[d.slot] : d.s0;
   if (!rows64_open<S, STATS, BOUND, RES>(a, sm, d)) return;
   double qdt = 0.0;
   int it;
@@ -636,6 +709,9 @@ __global__ __launch_bounds__(64 * kW, 2) void k_estep_rows64(EStepArgs<double> a
 #ifdef STC_STAMP
   d.st0 = stamp_now();
 #endif
+  d.nxt = 0;
+  d.pfs = 0;
+  d.pfon = d.pfv = false;
   d.slot = a.slot0 + blockIdx.x;
   d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
   d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
@@ -655,11 +731,15 @@ template <class S, bool STATS, bool BOUND>
 __global__ __launch_bounds__(64 * kW, 2) void k_estep_rows64_pers(EStepArgs<double> a, int32_t* ticket) {
   __shared__ RLds<S> sm;
   __shared__ int s_tk;
-  if (threadIdx.x == 0) s_tk = atomicAdd(ticket, 1);
+  if (threadIdx.x == 0) {
+    s_tk = atomicAdd(ticket, 1);
+    sm.pf.valid = 0;
+  }
   __syncthreads();
   int cur = s_tk;
+  const bool pfon = R64_PREFETCH && a.batch && a.orig && a.bptr;
   while (cur < a.n) {
-    __syncthreads();  // every thread has read s_tk
+    __syncthreads();  // every thread has read s_tk and the prefetch flags
     int nxt = 0;
     if (threadIdx.x == 0) nxt = atomicAdd(ticket, 1);  // the next document's ticket, stored after this one
     RDoc d;
@@ -668,15 +748,33 @@ __global__ __launch_bounds__(64 * kW, 2) void k_estep_rows64_pers(EStepArgs<doub
 #endif
     d.tid = threadIdx.x;
     asm volatile("" : "+v"(d.tid));
+    d.nxt = nxt;
+    d.pfs = 0;
+    d.pfon = pfon;
+    d.pfv = pfon && sm.pf.valid && sm.pf.slot == cur;
     d.slot = a.slot0 + cur;
-    d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
-    d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
-    d.s0 = a.indptr[d.row];
-    d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
+    if (d.pfv) {  // row, member, entry offset and extent from the previous document's prefetch
+      d.row = sm.pf.rme[0];
+      d.mem = sm.pf.rme[1];
+      d.e0 = (int64_t)(((uint64_t)(uint32_t)sm.pf.rme[3] << 32) | (uint32_t)sm.pf.rme[2]);
+      d.s0 = (int64_t)(((uint64_t)(uint32_t)sm.pf.ext[1] << 32) | (uint32_t)sm.pf.ext[0]);
+      const int64_t s1 = (int64_t)(((uint64_t)(uint32_t)sm.pf.ext[3] << 32) | (uint32_t)sm.pf.ext[2]);
+      d.nnz = (int)(s1 - d.s0);
+    } else {  // (also every workgroup's first document)
+      d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
+      d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
+      d.s0 = a.indptr[d.row];
+      d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
+    }
     d.rsets = (d.nnz + 31) >> 5;
     if (d.rsets <= kOnChipSets) rows64_doc<S, STATS, BOUND, false, true>(a, sm, d);
-    if (threadIdx.x == 0) s_tk = nxt;
-    __syncthreads();  // LDS is the next document's; s_tk published
+    if (pfon && d.tid < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's prefetch DMA landed
+    if (threadIdx.x == 0) {
+      s_tk = nxt;
+      sm.pf.valid = d.pfs == 3;  // all three steps issued (and, after the drain above, landed)
+      sm.pf.slot = nxt;
+    }
+    __syncthreads();  // LDS is the next document's; s_tk and the prefetch published
     cur = s_tk;
   }
 }
@@ -707,6 +805,9 @@ __global__ __launch_bounds__(64 * kW, R64_LONG_OCC) void k_estep_rows64_long(ESt
     // lane maps and the α / ψc loads out of the document loop and hold them across the fixed point
     d.tid = threadIdx.x;
     asm volatile("" : "+v"(d.tid));
+    d.nxt = 0;
+    d.pfs = 0;
+    d.pfon = d.pfv = false;
     d.slot = a.slot0 + a.long_list[1 + j];
     d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
     d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
@@ -720,7 +821,7 @@ __global__ __launch_bounds__(64 * kW, R64_LONG_OCC) void k_estep_rows64_long(ESt
 
 template <class S>
 bool launch_persist(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound) {
-  if (!R64_PERSIST || !a.long_list) return false;
+  if (!R64_PERSIST || !a.long_list || bound) return false;  // (the bound E-step keeps a workgroup per slot)
   int32_t* ticket = a.long_list + a.n + 1;  // the word past the long-document list (api.hip reserves it)
   auto go = [&](const void* kern) {
     int dev = 0, cus = 0, per_cu = 0;
@@ -736,7 +837,6 @@ bool launch_persist(hipStream_t s, const EStepArgs<double>& a, bool stats, bool 
     return true;
   };
   if (stats) return go((const void*)k_estep_rows64_pers<S, true, false>);
-  if (bound) return go((const void*)k_estep_rows64_pers<S, false, true>);
   return go((const void*)k_estep_rows64_pers<S, false, false>);
 }
 template <class S>
