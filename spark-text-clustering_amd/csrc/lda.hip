@@ -469,15 +469,58 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
   flush(cur);
 }
 
+// Full tiles: kTile consecutive chunks all inside one run (the entries just before and just after the
+// tile carry the same term, so — the keys being sorted — every entry of the tile does).  Each such tile's
+// head partials are summed here, in chunk order, one wave per tile, into the tail row of its first chunk
+// (an interior chunk's tail row is otherwise unused: k_sstats writes its whole sum to the head row).
+// k_fixup's owner then steps over a full tile with one add, so the run of a frequent term (thousands
+// of chunks at the headline corpus) costs its owner tens of dependent round trips, not hundreds.
+constexpr int kTile = 32;
+template <typename T, int Q>
+__global__ __launch_bounds__(256) void k_fixup_tiles(const uint32_t* __restrict__ skeys, int64_t E, int kp,
+                                                     const T* __restrict__ headbuf, T* __restrict__ tailbuf,
+                                                     int64_t nchunks, StatMap map) {
+  constexpr int kG = 32 / Q;
+  const int c0 = (int)blockIdx.y * 64 * Q;
+  const int lane = threadIdx.x & 63;
+  const int64_t cb = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kTile;
+  if (cb == 0 || cb + kTile >= nchunks) return;  // an entry before the tile and one after it
+  const uint32_t key = skeys[cb * kChunk - 1];
+  if (skeys[(cb + kTile) * kChunk] != key) return;
+  if (map.sub >= 0 && stat_sub(map, key) != map.sub) return;  // another sub-chunk launch's row
+  T acc[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) acc[q] = T(0);
+  for (int g0 = 0; g0 < kTile; g0 += kG) {
+    T h[kG][Q];
+#pragma unroll
+    for (int g = 0; g < kG; ++g)
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int col = c0 + lane + 64 * q;
+        h[g][q] = col < kp ? headbuf[(cb + g0 + g) * kp + col] : T(0);
+      }
+#pragma unroll
+    for (int g = 0; g < kG; ++g)
+#pragma unroll
+      for (int q = 0; q < Q; ++q) acc[q] += h[g][q];
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int col = c0 + lane + 64 * q;
+    if (col < kp) tailbuf[cb * kp + col] = acc[q];
+  }
+}
+
 template <typename T, int Q>
 __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skeys, int64_t E,
                                                int kp, T* __restrict__ stat,
                                                const T* __restrict__ headbuf,
                                                const T* __restrict__ tailbuf, int64_t nchunks,
                                                StatMap map) {
-  // the run's owner (the chunk where it starts) adds the head partials of the chunks the run covers,
-  // in chunk order; kG chunks are fetched at a time (keys and partials), so a run over hundreds of
-  // chunks (the most frequent terms) costs hundreds / kG dependent round trips, not hundreds
+  // the run's owner (the chunk where it starts) adds the partials of the chunks the run covers, in
+  // chunk order: chunk by chunk up to a kTile boundary, then whole full tiles (k_fixup_tiles' sums),
+  // then chunk by chunk to the run's end.  kG chunks / tiles are fetched at a time (keys and partials).
   constexpr int kG = 32 / Q;
   const int c0 = (int)blockIdx.y * 64 * Q;  // this slab's first topic column
   const int lane = threadIdx.x & 63;
@@ -497,32 +540,66 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
     acc[q] = col < kp ? tailbuf[c * kp + col] : T(0);
   }
   bool more = true;
-  for (int64_t cb = c + 1; more && cb < nchunks; cb += kG) {
-    bool go[kG];
+  int64_t cb = c + 1;
+  auto chunks = [&](int64_t stop) {  // chunk by chunk over [cb, stop) while the run goes on
+    while (more && cb < stop) {
+      const int64_t m = stop - cb < kG ? stop - cb : kG;
+      bool go[kG];
+      T h[kG][Q];
+#pragma unroll
+      for (int g = 0; g < kG; ++g) {  // chunk cb+g continues the run past its end?
+        const int64_t c2 = cb + g < nchunks ? cb + g : nchunks - 1;
+        const int64_t q0 = c2 * kChunk;
+        const int64_t q1 = (q0 + kChunk < E) ? q0 + kChunk : E;
+        go[g] = skeys[q1 - 1] == last && q1 < E && skeys[q1] == last;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const int col = c0 + lane + 64 * q;
+          h[g][q] = col < kp ? headbuf[c2 * kp + col] : T(0);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < kG; ++g) {
+        if (more && g < m) {
+#pragma unroll
+          for (int q = 0; q < Q; ++q) acc[q] += h[g][q];
+          more = go[g];
+        }
+      }
+      cb += m;
+    }
+  };
+  chunks((c + kTile) / kTile * kTile < nchunks ? (c + kTile) / kTile * kTile : nchunks);
+  // whole tiles: cb is a tile boundary and the run reached it (the entry before cb is `last`), so the
+  // tile is full — k_fixup_tiles summed it — exactly when the entry after it is `last` too
+  while (more && cb + kTile < nchunks) {
+    bool full[kG];
     T h[kG][Q];
 #pragma unroll
-    for (int g = 0; g < kG; ++g) {  // chunk cb+g continues the run past its end?
-      const int64_t c2 = cb + g < nchunks ? cb + g : nchunks - 1;
-      const int64_t q0 = c2 * kChunk;
-      const int64_t q1 = (q0 + kChunk < E) ? q0 + kChunk : E;
-      go[g] = skeys[q1 - 1] == last && q1 < E && skeys[q1] == last;
+    for (int g = 0; g < kG; ++g) {
+      const int64_t t = cb + (int64_t)g * kTile;
+      const int64_t tc = t < nchunks ? t : nchunks - 1;
+      full[g] = t + kTile < nchunks && skeys[(t + kTile) * kChunk] == last;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const int col = c0 + lane + 64 * q;
-        h[g][q] = col < kp ? headbuf[c2 * kp + col] : T(0);
+        h[g][q] = col < kp ? tailbuf[tc * kp + col] : T(0);
       }
     }
+    bool tiles = true;
 #pragma unroll
     for (int g = 0; g < kG; ++g) {
-      if (more && cb + g < nchunks) {
+      if (tiles && full[g]) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) acc[q] += h[g][q];
-        more = go[g];
+        cb += kTile;
       } else {
-        more = false;
+        tiles = false;
       }
     }
+    if (!tiles) break;
   }
+  chunks(nchunks);
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     const int col = c0 + lane + 64 * q;
@@ -537,6 +614,12 @@ static void sstats_q(hipStream_t s, const uint32_t* skeys, const uint64_t* svals
   const dim3 grid((unsigned)ceil_div(nchunks, 4), (unsigned)ceil_div(kp, 64 * Q));
   k_sstats<T, Q><<<grid, 256, 0, s>>>(skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, nchunks, map);
   KERNEL_CHECK();
+  const int64_t ntiles = ceil_div(nchunks, (int64_t)kTile);
+  if (ntiles > 1) {
+    k_fixup_tiles<T, Q><<<dim3((unsigned)ceil_div(ntiles, 4), grid.y), 256, 0, s>>>(skeys, E, kp, headbuf, tailbuf,
+                                                                                   nchunks, map);
+    KERNEL_CHECK();
+  }
   k_fixup<T, Q><<<grid, 256, 0, s>>>(skeys, E, kp, stat, headbuf, tailbuf, nchunks, map);
   KERNEL_CHECK();
 }

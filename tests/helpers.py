@@ -31,6 +31,22 @@ def random_corpus(rng, D, V, min_nnz=1, max_nnz=40, max_count=6, empty_every=0):
     return stc.CsrMatrix.from_rows(rows, V)
 
 
+def long_run_corpus(rng, D, V, hot):
+    """Every document holds the `hot` terms (the first in all documents, the others in most), plus 3-6
+    random ones: the term-sorted entries have runs of thousands of entries — hundreds of sstats chunks,
+    several full 32-chunk tiles (lda.hip k_fixup_tiles) — starting at odd offsets."""
+    import stc
+
+    hot = np.asarray(hot, np.int32)
+    keep = rng.random((D, hot.size)) < np.linspace(1.0, 0.55, hot.size)
+    cold = [np.setdiff1d(rng.choice(V, size=int(rng.integers(3, 7)), replace=False), hot) for _ in range(D)]
+    rows = []
+    for d in range(D):
+        ids = np.unique(np.concatenate([hot[keep[d]], cold[d]])).astype(np.int32)
+        rows.append((ids, rng.integers(1, 5, ids.size).astype(np.float64)))
+    return stc.CsrMatrix.from_rows(rows, V)
+
+
 def planted_corpus(rng, D, V, k, L=60, alpha=0.1):
     """A small LDA-generative corpus (topics = Zipf over their own term permutation)."""
     import stc

@@ -9,7 +9,7 @@ Tolerances: fp64, only the summation order of sstats across shards differs (1e-1
 import numpy as np
 import pytest
 
-from helpers import random_corpus
+from helpers import long_run_corpus, random_corpus
 
 pytestmark = pytest.mark.gpu
 
@@ -347,3 +347,29 @@ def test_chunked_reduce_scatter_is_bitwise_the_single_one(ctx, monkeypatch, dtyp
         for a, b in zip(got[:3], ref[:3]):
             np.testing.assert_array_equal(a, b)
         assert got[3] == ref[3]
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_chunked_reduce_scatter_long_runs(ctx, monkeypatch, dtype):
+    """The sub-chunk sstats launches (StatMap) where frequent terms' runs span full 32-chunk tiles in
+    every member (lda.hip k_fixup_tiles: a sub-chunk launch sums only its own terms' tiles): an injected
+    step of 60000 documents over 3 members, hot terms in slices 0, 1 and 2 and in several sub-chunks,
+    STC_RS_CHUNKS=4 bit-identical to the single reduce-scatter."""
+    import stc
+
+    rng = np.random.default_rng(32)
+    D, V, k = 60000, 5000, 24
+    corpus = long_run_corpus(rng, D, V, [0, 1, 1500, 3100, 4900, 4999])
+    ids = np.arange(D)
+    g0 = rng.gamma(100.0, 0.01, size=(D, k))
+    out = {}
+    for chunks in ("1", "4"):
+        monkeypatch.setenv("STC_RS_CHUNKS", chunks)
+        with stc.LdaGroup([0, 0, 0], k, V, dtype=dtype, seed=8, optimize_doc_concentration=True) as g:
+            g.set_corpus(corpus)
+            g.init_random(3)
+            st = g.step(ids, g0)
+            out[chunks] = (g.topics(), g.alpha(), st)
+    for a, b in zip(out["4"][:2], out["1"][:2]):
+        np.testing.assert_array_equal(a, b)
+    assert out["4"][2] == out["1"][2]

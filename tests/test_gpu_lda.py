@@ -11,7 +11,7 @@ test_gpu_config1.py), so fp32 is not a north-star-parity mode and every fp32 ben
 import numpy as np
 import pytest
 
-from helpers import golden_json, golden_npz, planted_corpus, random_corpus
+from helpers import golden_json, golden_npz, long_run_corpus, planted_corpus, random_corpus
 
 pytestmark = pytest.mark.gpu
 
@@ -126,6 +126,44 @@ def test_estep_fp32_at_production_scale_lambda(ctx, oracle, k, scale):
         assert np.abs(gamma[i] - g).sum() <= 1e-3 * k + 1e-4 * g.sum(), (i, np.abs(gamma[i] - g).sum())
         big = g >= 1.0
         np.testing.assert_allclose(gamma[i][big], g[big], rtol=TOL["f32"]["gamma"])
+
+
+@pytest.mark.parametrize("dtype,k", [("f64", 16), ("f64", 100), ("f64", 300), ("f32", 100), ("f32", 700)])
+def test_sstats_long_runs_over_tiles(ctx, oracle, dtype, k):
+    """sstats where frequent terms' runs span hundreds of chunks (k_fixup walks full tiles): stat vs
+    Spark's sstats rebuilt on the host from the kernel's own γ (eθ = exp(ψ(γ) − ψ(Σγ)) with Breeze's ψ,
+    φnorm = eθ·expElogβ[:, ids] + 1e-100, stat[v] = Σ_d eθ_d · cnt_dv / φnorm_dv) — the summation of the
+    run partials is all this checks, so the E-step's iterate is taken as given — and bitwise equal over
+    two launches.  f64 1e-10 relative; f32 2e-3 per entry (fp32 ψ of a dying topic's γ ~ 1e-3 is off by
+    ~6e-5 absolute, so its eθ by that relative) and 2e-4 on the hot rows (fp32 sums of ~2e4 entries)."""
+    import scipy.sparse as sp
+
+    rng = np.random.default_rng(5 + k)
+    D, V = 24000, 4096
+    corpus = long_run_corpus(rng, D, V, [0, 1, 2, 900, 901, 2047, 4095])
+    lam = rng.gamma(100.0, 0.01, size=(V, k))
+    g0 = rng.gamma(100.0, 0.01, size=(D, k))
+    h, _ = _handle(ctx, corpus, k, dtype, lam)
+    ids = np.arange(D)
+    gamma, stat, _ = h.estep(ids, g0, want_stat=True)
+    _, stat2, _ = h.estep(ids, g0, want_stat=True)
+    np.testing.assert_array_equal(stat, stat2)
+    eth = np.exp(oracle.dirichlet_expectation(gamma))  # D × k
+    eeb = oracle.topics_exp_elog_beta(lam)  # V × k
+    rows = np.repeat(np.arange(D), np.diff(corpus.indptr))
+    phinorm = np.empty(corpus.indices.size)
+    for s in range(0, rows.size, 1 << 14):  # bounded host memory at k = 700
+        e = slice(s, s + (1 << 14))
+        phinorm[e] = np.einsum("ij,ij->i", eth[rows[e]], eeb[corpus.indices[e]]) + 1e-100
+    w = sp.csr_matrix((corpus.values / phinorm, (corpus.indices, rows)), shape=(V, D))
+    ref = np.asarray(w @ eth)
+    assert np.count_nonzero(corpus.indices == 0) == D  # term 0's run: D entries, D / 256 chunks
+    big = ref > 1e-6 * ref.max()
+    rel = np.abs(stat[big] - ref[big]) / ref[big]
+    assert rel.max() < (1e-10 if dtype == "f64" else 2e-3), rel.max()
+    hot = [0, 1, 2, 900, 901, 2047, 4095]  # the long runs: a lost or doubled tile is percent-level here
+    np.testing.assert_allclose(stat[hot], ref[hot], rtol=1e-10 if dtype == "f64" else 2e-4,
+                               atol=1e-6 * ref.max())  # fp32 flushes entries ~1e-37 to zero
 
 
 def test_estep_long_documents_global_path(ctx, oracle):
