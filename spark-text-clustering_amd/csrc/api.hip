@@ -290,6 +290,20 @@ void coll_all_gather(Ctx& c, const void* send, void* recv, size_t sendcount, ncc
   L.barrier();
 }
 
+// The sstats pairs' radix sort by term (u32 keys, u64 values): rocprim's onesweep at STC_SORT_BITS bits (11: slower)
+// per pass (gfx950's tuned block shape, 1024 threads × 8 items)
+#ifndef STC_SORT_BITS
+#define STC_SORT_BITS 9  // 18-bit term ids (V = 2^18) in two passes: sstats phase −75 µs headline, −90 µs planted vs 8
+#endif
+using TermSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>, STC_SORT_BITS,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+hipError_t term_sort(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const uint64_t* vin, uint64_t* vout,
+                     int64_t n, int bits, hipStream_t s) {
+  return rocprim::radix_sort_pairs<TermSortConfig>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, s);
+}
+
 inline int bits_for(int64_t n) {
   int b = 1;
   while ((int64_t(1) << b) < n) ++b;
@@ -402,10 +416,8 @@ void ensure_batch(stc_lda& L, int64_t n, int64_t E, bool from_next = false) {
   L.tailbuf.reserve(ts * nchunks * L.kp);
   L.lpart.reserve(sizeof(double) * lda::kLogphatBlocks * (L.k + 1));
   size_t tb = 0;
-  HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, L.keys.as<uint32_t>(), L.skeys.as<uint32_t>(),
-                                               L.vals.as<uint64_t>(), L.svals.as<uint64_t>(),
-                                               (int)std::max<int64_t>(E, 1), 0, bits_for(L.V),
-                                               L.ctx->stream));
+  HIP_CHECK(term_sort(nullptr, tb, L.keys.as<uint32_t>(), L.skeys.as<uint32_t>(), L.vals.as<uint64_t>(),
+                      L.svals.as<uint64_t>(), std::max<int64_t>(E, 1), bits_for(L.V), L.ctx->stream));
   L.sort_tmp.reserve(tb);
 }
 
@@ -746,9 +758,8 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.vpad * L.kp, s));  // padded rows stay zero
   if (E > 0) {
     size_t tb = L.sort_tmp.bytes;
-    HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(L.sort_tmp.p, tb, L.keys.as<uint32_t>(),
-                                                 L.skeys.as<uint32_t>(), L.vals.as<uint64_t>(),
-                                                 L.svals.as<uint64_t>(), (int)E, 0, bits_for(L.V), s));
+    HIP_CHECK(term_sort(L.sort_tmp.p, tb, L.keys.as<uint32_t>(), L.skeys.as<uint32_t>(), L.vals.as<uint64_t>(),
+                        L.svals.as<uint64_t>(), E, bits_for(L.V), s));
   }
   const lda::StatMap lay = split ? stat_layout(L) : lda::StatMap{};
   if (lay.nsub <= 1) {
