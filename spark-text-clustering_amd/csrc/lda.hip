@@ -541,32 +541,48 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
   }
   bool more = true;
   int64_t cb = c + 1;
-  auto chunks = [&](int64_t stop) {  // chunk by chunk over [cb, stop) while the run goes on
+  // chunk by chunk over [cb, stop) while the run goes on.  The run's extent within a batch of kG chunks
+  // comes from their end keys first (chunk cb is in the run; cb + g is when cb + g − 1 went on past its
+  // end), and only those chunks' partials are read — most runs end in the chunk after their owner, and
+  // reading kG partials for each of them was ≈ 0.4 GB per launch at the headline
+  auto chunks = [&](int64_t stop) {
     while (more && cb < stop) {
-      const int64_t m = stop - cb < kG ? stop - cb : kG;
+      const int m = stop - cb < kG ? (int)(stop - cb) : kG;
       bool go[kG];
       T h[kG][Q];
 #pragma unroll
-      for (int g = 0; g < kG; ++g) {  // chunk cb+g continues the run past its end?
+      for (int g = 0; g < kG; ++g) {  // chunk cb+g (all `last` when in the run) goes on past its end?
         const int64_t c2 = cb + g < nchunks ? cb + g : nchunks - 1;
-        const int64_t q0 = c2 * kChunk;
-        const int64_t q1 = (q0 + kChunk < E) ? q0 + kChunk : E;
-        go[g] = skeys[q1 - 1] == last && q1 < E && skeys[q1] == last;
+        const int64_t q1 = (c2 * kChunk + kChunk < E) ? c2 * kChunk + kChunk : E;
+        go[g] = q1 < E && skeys[q1] == last;
+      }
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {  // chunk cb's partial, with the keys
+        const int col = c0 + lane + 64 * q;
+        h[0][q] = col < kp ? headbuf[cb * kp + col] : T(0);
+      }
+      int n_in = 1;       // chunks of this batch in the run
+      bool gl = go[0];    // the last of them goes on past its end
+#pragma unroll
+      for (int g = 1; g < kG; ++g)
+        if (n_in == g && g < m && go[g - 1]) {
+          n_in = g + 1;
+          gl = go[g];
+        }
+#pragma unroll
+      for (int g = 1; g < kG; ++g)
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
           const int col = c0 + lane + 64 * q;
-          h[g][q] = col < kp ? headbuf[c2 * kp + col] : T(0);
+          h[g][q] = g < n_in && col < kp ? headbuf[(cb + g) * kp + col] : T(0);
         }
-      }
 #pragma unroll
-      for (int g = 0; g < kG; ++g) {
-        if (more && g < m) {
+      for (int g = 0; g < kG; ++g)
+        if (g < n_in)
 #pragma unroll
           for (int q = 0; q < Q; ++q) acc[q] += h[g][q];
-          more = go[g];
-        }
-      }
-      cb += m;
+      more = gl;
+      cb += n_in;
     }
   };
   chunks((c + kTile) / kTile * kTile < nchunks ? (c + kTile) / kTile * kTile : nchunks);
