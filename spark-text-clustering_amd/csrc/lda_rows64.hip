@@ -48,8 +48,9 @@
 #define R64_RCP_NR 2  // Newton steps after v_rcp_f64 in that chain
 #endif
 #ifndef R64_MIRROR
-#define R64_MIRROR 0  // 1 (k > 64): the idle wave of the ψ wave's topic set computes Σ|Δγ| off the ψ chain —
-                      // measured +1.3 % E-step on the headline (r04: 31.96 vs 31.54 ms), so off
+#define R64_MIRROR 1  // 1 (k > 64): the idle wave of the ψ wave's topic set computes Σ|Δγ| off the ψ chain.
+                      // r04 measured it +1.3 % (31.96 vs 31.54 ms, off then); after the in-wave s
+                      // reduce-scatter and the resident grid it is −4 %: headline E-step 27.05 → 25.97 ms
 #endif
 #ifndef R64_SB_RS
 #define R64_SB_RS 1  // Phase B's s partials reduce-scattered over the wave's row lanes (4 per topic, not 32)
