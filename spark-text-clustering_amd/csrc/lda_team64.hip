@@ -42,6 +42,9 @@ constexpr int kTSlotD = 64 * kTSets;    // granule slot of a member's Σ|Δγ| p
 constexpr int kTSlotG = kTSlotD + 1;    // … of its final Σγ partial
 constexpr int kTXStride = kTSlotG + 1;  // granules per member and parity
 constexpr int kTMaxP = 8;               // members at most (k ≤ 832)
+#ifndef TG_MIRROR
+#define TG_MIRROR 1  // the ψ wave's Σ|Δγ| reduction moved to the idle wave of its topic set (0: on the ψ wave)
+#endif
 #ifndef TG_LOAD_BATCH
 #define TG_LOAD_BATCH 2                 // row sets whose block loads are in flight together
 #endif
@@ -278,6 +281,13 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
   }
   __syncthreads();  // the staging area is the loop's partial arrays; (also publishes the first eθ, γ, α/ψc)
   STAMP(0);  // block loads and their barrier
+  // mirror mode (as lda_rows64.hip): waves w and w ^ 4 share a topic set and take turns as its ψ wave and
+  // as its Σ|Δγ| wave; each keeps γ / eθ of its lane's topic as it last computed them
+  double gm = 0.0, em = 0.0;
+  if (TG_MIRROR && t.town) {
+    gm = sm.gam[t.tt];
+    em = sm.eth[t.ttl][t.ttp];
+  }
 
   double* const pa = &sm.u.l.pa[w][0][0];
   double* const sb = &sm.u.l.sb[0][0];
@@ -415,7 +425,7 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
         const double2* const sp = reinterpret_cast<const double2*>(sb + t.tt * kTSbPitch);
         const double2 x0 = sp[0], x1 = sp[1], x2 = sp[2], x3 = sp[3];  // the eight waves' sums, fixed order
         const double s = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
-        const double g = sm.gam[t.tt], eo = sm.eth[t.ttl][t.ttp];
+        const double g = TG_MIRROR ? gm : sm.gam[t.tt], eo = sm.eth[t.ttl][t.ttp];
         const double2 ap = *reinterpret_cast<const double2*>(&sm.apc[t.tt][0]);  // α_t, ψc_t
         const double2 e01 = *reinterpret_cast<const double2*>(&sm.esum[0]);
         const double2 e23 = *reinterpret_cast<const double2*>(&sm.esum[2]);
@@ -426,11 +436,30 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
         const double gn = fma(eo, s, ap.x);  // γ ← eθ ⊙ s + α
         dg = fabs(gn - g);
         sm.gam[t.tt] = gn;
-        sm.eth[t.ttl][t.ttp] = exp_digamma_minus_v2<2>(gn, csn + ap.y);
+        const double en = exp_digamma_minus_v2<2>(gn, csn + ap.y);
+        sm.eth[t.ttl][t.ttp] = en;
+        gm = gn;
+        em = en;
+      }
+      if (!TG_MIRROR) {
+        const double dw = wave_sum_d(dg);
+        if (lane == 0) sm.dpart[w & 3] = dw;
+      }
+      __builtin_amdgcn_s_setprio(0);
+    } else if (TG_MIRROR) {
+      // the topic set's other wave: the same γ update from its own γ / eθ registers (bitwise the ψ wave's:
+      // same partials, same order) and Σ|Δγ|, off the ψ chain
+      double dg = 0.0;
+      if (t.town) {
+        const double2* const sp = reinterpret_cast<const double2*>(sb + t.tt * kTSbPitch);
+        const double2 x0 = sp[0], x1 = sp[1], x2 = sp[2], x3 = sp[3];
+        const double s = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
+        const double gn = fma(em, s, sm.apc[t.tt][0]);
+        dg = fabs(gn - gm);
+        gm = gn;  // (its eθ: the ψ wave's, from LDS, when this wave is next the ψ wave)
       }
       const double dw = wave_sum_d(dg);
       if (lane == 0) sm.dpart[w & 3] = dw;
-      __builtin_amdgcn_s_setprio(0);
     }
     STAMP(psi ? 6 : 8);  // ψ phase (ψ waves; the others: nothing)
     __syncthreads();  // (2) eθ, γ, Σ|Δγ| partials published
