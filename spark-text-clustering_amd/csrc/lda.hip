@@ -688,8 +688,11 @@ __device__ __forceinline__ double row_max(double m, double) { return wave_max(m)
 // four waves of a block take rows w, w+4, …; the block's partials are added in wave order, so colsum
 // is identical for any vocabulary slicing that keeps the blocks (§6).  UPDATE = false: colsum
 // partials and Bp of the current λ (set_topics / init_random).
+// five workgroups per CU (≤ 102 VGPRs, no spills; the default budget took 106 and four): the pass is
+// latency-bound, one row in flight per wave — M-step 0.361 → 0.330 ms at the headline (6: 48 B of scratch
+// per lane, 0.41 ms; the next row's loads issued before this row's ψ / exp, measured slower)
 template <typename T, int Q, bool UPDATE>
-__global__ __launch_bounds__(256) void k_lambda_eeb(double* __restrict__ lam, const T* __restrict__ stat,
+__global__ __launch_bounds__(256, 5) void k_lambda_eeb(double* __restrict__ lam, const T* __restrict__ stat,
                                                     T* __restrict__ Bp, double* __restrict__ logscale,
                                                     int64_t V, int k, int kp, double rho, double scale,
                                                     double eta, const double* __restrict__ gate,
