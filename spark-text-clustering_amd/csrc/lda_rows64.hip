@@ -35,15 +35,6 @@
 #ifndef R64_PRIO
 #define R64_PRIO 2  // wave priority raised over the latency-critical phases (1: ψ; 2: ψ + r): −2 % E-step (r03)
 #endif
-#ifndef R64_PSI_V2
-#define R64_PSI_V2 1  // the ψ phase's chain: psi64.h exp_digamma_minus_v2 (0: the round-3 form)
-#endif
-#ifndef R64_PSI_V3
-#define R64_PSI_V3 0  // the v2 chain with its constants read from an LDS table (psi64.h exp_digamma_minus_v3)
-#endif
-#ifndef R64_PSI_V4
-#define R64_PSI_V4 1  // the v2 chain with its exp() constants in VGPRs across the fixed point (exp_digamma_minus_v4)
-#endif
 #ifndef R64_RCP_NR
 #define R64_RCP_NR 2  // Newton steps after v_rcp_f64 in that chain
 #endif
@@ -51,17 +42,6 @@
 #define R64_MIRROR 1  // 1 (k > 64): the idle wave of the ψ wave's topic set computes Σ|Δγ| off the ψ chain.
                       // r04 measured it +1.3 % (31.96 vs 31.54 ms, off then); after the in-wave s
                       // reduce-scatter and the resident grid it is −4 %: headline E-step 27.05 → 25.97 ms
-#endif
-#ifndef R64_SB_RS
-#define R64_SB_RS 1  // Phase B's s partials reduce-scattered over the wave's row lanes (4 per topic, not 32)
-#endif
-#ifndef R64_PERSIST
-#define R64_PERSIST 1  // the common documents on a resident grid taking tickets (1) or one workgroup per slot (0)
-#endif
-#ifndef R64_PREFETCH
-#define R64_PREFETCH 0  // 1: the resident grid fetches the next document's identity and entries to LDS (LDS-DMA)
-                        // during this one — correct, but measured slower (headline 27.8 vs 27.0 ms, planted
-                        // 4.40 vs 4.36 ms: wave 0's DMA steps and drains, 256 VGPRs)
 #endif
 #ifndef R64_LONG_OCC
 #define R64_LONG_OCC 1  // long-document kernel workgroups per CU the register budget is cut for
@@ -73,8 +53,7 @@ namespace lda {
 namespace {
 
 constexpr int kW = 4;          // waves per document
-constexpr int kSbPitch = R64_SB_RS ? 4 : 34;  // s-partial row pitch (doubles): per wave (R64_SB_RS) or per row lane
-                                               // (conflict-free 8-B stores, 16-B reads)
+constexpr int kSbPitch = 4;   // s-partial row pitch (doubles): one sum per wave (rs_rows8), 16-B reads
 constexpr int kPaPitch = 10;   // φ-partial row pitch (doubles): conflict-free 16-B worker reads
 constexpr int kOnChipSets = 6; // row sets the common kernel holds (5 in VGPRs + 1 in LDS)
 constexpr int kMaxSets = 8;    // one worker lane per wave row: 8 row lanes × 8 sets = 64 lanes
@@ -93,18 +72,6 @@ using RCommon = RShape<KL, 5, kOnChipSets>;
 template <int KL>
 using RLong = RShape<KL, kMaxSets, kMaxSets>;
 
-__device__ __forceinline__ double exp_digamma_minus_r64(double x, double cst, const PsiK& tab) {
-#if R64_PSI_V3
-  return exp_digamma_minus_v3<R64_RCP_NR>(x, cst, tab);
-#elif R64_PSI_V2
-  (void)tab;
-  return exp_digamma_minus_v2<R64_RCP_NR>(x, cst);
-#else
-  (void)tab;
-  return exp_digamma_minus_s(x, cst);
-#endif
-}
-
 template <class S>
 struct RLds {
   double eth[8][S::KLP] __attribute__((aligned(16)));  // eθ, topic t at [t / KL][t % KL]
@@ -117,7 +84,7 @@ struct RLds {
   double cs;                       // ψ(Σγ') of the current eθ (the bound's scale)
   double apc[S::KT][2] __attribute__((aligned(16)));  // α_t, ψc_t of the ψ lanes' topics (not in VGPRs)
   double ac[4] __attribute__((aligned(16)));  // Σα, Σcts, ψ(Σα + Σcts) (the flat ψ(Σγ'))
-  PsiK psik;                       // the ψ/exp chain's constants (R64_PSI_V3)
+  PsiK psik;                       // the exp() constants of the ψ chain (psi_expk_load)
   union {
     struct {
       double pa[kW][8 * S::RMAX][kPaPitch];  // φ partials (wave, wave row, topic lane)
@@ -126,15 +93,6 @@ struct RLds {
     double stage[kW][8][S::KT + 2];          // load phase: eight B rows per wave at a time
   } u __attribute__((aligned(16)));
   double ovf[S::NOVF > 0 ? S::NOVF * kW * S::KL * 64 : 1];  // row sets past RREG ([set][w][p][lane])
-  // resident grid (R64_PREFETCH): the next document's row / member / entry offset, its CSR extent and its
-  // ≤ 192 (term id, count) pairs, loaded by LDS-DMA in the idle waits of this document's fixed point
-  struct {
-    double vals[32 * kOnChipSets];
-    int32_t ids[32 * kOnChipSets];
-    int32_t rme[4];   // batch[slot], orig[slot], bptr[slot] (two words)
-    int32_t ext[4];   // indptr[row], indptr[row + 1] (two words each)
-    int32_t slot, valid;
-  } pf __attribute__((aligned(16)));
 };
 
 // Per-lane document context: set up once per document by rows64_open, outside the row-set
@@ -147,10 +105,6 @@ struct RLds {
 struct RDoc {
   int64_t slot, row, mem, s0, e0;
   int nnz, rsets;
-  int nxt;                           // resident grid: the next ticket (valid in thread 0)
-  int pfs;                           // prefetch steps issued during this document (wave 0)
-  bool pfon;                         // resident grid with batch / orig / bptr: prefetch the next document
-  bool pfv;                          // this document's identity and entries came from the prefetch
   int tid;                           // the resident long kernel's threadIdx.x, laundered per document
   int lane, w, tl, rl;
   int npsi, half, pw, tt, ttl, ttp;  // ψ-lane topic map
@@ -196,13 +150,8 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
   const int qn = 32 * (lane >> 3) + 8 * w + (lane & 7);
   d.wv = lane < 8 * d.rsets && qn < d.nnz;
   const int64_t qe = d.wv ? d.s0 + qn : 0;
-  if (d.pfv) {  // prefetched into LDS during the previous document
-    d.qid = d.wv ? sm.pf.ids[qn] : 0;
-    d.qc = d.wv ? sm.pf.vals[qn] : 0.0;
-  } else {
-    d.qid = d.wv ? a.indices[qe] : 0;
-    d.qc = d.wv ? a.values[qe] : 0.0;
-  }
+  d.qid = d.wv ? a.indices[qe] : 0;
+  d.qc = d.wv ? a.values[qe] : 0.0;
   // (m_v = logscale[id] and ε' are loaded in rows64_iterate beside the block's B rows: a third dependent
   // round trip here would sit on the prologue's chain)
 
@@ -230,9 +179,7 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
     if (d.tval) sm.gam[tt] = g0;
   }
   for (int i = tid; i < 8 * KLP; i += 64 * kW) (&sm.eth[0][0])[i] = 0.0;
-#if R64_PSI_V3 || R64_PSI_V4
   psik_fill(sm.psik, tid, 64 * kW);  // (published by the barrier below)
-#endif
   {
     const double gs = wave_sum_d(g0), as = wave_sum_d(alp), cts = wave_sum_d(d.qc);
     if (lane == 0) {
@@ -271,58 +218,10 @@ __device__ __forceinline__ bool rows64_open(const EStepArgs<double>& a, RLds<S>&
   // eθ' = exp(ψ(γ) − ψ(Σγ) − ψc_t): Spark's exp(E[log θ]) times expElogβ's per-topic factor
   {
     const double cs0 = digamma_fast_d(gsum0);
-    if (w < npsi && d.town) sm.eth[d.ttl][d.ttp] = exp_digamma_minus_r64(g0, cs0 + pc, sm.psik);
+    if (w < npsi && d.town) sm.eth[d.ttl][d.ttp] = exp_digamma_minus_v2<R64_RCP_NR>(g0, cs0 + pc);
     if (tid == 0) sm.cs = cs0;
   }
   return true;  // (the block loads' barrier publishes eθ)
-}
-
-// One step of the next document's prefetch (resident grid, wave 0, in the wait of an iteration in which it
-// is not a ψ wave): (0) its row, member and entry offset; (1) its CSR extent; (2) its ≤ 192 ids and counts —
-// each an LDS-DMA (global_load_lds: no register destination) whose source address depends only on the
-// previous step's result, read back from LDS after a vmcnt drain that finds it long complete.  A document
-// that converges first leaves the chain unfinished: the next one then loads for itself.
-template <class S>
-__device__ __forceinline__ void rows64_prefetch_step(const EStepArgs<double>& a, RLds<S>& sm, RDoc& d, int lane) {
-  typedef __attribute__((address_space(3))) void* lds_t;
-  if (d.pfs >= 3) return;  // done, or given up (no next document / a long one)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the previous step's DMA (issued two iterations ago)
-  const int nxt = __builtin_amdgcn_readfirstlane(d.nxt);
-  const int64_t slot = a.slot0 + nxt;
-  if (d.pfs == 0) {
-    if (nxt >= a.n) {  // no next document
-      d.pfs = 9;
-      return;
-    }
-    if (lane < 4) {
-      const int32_t* src = lane == 0 ? a.batch + slot
-                         : lane == 1 ? a.orig + slot
-                                     : reinterpret_cast<const int32_t*>(a.bptr + slot) + (lane - 2);
-      __builtin_amdgcn_global_load_lds(src, (lds_t)&sm.pf.rme[0], 4, 0, 0);
-    }
-  } else if (d.pfs == 1) {
-    const int64_t row = sm.pf.rme[0];
-    if (lane < 4) __builtin_amdgcn_global_load_lds(reinterpret_cast<const int32_t*>(a.indptr + row) + lane,
-                                                   (lds_t)&sm.pf.ext[0], 4, 0, 0);
-  } else {
-    const int64_t s0 = (int64_t)(((uint64_t)(uint32_t)sm.pf.ext[1] << 32) | (uint32_t)sm.pf.ext[0]);
-    const int64_t s1 = (int64_t)(((uint64_t)(uint32_t)sm.pf.ext[3] << 32) | (uint32_t)sm.pf.ext[2]);
-    const int64_t nnz64 = s1 - s0;
-    if (nnz64 < 0 || nnz64 > 32 * kOnChipSets) {  // the long-document kernel's: no prefetch
-      d.pfs = 9;
-      return;
-    }
-    const int nnz = (int)nnz64;
-#pragma unroll
-    for (int i = 0; i < kOnChipSets / 2; ++i)  // ids: 64 dwords per instruction
-      if (64 * i + lane < nnz) __builtin_amdgcn_global_load_lds(a.indices + s0 + 64 * i + lane, (lds_t)&sm.pf.ids[64 * i], 4, 0, 0);
-#pragma unroll
-    for (int i = 0; i < kOnChipSets; ++i)  // counts: two dwords each, 64 dwords per instruction
-      if (64 * i + lane < 2 * nnz)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const int32_t*>(a.values + s0) + 64 * i + lane,
-                                         (lds_t)(reinterpret_cast<int32_t*>(sm.pf.vals) + 64 * i), 4, 0, 0);
-  }
-  d.pfs += 1;
 }
 
 // the document block (R row sets) and the fixed point; returns the iteration count, the worker's φ
@@ -415,9 +314,7 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
 
   double* const pa = &sm.u.l.pa[w][0][0];
   double* const sb = &sm.u.l.sb[0][0];
-#if R64_PSI_V4
   const PsiExpK expk = psi_expk_load(sm.psik);
-#endif
   double rr[R];
   double qr = 0.0;  // worker: r of its row (φ without ε' in qdt)
   qdt = 0.0;
@@ -472,7 +369,6 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
     if ((it > 0 && dsum <= a.stop_thr) || it >= a.max_iter) break;
 
     // Phase B: s partials over the lane's R rows, one row lane's slot per topic
-#if R64_SB_RS
     {  // the eight row lanes summed inside the wave (estep_common.h rs_rows8): lane (tl, rl) stores the wave
        // sums of its topic lane's topics 2·rl, 2·rl + 1, so a ψ lane reads 4 partials instead of 32
       double x[16];
@@ -490,15 +386,6 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
       if (2 * rl < KL) sb[(KL * tl + 2 * rl) * kSbPitch + w] = s0;
       if (2 * rl + 1 < KL) sb[(KL * tl + 2 * rl + 1) * kSbPitch + w] = s1;
     }
-#else
-#pragma unroll
-    for (int p = 0; p < KL; ++p) {
-      double x = 0.0;
-#pragma unroll
-      for (int j = 0; j < R; ++j) x = fma(BV(j, p), rr[j], x);
-      sb[(KL * tl + p) * kSbPitch + 8 * w + rl] = x;
-    }
-#endif
     STAMP(3);  // s FMAs + partial stores
     __syncthreads();  // (1) s partials and esum published
     STAMP(4);  // barrier 1
@@ -509,38 +396,18 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
       if (town) {
         // every LDS read of the phase issued together: the partials, γ, eθ, the four ε' sums
         const double2* const sp = reinterpret_cast<const double2*>(sb + tt * kSbPitch);
-#if R64_SB_RS
         const double2 x0 = sp[0], x1 = sp[1];  // the four waves' sums
-#else
-        double2 xs[16];
-#pragma unroll
-        for (int h = 0; h < 16; ++h) xs[h] = sp[h];
-#endif
         const double g = mir ? gm : sm.gam[tt], eo = sm.eth[ttl][ttp];
         const double2 ap = *reinterpret_cast<const double2*>(&sm.apc[tt][0]);  // α_t, ψc_t
         const double2 e01 = *reinterpret_cast<const double2*>(&sm.esum[0]);
         const double2 e23 = *reinterpret_cast<const double2*>(&sm.esum[2]);
-#if R64_SB_RS
         const double s = (x0.x + x0.y) + (x1.x + x1.y);
-#else
-        double c4[4];
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const double2 x0 = xs[4 * h], x1 = xs[4 * h + 1], x2 = xs[4 * h + 2], x3 = xs[4 * h + 3];
-          c4[h] = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
-        }
-        const double s = (c4[0] + c4[1]) + (c4[2] + c4[3]);
-#endif
         const double et = (e01.x + e01.y) + (e23.x + e23.y);
         const double csn = et != 0.0 ? digamma_fast_d(sm.ac[0] + sm.ac[1] - et) : sm.ac[2];
         const double gn = fma(eo, s, ap.x);  // γ ← eθ ⊙ s + α
         dg = fabs(gn - g);
         sm.gam[tt] = gn;
-#if R64_PSI_V4
         const double en = exp_digamma_minus_v4<R64_RCP_NR>(gn, csn + ap.y, expk);
-#else
-        const double en = exp_digamma_minus_r64(gn, csn + ap.y, sm.psik);
-#endif
         sm.eth[ttl][ttp] = en;
         gm = gn;
         em = en;
@@ -558,29 +425,14 @@ __device__ __forceinline__ int rows64_iterate(const EStepArgs<double>& a, RLds<S
       if (town) {
         const double2* const sp = reinterpret_cast<const double2*>(sb + tt * kSbPitch);
         const double al = sm.apc[tt][0];
-#if R64_SB_RS
         const double2 y0 = sp[0], y1 = sp[1];
         const double s = (y0.x + y0.y) + (y1.x + y1.y);
-#else
-        double2 xs[16];
-#pragma unroll
-        for (int h = 0; h < 16; ++h) xs[h] = sp[h];
-        double c4[4];
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-          const double2 x0 = xs[4 * h], x1 = xs[4 * h + 1], x2 = xs[4 * h + 2], x3 = xs[4 * h + 3];
-          c4[h] = ((x0.x + x0.y) + (x1.x + x1.y)) + ((x2.x + x2.y) + (x3.x + x3.y));
-        }
-        const double s = (c4[0] + c4[1]) + (c4[2] + c4[3]);
-#endif
         const double gn = fma(em, s, al);
         dg = fabs(gn - gm);
         gm = gn;  // (its eθ: the ψ wave's, from LDS, when this wave is next the ψ wave)
       }
       const double d = wave_sum_d(dg);
       if (lane == 0) sm.dsum[pw] = d;
-    } else if (R64_PREFETCH && d.pfon && w == 0 && (it & 1) && it <= 5) {
-      rows64_prefetch_step<S>(a, sm, d, lane);  // wave 0 waits at barrier 2 here anyway
     }
     STAMP(psi ? 5 : 8);  // ψ phase (ψ waves; non-ψ waves: nothing)
     __syncthreads();  // (2) eθ, γ, Σ|Δγ| published
@@ -682,7 +534,7 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
 // LONG: the 7–8-row-set documents; RES: a resident kernel (d.tid laundered per document)
 template <class S, bool STATS, bool BOUND, bool LONG, bool RES = LONG>
 __device__ __forceinline__ void rows64_doc(const EStepArgs<double>& a, RLds<S>& sm, RDoc& d) {
-  if (!d.pfv) d.e0 = a.bptr ? a.bptr[d.slot] : d.s0;
+  d.e0 = a.bptr ? a.bptr[d.slot] : d.s0;
   if (!rows64_open<S, STATS, BOUND, RES>(a, sm, d)) return;
   double qdt = 0.0;
   int it;
@@ -710,9 +562,6 @@ __global__ __launch_bounds__(64 * kW, 2) void k_estep_rows64(EStepArgs<double> a
 #ifdef STC_STAMP
   d.st0 = stamp_now();
 #endif
-  d.nxt = 0;
-  d.pfs = 0;
-  d.pfon = d.pfv = false;
   d.slot = a.slot0 + blockIdx.x;
   d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
   d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
@@ -723,24 +572,20 @@ __global__ __launch_bounds__(64 * kW, 2) void k_estep_rows64(EStepArgs<double> a
   rows64_doc<S, STATS, BOUND, false>(a, sm, d);
 }
 
-// The same documents on a resident grid (R64_PERSIST): every workgroup takes the next slot from a ticket
-// counter and walks until the tickets run out (no dependency between workgroups: any residency drains).
-// A workgroup per slot paid a dispatch and its own prologue start per document; here the next ticket is
-// requested at the start of a document and read at its end, and the per-document lane maps are laundered
-// (as in the long-document kernel) so they are not hoisted and held across the fixed point.
+// The same documents on a resident grid: every workgroup takes the next slot from a ticket counter and
+// walks until the tickets run out (no dependency between workgroups: any residency drains).  A workgroup
+// per slot paid a dispatch and its own prologue start per document; here the next ticket is requested at
+// the start of a document and read at its end, and the per-document lane maps are laundered (as in the
+// long-document kernel) so they are not hoisted and held across the fixed point.
 template <class S, bool STATS, bool BOUND>
 __global__ __launch_bounds__(64 * kW, 2) void k_estep_rows64_pers(EStepArgs<double> a, int32_t* ticket) {
   __shared__ RLds<S> sm;
   __shared__ int s_tk;
-  if (threadIdx.x == 0) {
-    s_tk = atomicAdd(ticket, 1);
-    sm.pf.valid = 0;
-  }
+  if (threadIdx.x == 0) s_tk = atomicAdd(ticket, 1);
   __syncthreads();
   int cur = s_tk;
-  const bool pfon = R64_PREFETCH && a.batch && a.orig && a.bptr;
   while (cur < a.n) {
-    __syncthreads();  // every thread has read s_tk and the prefetch flags
+    __syncthreads();  // every thread has read s_tk
     int nxt = 0;
     if (threadIdx.x == 0) nxt = atomicAdd(ticket, 1);  // the next document's ticket, stored after this one
     RDoc d;
@@ -749,33 +594,15 @@ __global__ __launch_bounds__(64 * kW, 2) void k_estep_rows64_pers(EStepArgs<doub
 #endif
     d.tid = threadIdx.x;
     asm volatile("" : "+v"(d.tid));
-    d.nxt = nxt;
-    d.pfs = 0;
-    d.pfon = pfon;
-    d.pfv = pfon && sm.pf.valid && sm.pf.slot == cur;
     d.slot = a.slot0 + cur;
-    if (d.pfv) {  // row, member, entry offset and extent from the previous document's prefetch
-      d.row = sm.pf.rme[0];
-      d.mem = sm.pf.rme[1];
-      d.e0 = (int64_t)(((uint64_t)(uint32_t)sm.pf.rme[3] << 32) | (uint32_t)sm.pf.rme[2]);
-      d.s0 = (int64_t)(((uint64_t)(uint32_t)sm.pf.ext[1] << 32) | (uint32_t)sm.pf.ext[0]);
-      const int64_t s1 = (int64_t)(((uint64_t)(uint32_t)sm.pf.ext[3] << 32) | (uint32_t)sm.pf.ext[2]);
-      d.nnz = (int)(s1 - d.s0);
-    } else {  // (also every workgroup's first document)
-      d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
-      d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
-      d.s0 = a.indptr[d.row];
-      d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
-    }
+    d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
+    d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
+    d.s0 = a.indptr[d.row];
+    d.nnz = (int)(a.indptr[d.row + 1] - d.s0);
     d.rsets = (d.nnz + 31) >> 5;
     if (d.rsets <= kOnChipSets) rows64_doc<S, STATS, BOUND, false, true>(a, sm, d);
-    if (pfon && d.tid < 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's prefetch DMA landed
-    if (threadIdx.x == 0) {
-      s_tk = nxt;
-      sm.pf.valid = d.pfs == 3;  // all three steps issued (and, after the drain above, landed)
-      sm.pf.slot = nxt;
-    }
-    __syncthreads();  // LDS is the next document's; s_tk and the prefetch published
+    if (threadIdx.x == 0) s_tk = nxt;
+    __syncthreads();  // LDS is the next document's; s_tk published
     cur = s_tk;
   }
 }
@@ -806,9 +633,6 @@ __global__ __launch_bounds__(64 * kW, R64_LONG_OCC) void k_estep_rows64_long(ESt
     // lane maps and the α / ψc loads out of the document loop and hold them across the fixed point
     d.tid = threadIdx.x;
     asm volatile("" : "+v"(d.tid));
-    d.nxt = 0;
-    d.pfs = 0;
-    d.pfon = d.pfv = false;
     d.slot = a.slot0 + a.long_list[1 + j];
     d.row = a.batch ? (int64_t)a.batch[d.slot] : d.slot;
     d.mem = a.orig ? (int64_t)a.orig[d.slot] : d.slot;
@@ -822,7 +646,7 @@ __global__ __launch_bounds__(64 * kW, R64_LONG_OCC) void k_estep_rows64_long(ESt
 
 template <class S>
 bool launch_persist(hipStream_t s, const EStepArgs<double>& a, bool stats, bool bound) {
-  if (!R64_PERSIST || !a.long_list || bound) return false;  // (the bound E-step keeps a workgroup per slot)
+  if (!a.long_list || bound) return false;  // (the bound E-step keeps a workgroup per slot)
   int32_t* ticket = a.long_list + a.n + 1;  // the word past the long-document list (api.hip reserves it)
   auto go = [&](const void* kern) {
     int dev = 0, cus = 0, per_cu = 0;

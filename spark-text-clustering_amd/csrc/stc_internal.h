@@ -318,57 +318,6 @@ __device__ inline double exp_digamma_minus_d(double x, double cst) {
   return y * exp(((sh ? breeze_shift_fix(x, iy, sh) - c : 0.0) - 0.5 * iy + t) - cst);
 }
 
-// Latency-shaped forms of the above for the fp64 E-step's per-iteration critical path (lda_rows64.hip):
-// the same Breeze series, but branch-free (the shift part is computed for every lane and selected, so
-// the compiler cannot sink it into a divergent branch that serialises it after the y part) and every
-// polynomial in Estrin form (dependency depth ⌈log2 n⌉ + 1 instead of n), with exp() evaluated here:
-// Cody–Waite reduction to |r| ≤ ln2/2 and the degree-13 Taylor polynomial (truncation 4e-18 relative).
-__device__ __forceinline__ double exp_estrin(double z) {
-  const double n = __builtin_rint(z * 1.4426950408889634);
-  double r = fma(-n, 6.93147180369123816490e-01, z);  // ln2_hi: 32 significant bits, n·ln2_hi exact
-  r = fma(-n, 1.90821492927058770002e-10, r);        // ln2_lo
-  const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
-  const double a0 = 1.0 + r, a1 = fma(r, 1.0 / 6.0, 0.5), a2 = fma(r, 1.0 / 120.0, 1.0 / 24.0),
-               a3 = fma(r, 1.0 / 5040.0, 1.0 / 720.0), a4 = fma(r, 1.0 / 362880.0, 1.0 / 40320.0),
-               a5 = fma(r, 1.0 / 39916800.0, 1.0 / 3628800.0), a6 = fma(r, 1.0 / 6227020800.0, 1.0 / 479001600.0);
-  const double b0 = fma(r2, a1, a0), b1 = fma(r2, a3, a2), b2 = fma(r2, a5, a4);
-  const double c0 = fma(r4, b1, b0), c1 = fma(r4, a6, b2);
-  const double p = fma(r8, c1, c0);
-  // n < -1100: 0 (p·2^n underflows); the E-step never asks for overflow (its argument is ≤ ~0)
-  return __builtin_ldexp(p, (int)fmax(n, -1100.0));
-}
-__device__ __forceinline__ double breeze_trunc_estrin(double iy) {
-  const double f = iy * iy, f2 = f * f, f4 = f2 * f2, f8 = f4 * f4;
-  const double lo = fma(f, 26.284421368293753, -3.053401198888146);
-  const double mid = fma(f, 2372.137971404805, -260.94994774566294);
-  const double P = fma(f4, -12318.55039822477, fma(f2, mid, lo));
-  return (f8 * f) * P;
-}
-__device__ __forceinline__ double breeze_series_estrin(double f) {  // f·(−1/12 + f/120 − …) of digamma_t
-  const double f2 = f * f, f4 = f2 * f2;
-  const double a0 = fma(f, 1.0 / 120.0, -1.0 / 12.0), a1 = fma(f, 1.0 / 240.0, -1.0 / 252.0),
-               a2 = fma(f, 691.0 / 32760.0, -1.0 / 132.0), a3 = fma(f, 3617.0 / 8160.0, -1.0 / 12.0);
-  return f * fma(f4, fma(f2, a3, a2), fma(f2, a1, a0));
-}
-// exp(ψ(x) − cst) as exp_digamma_minus_d, branch-free with the Estrin forms
-__device__ __forceinline__ double exp_digamma_minus_fast(double x, double cst) {
-  const bool sh = x <= 5.0;
-  const double xs = sh ? x : 1.0;  // a safe operand for the lanes that do not shift
-  const double x2 = xs * xs, x4 = x2 * x2;
-  // q = xs(xs+1)…(xs+5) and p = q'·… (Σ_{i<6} 1/(xs+i) = p/q) in Estrin form
-  const double q = xs * fma(x4, xs + 15.0, fma(x2, fma(xs, 85.0, 225.0), fma(xs, 274.0, 120.0)));
-  const double p = fma(x4, fma(xs, 6.0, 75.0), fma(x2, fma(xs, 340.0, 675.0), fma(xs, 548.0, 120.0)));
-  const double iq = rcp_nr(q);
-  double c = p * iq;
-  c = fma(fma(-q, c, p), iq, c);
-  const double y = sh ? x + 6.0 : x;
-  const double iy = rcp_nr(y);
-  const double yb = xs + (floor(5.0 - xs) + 1.0);
-  const double fix = breeze_trunc_estrin(iy) - breeze_trunc_estrin(__builtin_amdgcn_rcp(yb));
-  const double shift = sh ? fix - c : 0.0;
-  return y * exp_estrin(((shift - 0.5 * iy) + breeze_series_estrin(iy * iy)) - cst);
-}
-
 __host__ __device__ inline double trigamma_d(double x) {
   double r = 0;
   while (x <= 5.0) {

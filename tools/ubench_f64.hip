@@ -1,6 +1,6 @@
 // ubench_f64.hip — latency / issue microbenchmarks for the fp64 E-step's building blocks on gfx950
 // (MI355X): dependent and independent v_fma_f64, v_rcp_f64, the ψ/exp chain of the ψ phase
-// (psi64.h exp_digamma_minus_s, stc_internal.h exp_digamma_minus_fast), a dependent ds_read_b128, the
+// (psi64.h exp_digamma_minus_v2, one and two Newton steps), a dependent ds_read_b128, the
 // fp64 wave reduction, and a 4-wave s_barrier — each with 1, 2 and 3 waves per SIMD (one workgroup
 // of 4·W waves on one CU).  Prints one JSON line per case: cycles per operation per wave (s_memtime
 // around the loop, max over the waves).  Build: make -C tools ubench (hipcc, gfx950).
@@ -24,7 +24,7 @@ __device__ __forceinline__ unsigned long long now() {
   return t;
 }
 
-enum Op { FMA_DEP, FMA_IND8, RCP_DEP, PSI_S, PSI_S_X2, PSI_FAST, LDS_DEP, WSUM, BARRIER, RCPNR_DEP, PSI_V2_2, PSI_V2_1,
+enum Op { FMA_DEP, FMA_IND8, RCP_DEP, LDS_DEP, WSUM, BARRIER, RCPNR_DEP, PSI_V2_2, PSI_V2_1,
           PKFMA_IND8, FMA_BANK_SAME, FMA_BANK_SPLIT, FMA_SHARED_E };
 
 template <int OP>
@@ -58,19 +58,6 @@ __global__ void k_bench(double* out, unsigned long long* cyc, double a, double b
       for (int i = 0; i < kN; ++i) {
         x = rcp_nr(x);
         asm volatile("" : "+v"(x));
-      }
-    } else if (OP == PSI_S) {
-#pragma unroll 2
-      for (int i = 0; i < kN / 16; ++i) {
-        x = fma(exp_digamma_minus_s(x, a), 0.25, b);
-        asm volatile("" : "+v"(x));
-      }
-    } else if (OP == PSI_S_X2) {
-#pragma unroll 2
-      for (int i = 0; i < kN / 16; ++i) {
-        x = fma(exp_digamma_minus_s(x, a), 0.25, b);
-        y = fma(exp_digamma_minus_s(y, a), 0.25, b);
-        asm volatile("" : "+v"(x), "+v"(y));
       }
     } else if (OP == PSI_V2_2 || OP == PSI_V2_1) {
 #pragma unroll 2
@@ -118,12 +105,6 @@ __global__ void k_bench(double* out, unsigned long long* cyc, double a, double b
               "v_fmac_f64 v[88:89], v[122:123], v[128:129]\n v_fmac_f64 v[92:93], v[126:127], v[128:129]" ::
                   : "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130", "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141", "v142", "v143", "v144", "v145", "v146", "v147", "v148", "v149", "v150", "v151", "v152", "v153", "v154", "v155", "v156", "v157", "v158", "v159");
       }
-    } else if (OP == PSI_FAST) {
-#pragma unroll 2
-      for (int i = 0; i < kN / 16; ++i) {
-        x = fma(exp_digamma_minus_fast(x, a), 0.25, b);
-        asm volatile("" : "+v"(x));
-      }
     } else if (OP == LDS_DEP) {
 #pragma unroll 8
       for (int i = 0; i < kN; ++i) {
@@ -153,8 +134,7 @@ __global__ void k_bench(double* out, unsigned long long* cyc, double a, double b
 // operations per timed loop, for the per-op figure
 static int ops(int op) {
   switch (op) {
-    case PSI_S: case PSI_FAST: case PSI_V2_2: case PSI_V2_1: return kN / 16;
-    case PSI_S_X2: return kN / 16;  // pairs
+    case PSI_V2_2: case PSI_V2_1: return kN / 16;
     case WSUM: return kN / 8;
     default: return kN;
   }
@@ -217,9 +197,6 @@ int main() {
     run<FMA_IND8>("fma_f64_8_independent", w, d_out, d_cyc);
     run<RCP_DEP>("rcp_f64_dependent", w, d_out, d_cyc);
     run<RCPNR_DEP>("rcp_nr_dependent", w, d_out, d_cyc);
-    run<PSI_S>("exp_digamma_minus_s_dependent", w, d_out, d_cyc);
-    run<PSI_S_X2>("exp_digamma_minus_s_2_chains", w, d_out, d_cyc);
-    run<PSI_FAST>("exp_digamma_minus_fast_dependent", w, d_out, d_cyc);
     run<PSI_V2_2>("exp_digamma_minus_v2_nr2_dependent", w, d_out, d_cyc);
     run<PSI_V2_1>("exp_digamma_minus_v2_nr1_dependent", w, d_out, d_cyc);
     run<PKFMA_IND8>("pk_fma_f32_8_independent", w, d_out, d_cyc);
