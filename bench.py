@@ -344,7 +344,8 @@ class _Group:
 
     def counters(self):  # (Σ over the members, member 0)
         cs = self.h.counters()
-        tot = {key: sum(c[key] for c in cs) for key in cs[0]}
+        tot = {key: sum(c[key] for c in cs) for key in cs[0] if key != "kernels"}
+        tot["kernels"] = {f: sum(c["kernels"][f] for c in cs) for f in cs[0]["kernels"]}
         return tot, cs[0]
 
     def phases(self):  # member 0's phase times, and the slowest member's E-step
@@ -395,7 +396,9 @@ def run_state(m, lam0, barrier, log, a, dtype, steps, warmup):
             "docs": c1["docs"] - c0["docs"], "entries": c1["entries"] - c0["entries"],
             "iters": c1["inner_iters"] - c0["inner_iters"], "cap_hits": c1["cap_hits"] - c0["cap_hits"],
             "docs_local": l1["docs"] - l0["docs"], "entries_local": l1["entries"] - l0["entries"],
-            "iters_local": l1["inner_iters"] - l0["inner_iters"]}
+            "iters_local": l1["inner_iters"] - l0["inner_iters"],
+            # the E-step kernels the library actually launched in the timed steps (stc_lda_kernel_counts)
+            "kernels": {f: l1["kernels"][f] - l0["kernels"][f] for f in l1["kernels"] if l1["kernels"][f] > l0["kernels"][f]}}
 
 
 # north-star parity of each dtype (tests/test_gpu_config1.py: configs[0] against the oracle)
@@ -463,21 +466,33 @@ def summarize(r, a, dtype, world, steps, corpus_kind, kernel):
     }
 
 
-def kernel_name(dtype, k):
-    """The training E-step kernel libstc dispatches (api.hip use_wide: grid kernels up to their topic
-    capacity, fp32 k <= 128 / fp64 k <= 104, the many-topic kernel past it)."""
-    if dtype == "f64" and 104 < k <= 832:
-        return ("k_estep_tgrid64 (lda_team64.hip): the fp64 many-topic training E-step, a team of "
-                f"{-(-k // 104)} CUs per document with the topics split (rows64 grid in each member), one launch "
-                "per minibatch (documents past 448 rows: k_estep_wide / _mc)")
-    if k > (128 if dtype == "f32" else 104):
-        return ("k_estep_wide / k_estep_wide_mc (lda_wide.hip): the many-topic training E-step (k <= 512: a "
-                "team of CUs per document), one launch per minibatch")
-    if dtype == "f64":
-        return ("k_estep_rows64_pers (lda_rows64.hip): the fp64 training E-step, one launch per minibatch on a "
-                "resident grid taking document tickets (plus the 7-8-row-set launch when a document has > 192 rows)")
-    return ("k_estep_grid_pers (lda_grid.hip): the fp32 training E-step, one launch per minibatch on a resident "
-            "grid taking document tickets")
+KERNEL_TEXT = {
+    "k_estep_rows64": "k_estep_rows64_pers (lda_rows64.hip): the fp64 training E-step, one launch per minibatch on a "
+                      "resident grid taking document tickets",
+    "k_estep_grid": "k_estep_grid_pers (lda_grid.hip): the fp32 training E-step, one launch per minibatch on a resident "
+                    "grid taking document tickets",
+    "k_estep_tgrid64": "k_estep_tgrid64 (lda_team64.hip): the fp64 many-topic training E-step, a team of CUs per "
+                       "document with the topics split (rows64 grid in each member), one launch per minibatch",
+    "k_estep_wide_mc": "k_estep_wide_mc (lda_wide.hip): the many-topic training E-step, the rows of a document split "
+                       "over a team of CUs, one launch per minibatch",
+    "k_estep_wide_tc": "k_estep_wide_tc (lda_wide.hip): the many-topic training E-step, the topics of a document split "
+                       "over a team of CUs, one launch per minibatch",
+    "k_estep_wide": "k_estep_wide (lda_wide.hip): the many-topic training E-step, one CU per document, one launch per "
+                    "minibatch",
+    "k_estep": "k_estep (lda.hip): the workgroup E-step for documents past the fast kernels' row capacity",
+}
+
+
+def kernel_name(launched):
+    """The training E-step kernel libstc dispatched in the timed steps, from its own launch counters
+    (stc_lda_kernel_counts; ADVICE r5: not inferred from k and dtype): the family with the most launches,
+    the others (the 7-8-row-set pass, team fallbacks, the workgroup kernel) named beside it."""
+    fams = {f: n for f, n in launched.items() if f in KERNEL_TEXT}
+    if not fams:
+        return "no E-step launch in the timed steps"
+    main = max(fams, key=lambda f: fams[f])
+    extra = {f: n for f, n in launched.items() if f != main}
+    return KERNEL_TEXT[main] + (f"; also launched: {extra}" if extra else "")
 
 
 def launch_mode(gpus, env, force_group=False):
@@ -544,7 +559,11 @@ def main():
     if mode == "ranks":
         import torch.distributed as dist  # control plane only (uid exchange, barrier, max time)
 
-        dist.init_process_group("gloo")
+        import datetime
+
+        # a bounded control plane: a rank whose peer died fails its barrier instead of waiting 30 min; the
+        # data path's own waits end at STC_COLL_TIMEOUT_MS (api.hip poll_wait) and abort the communicator
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=int(os.environ.get("STC_DIST_TIMEOUT_S", "900"))))
     import stc
 
     lam_head = None
@@ -602,7 +621,7 @@ def main():
         del tokens
 
     r = run_state(model, lam_head, barrier, log, a, a.dtype, a.steps, a.warmup)
-    head = summarize(reduce_run(r), a, a.dtype, world, a.steps, a.corpus, kernel_name(a.dtype, a.k))
+    head = summarize(reduce_run(r), a, a.dtype, world, a.steps, a.corpus, kernel_name(r["kernels"]))
     h = model.h
 
     lines = []
@@ -610,13 +629,13 @@ def main():
         other = "f32" if a.dtype == "f64" else "f64"
         dcorp[other] = stc.DeviceCsr.upload(ctx, corpus, DT[other])
         r2 = run_state(_Single(stc, ctx, a, other, dcorp[other], total), None, barrier, log, a, other, a.steps, a.warmup)
-        s2 = summarize(reduce_run(r2), a, other, world, a.steps, a.corpus, kernel_name(other, a.k))
+        s2 = summarize(reduce_run(r2), a, other, world, a.steps, a.corpus, kernel_name(r2["kernels"]))
         lines.append(dict(label=f"{other} E-step, same corpus and model state", dtype=other, corpus=a.corpus, **s2))
         pc, lam_p = planted
         for dt in (a.dtype, other):
             dp = stc.DeviceCsr.upload(ctx, pc, DT[dt])
             r3 = run_state(_Single(stc, ctx, a, dt, dp, a.docs), lam_p, barrier, log, a, dt, a.steps, a.warmup)
-            s3 = summarize(reduce_run(r3), a, dt, world, a.steps, "zipf-lda", kernel_name(dt, a.k))
+            s3 = summarize(reduce_run(r3), a, dt, world, a.steps, "zipf-lda", kernel_name(r3["kernels"]))
             lines.append(dict(label=f"{dt} E-step, planted-topic corpus at the planted model (SURVEY §8(d) state B)",
                               dtype=dt, corpus="zipf-lda", **s3))
             dp.free()

@@ -150,8 +150,9 @@ int stc_hash_tokens(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const in
  * laid out as stc_hashing_tf's input: the separator-free lower-cased blob utf8_out (utf8_cap bytes;
  * n_bytes + n_bytes / 2 always suffices: lower-casing can grow a 2-byte character to 3 bytes — when the
  * text needs more than utf8_cap the call fails with STC_ERR_INVALID_ARG before writing any output and
- * *n_out_bytes holds the size needed; utf8_out = NULL with utf8_cap = 0 is that size query), tok_off_out
- * (capacity n_bytes + n_docs + 1) and doc_off_out[n_docs+1].
+ * *n_out_bytes holds the size needed), tok_off_out (capacity n_bytes + n_docs + 1) and doc_off_out[n_docs+1].
+ * Size query: utf8_out = NULL with utf8_cap = 0 returns STC_OK with only *n_out_bytes (and *n_tok_out when
+ * given) set; tok_off_out and doc_off_out may then be NULL.
  * Lower-casing is Java 8's String.toLowerCase (root locale, Unicode 6.2) for every code point: the BMP
  * through a generated table, Deseret inline, characters Java 8 does not case passed through, and the 18
  * code points whose mapping is not a same-length 1:1 map by rule: U+0130 İ → "i̇" (2 → 3 bytes), U+03A3 Σ
@@ -271,6 +272,22 @@ int stc_lda_enable_timing(stc_lda* lda, int on);
  * [3] docs stopped by max_inner_iter                                                         */
 int stc_lda_counters(stc_lda* lda, int64_t out[4]);
 int stc_lda_phase_times(stc_lda* lda, double* ms_out /* 5 */, int64_t* steps_out);
+/* E-step launches per kernel family, cumulative since creation (training and inference): what actually
+ * ran, so a caller can name the kernel it timed (a team launch that timed out and was re-run on the
+ * one-CU kernel counts under its family, under STC_KC_WIDE and under STC_KC_TEAM_FALLBACK) */
+enum stc_kernel_count {
+  STC_KC_ROWS64 = 0,        /* k_estep_rows64[_pers]: fp64, k <= 104 */
+  STC_KC_ROWS64_LONG = 1,   /* k_estep_rows64_long: the pass over 7-8-row-set documents (may find none) */
+  STC_KC_GRID = 2,          /* k_estep_grid[_pers] (+ its long-document pass): fp32, k <= 128 */
+  STC_KC_WIDE = 3,          /* k_estep_wide: many topics, one CU per document */
+  STC_KC_WIDE_MC = 4,       /* k_estep_wide_mc: many topics, the rows split over a team of CUs */
+  STC_KC_WIDE_TC = 5,       /* k_estep_wide_tc: many topics, the topics split over a team */
+  STC_KC_TGRID64 = 6,       /* k_estep_tgrid64: fp64, the topics split, the rows64 grid in each member */
+  STC_KC_TEAM_FALLBACK = 7, /* team launches re-run on k_estep_wide after a co-residency timeout */
+  STC_KC_WORKGROUP = 8,     /* k_estep: documents past the fast kernels' row capacity */
+  STC_KC_N = 12
+};
+int stc_lda_kernel_counts(stc_lda* lda, int64_t out[12]);
 
 /* ---- one process, N devices ---------------------------------------------------------------
  * The reference trains in ONE JVM (Spark local[*], LDATraining.scala:7), so its drop-in drives every GPU

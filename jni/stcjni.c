@@ -586,6 +586,15 @@ JNIEXPORT void JNICALL FN(ldaCounters)(JNIEnv* env, jclass c, jlong lda, jlongAr
   check(env, st);
 }
 
+/* out[12]: E-step launches per kernel family (stc.h enum stc_kernel_count) */
+JNIEXPORT void JNICALL FN(ldaKernelCounts)(JNIEnv* env, jclass c, jlong lda, jlongArray out) {
+  if (NEED(out, STC_KC_N, "ldaKernelCounts out")) return;
+  jlong* p = PIN(jlong, Long, out);
+  int st = stc_lda_kernel_counts(LDA(lda), (int64_t*)p);
+  UNPIN(Long, out, p, 0);
+  check(env, st);
+}
+
 /* msOut[5]; returns the number of timed steps */
 JNIEXPORT jlong JNICALL FN(ldaPhaseTimes)(JNIEnv* env, jclass c, jlong lda, jdoubleArray ms_out) {
   int64_t steps = 0;

@@ -1,7 +1,8 @@
 package org.apache.spark.ml.clustering
 
 import org.apache.spark.ml.linalg.Vector
-import org.apache.spark.ml.util.Identifiable
+import org.apache.spark.ml.param.ParamMap
+import org.apache.spark.ml.util.{Identifiable, MLReadable, MLReader, MLWriter}
 import org.apache.spark.mllib.clustering.{HipLocalLDAModel, HipOnlineLDAOptimizer, LDA => OldLDA, LocalLDAModel => OldLocalLDAModel}
 import org.apache.spark.mllib.linalg.{Vectors => OldVectors}
 import org.apache.spark.sql.{DataFrame, Dataset, Row, SparkSession}
@@ -65,7 +66,15 @@ class HipLDA(override val uid: String) extends LDA(uid) {
  * topicDistributionCol = θ of each row's features) runs one stc_group_topic_distribution call per
  * partition on the GPU group of `hip` instead of Spark's per-row CPU E-step UDF.  A partition evaluated in
  * another JVM, or after the group was released, gets Spark's CPU function (the same result up to the
- * E-step's convergence tolerance and γ₀ seeding).  γ₀ of row i of partition p is keyed (seed, p·2^32 + i).
+ * E-step's convergence tolerance and γ₀ seeding); those partitions are counted in `cpuFallbackPartitions`
+ * (a Spark accumulator, summed over every transform of this model once its job has run) and logged by the
+ * executor that ran them, so a multi-executor deployment can see that the GPU transform did not run there.
+ * γ₀ of row i of partition p is keyed (seed, p·2^32 + i).
+ *
+ * Persistence is Spark's own: `write` saves the model as a plain ml LocalLDAModel (its metadata names
+ * LocalLDAModel, so LocalLDAModel.load and PipelineModel.load read it back — ADVICE r5), `copy` keeps
+ * this class (pipelines and tuning keep the GPU transform), and HipLDAModel.load delegates to
+ * LocalLDAModel.load.
  */
 class HipLDAModel private[clustering] (
     uid: String,
@@ -74,6 +83,12 @@ class HipLDAModel private[clustering] (
     sparkSession: SparkSession)
   extends LocalLDAModel(uid, vocabSize, hip, sparkSession) {
 
+  @transient private lazy val fallbacks =
+    sparkSession.sparkContext.longAccumulator(s"HipLDAModel($uid).transform CPU-fallback partitions")
+
+  /** Partitions of this model's transforms that ran Spark's CPU E-step (the group was not in their JVM). */
+  def cpuFallbackPartitions: Long = fallbacks.value
+
   override def transform(dataset: Dataset[_]): DataFrame = {
     if ($(topicDistributionCol).isEmpty) return super.transform(dataset)
     val df = dataset.toDF()
@@ -81,12 +96,36 @@ class HipLDAModel private[clustering] (
     val featIdx = df.schema.fieldIndex($(featuresCol))
     val key = hip.token
     val cpu = hip.cpuTopicDistributionMethod
+    val acc = fallbacks
+    val id = uid
     val rows = df.rdd.mapPartitionsWithIndex { (p, it) =>
       val part = it.toArray
       val docs = part.map(r => OldVectors.fromML(r.getAs[Vector](featIdx)))
-      val theta = HipLocalLDAModel.topicDistributionsLocal(key, docs, p.toLong << 32).getOrElse(docs.map(cpu))
+      val theta = HipLocalLDAModel.topicDistributionsLocal(key, docs, p.toLong << 32).getOrElse {
+        acc.add(1L)
+        System.err.println(s"HipLDAModel($id).transform: partition $p runs Spark's CPU E-step (the GPU group " +
+          "is not in this JVM)")
+        docs.map(cpu)
+      }
       part.iterator.zip(theta.iterator).map { case (r, t) => Row.fromSeq(r.toSeq :+ t.asML) }
     }
     df.sparkSession.createDataFrame(rows, outSchema)
   }
+
+  override def copy(extra: ParamMap): LocalLDAModel = {
+    val copied = new HipLDAModel(uid, vocabSize, hip, sparkSession)
+    copyValues(copied, extra).setParent(parent).asInstanceOf[LocalLDAModel]
+  }
+
+  /** Saved as the plain ml LocalLDAModel it extends (same params, topicsMatrix, α, η, gammaShape). */
+  override def write: MLWriter = {
+    val plain = new LocalLDAModel(uid, vocabSize, hip, sparkSession)
+    copyValues(plain).write
+  }
+}
+
+object HipLDAModel extends MLReadable[LocalLDAModel] {
+  /** A saved HipLDAModel is a LocalLDAModel directory (HipLDAModel.write): read it as one. */
+  override def read: MLReader[LocalLDAModel] = LocalLDAModel.read
+  override def load(path: String): LocalLDAModel = LocalLDAModel.load(path)
 }

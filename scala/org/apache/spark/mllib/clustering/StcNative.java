@@ -101,6 +101,8 @@ public final class StcNative {
   public static native void ldaEnableTiming(long lda, boolean on);
   public static native void ldaCounters(long lda, long[] out4);
   public static native long ldaPhaseTimes(long lda, double[] msOut5);
+  /** E-step launches per kernel family (stc.h enum stc_kernel_count), 12 words */
+  public static native void ldaKernelCounts(long lda, long[] out12);
 
   // ---- host helpers (pure Java): Spark vectors → CSR arrays
   /** CSR of sparse or dense rows: {indptr long[n+1], indices int[nnz], values double[nnz]} */

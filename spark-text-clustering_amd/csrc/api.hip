@@ -95,12 +95,14 @@ struct stc_lda {
   DevBuf team_words, team_x;
   unsigned* htmo = nullptr;  // pinned copy of the team kernel's timeout word
   int64_t team_fallbacks = 0;  // team launches re-run on the one-CU kernel after a timeout
+  int64_t kcount[STC_KC_N] = {};  // E-step launches per kernel family (stc_lda_kernel_counts)
 
   // M-step sharding over the vocabulary (multi-GPU): rank r owns λ / expElogβ rows [r·Vs, (r+1)·Vs);
   // Vs is a multiple of the λ-update block so the per-block colsum partials (and hence colsum) are
   // bit-identical to the one-GPU reduction.  virt > 1 runs the same slices on one GPU without
   // collectives (STC_VIRTUAL_SHARDS, for testing the slicing).
   int shards = 1, virt = 1;
+  int tail_fault = 0;  // test knob (STC_GROUP_STEP_FAULT): the tail_fault-th next step throws before its reduce-scatter
   bool force_coll = false;  // STC_COLLECTIVE_MSTEP=1: the RCCL slice path even on a 1-rank communicator (tests)
   // sharded steps: stat reduce-scattered in rs_chunks vocabulary sub-chunks on cstream, each as soon as
   // its sstats launch is done, and the M-step of sub-chunk j under the reduce-scatter of j+1
@@ -233,15 +235,81 @@ MemberPtrs published(const LocalColl& L) {
   return p;
 }
 
+// ---------------------------------------------------------------------------------------
+// Waiting on work that may hold RCCL collectives.  A collective whose peer never arrives (a member
+// thread or a rank that failed before enqueuing its side) never completes, and hipStreamSynchronize
+// would block for ever behind it.  So on a context with a communicator every wait polls — the stream or
+// event, the group's abort flag, ncclCommGetAsyncError — against a deadline (STC_COLL_TIMEOUT_MS,
+// default 120 s).  A timeout or an asynchronous RCCL error aborts this context's communicator
+// (ncclCommAbort releases its queued kernels) and throws STC_ERR_RCCL; a failed peer throws STC_ERR_STATE
+// (stc_group's for_members then aborts every member's communicator).  Without a communicator: plain
+// blocking waits, as before.
+// ---------------------------------------------------------------------------------------
+void abort_comm(Ctx& c) {
+  if (!c.comm || c.comm_aborted.exchange(true)) return;
+  (void)ncclCommAbort(c.comm);  // (c.comm stays set: the context keeps counting as collective, and refuses)
+}
+void check_comm(const Ctx& c) {
+  if (c.comm_aborted.load())
+    throw Error(STC_ERR_STATE, "the RCCL communicator was aborted after a failure: destroy this context / group");
+  if (c.abort_flag && c.abort_flag->load())
+    throw Error(STC_ERR_STATE, "another member of the group failed; its collectives were abandoned");
+}
+template <class Query, class Block>
+void poll_wait(Ctx& c, Query query, Block block, const char* what) {
+  if (!c.comm || !c.coll_enqueued) {  // nothing can be stuck behind a collective (e.g. the corpus upload)
+    HIP_CHECK(block());
+    return;
+  }
+  check_comm(c);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spin = 0;; ++spin) {
+    const hipError_t e = query();
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) HIP_CHECK(e);
+    check_comm(c);
+    ncclResult_t ae = ncclSuccess;
+    if (ncclCommGetAsyncError(c.comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+      abort_comm(c);
+      throw Error(STC_ERR_RCCL, std::string("RCCL asynchronous error while waiting for ") + what + ": " +
+                                    ncclGetErrorString(ae) + " (communicator aborted)");
+    }
+    const int64_t ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (ms > c.coll_timeout_ms) {
+      abort_comm(c);
+      throw Error(STC_ERR_RCCL, std::string("waiting for ") + what + ": not complete after " + std::to_string(ms) +
+                                    " ms (STC_COLL_TIMEOUT_MS = " + std::to_string(c.coll_timeout_ms) +
+                                    "): a collective's peer never arrived; communicator aborted");
+    }
+    // spin first (a step's wait is usually short), then sleep in 20 µs steps
+    if (spin < 2000) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+void wait_stream(Ctx& c, hipStream_t s) {
+  poll_wait(c, [&] { return hipStreamQuery(s); }, [&] { return hipStreamSynchronize(s); }, "a stream");
+}
+void wait_event(Ctx& c, hipEvent_t e) {
+  poll_wait(c, [&] { return hipEventQuery(e); }, [&] { return hipEventSynchronize(e); }, "an event");
+}
+
 void coll_group_start(Ctx& c) {
-  if (c.comm) RCCL_CHECK(ncclGroupStart());
+  if (!c.comm) return;
+  check_comm(c);
+  RCCL_CHECK(ncclGroupStart());
+  c.in_group = true;
+  c.coll_enqueued = true;
 }
 void coll_group_end(Ctx& c) {
-  if (c.comm) RCCL_CHECK(ncclGroupEnd());
+  if (!c.comm) return;
+  c.in_group = false;
+  RCCL_CHECK(ncclGroupEnd());
 }
 // in place: buf ← Σ over members
 void coll_all_reduce(Ctx& c, void* buf, size_t count, ncclDataType_t t, hipStream_t s) {
   if (c.comm) {
+    if (!c.in_group) check_comm(c);
+    c.coll_enqueued = true;
     RCCL_CHECK(ncclAllReduce(buf, buf, count, t, ncclSum, c.comm, s));
     return;
   }
@@ -260,6 +328,8 @@ void coll_all_reduce(Ctx& c, void* buf, size_t count, ncclDataType_t t, hipStrea
 // the member's own slice of send
 void coll_reduce_scatter(Ctx& c, const void* send, void* recv, size_t recvcount, ncclDataType_t t, hipStream_t s) {
   if (c.comm) {
+    if (!c.in_group) check_comm(c);
+    c.coll_enqueued = true;
     RCCL_CHECK(ncclReduceScatter(send, recv, recvcount, t, ncclSum, c.comm, s));
     return;
   }
@@ -274,6 +344,8 @@ void coll_reduce_scatter(Ctx& c, const void* send, void* recv, size_t recvcount,
 // recv[q·sendcount, +sendcount) ← member q's send, on every member (send may be its own slice of recv)
 void coll_all_gather(Ctx& c, const void* send, void* recv, size_t sendcount, ncclDataType_t t, hipStream_t s) {
   if (c.comm) {
+    if (!c.in_group) check_comm(c);
+    c.coll_enqueued = true;
     RCCL_CHECK(ncclAllGather(send, recv, sendcount, t, c.comm, s));
     return;
   }
@@ -332,7 +404,7 @@ void harvest_all(stc_lda& L) {
 // before a step records into the current set: a set is reused three steps later, long complete
 void claim_event_set(stc_lda& L) {
   if (!L.timing || !L.ev_pending[L.ev_set]) return;
-  HIP_CHECK(hipEventSynchronize(L.ev[L.ev_set][5]));
+  wait_event(*L.ctx, L.ev[L.ev_set][5]);
   harvest(L, L.ev_set);
 }
 
@@ -352,7 +424,7 @@ void ensure_layout(stc_lda& L) {
     tmp.reserve(8 * vpad * L.k);
     if (L.lam.p) {
       HIP_CHECK(hipMemcpyAsync(tmp.p, L.lam.p, 8 * L.V * L.k, hipMemcpyDeviceToDevice, L.ctx->stream));
-      HIP_CHECK(hipStreamSynchronize(L.ctx->stream));
+      wait_stream(*L.ctx, L.ctx->stream);
     }
     std::swap(tmp.p, L.lam.p);
     std::swap(tmp.bytes, L.lam.bytes);
@@ -455,7 +527,7 @@ Part partition(stc_lda& L, const int64_t* indptr, const int32_t* raw, int64_t n)
   int32_t ns = 0;
   HIP_CHECK(hipMemcpyAsync(&p.E, L.bptr.as<int64_t>() + n, 8, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipMemcpyAsync(&ns, L.sincl.as<int32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
+  wait_stream(*L.ctx, s);
   p.n_short = ns;
   lda::launch_part_scatter(s, raw, L.bnnz.as<int64_t>(), n, L.flags.as<int32_t>(), L.sincl.as<int32_t>(),
                            L.batch.as<int32_t>(), L.orig.as<int32_t>(), L.nnzp.as<int64_t>());
@@ -639,30 +711,39 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
     const TeamChoice tc = use_wide(L.k, L.dtype) && !bound ? team_choice<T>(L, mean_rows, m.max_row) : TeamChoice{};
     const bool team = tc.P > 1 && launch_wide_team<T>(L, w, stats, tc);
     if (team) {  // launched (a grid that could not be resident falls through to the one-CU kernel)
-      HIP_CHECK(hipStreamSynchronize(s));
+      L.kcount[tc.grid ? STC_KC_TGRID64 : tc.topics ? STC_KC_WIDE_TC : STC_KC_WIDE_MC] += 1;
+      wait_stream(*L.ctx, s);
       if (*L.htmo) {  // a team gave up: the same slots on the one-CU kernel (it rewrites every output)
         *L.htmo = 0;
         L.team_fallbacks += 1;
+        L.kcount[STC_KC_TEAM_FALLBACK] += 1;
+        L.kcount[STC_KC_WIDE] += 1;
         lda::launch_estep_wide<T>(s, w, stats, bound);
       }
-    } else if (use_wide(L.k, L.dtype)) lda::launch_estep_wide<T>(s, w, stats, bound);
-    else if constexpr (std::is_same<T, float>::value) {
+    } else if (use_wide(L.k, L.dtype)) {
+      L.kcount[STC_KC_WIDE] += 1;
+      lda::launch_estep_wide<T>(s, w, stats, bound);
+    } else if constexpr (std::is_same<T, float>::value) {
       const bool long_docs = m.max_row < 0 || m.max_row > lda::grid_onchip_rows(L.k);
       // the long-document list (count word + slots) and, past it, the resident grid's ticket word
       L.long_list.reserve(4 * (size_t)(n_short + 2));
       w.long_list = L.long_list.as<int32_t>();
+      L.kcount[STC_KC_GRID] += 1;
       lda::launch_estep_grid(s, w, stats, bound, long_docs);
     } else {
       const bool long_docs = m.max_row < 0 || m.max_row > lda::rows64_onchip_rows(L.k);
       // the long-document list (count word + slots) and, past it, the resident grid's ticket word
       L.long_list.reserve(4 * (size_t)(n_short + 2));
       w.long_list = L.long_list.as<int32_t>();
+      L.kcount[STC_KC_ROWS64] += 1;
+      if (long_docs) L.kcount[STC_KC_ROWS64_LONG] += 1;
       lda::launch_estep_rows64(s, w, stats, bound, long_docs);
     }
   }
   if (n > n_short) {
     a.slot0 = n_short;
     a.n = n - n_short;
+    L.kcount[STC_KC_WORKGROUP] += 1;
     lda::launch_estep<T>(s, a, stats, bound);
   }
 }
@@ -677,7 +758,7 @@ const T* upload_gamma0(stc_lda& L, const double* gamma0, int64_t n) {
   }
   L.g0.reserve(sizeof(T) * h.size());
   HIP_CHECK(hipMemcpyAsync(L.g0.p, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice, L.ctx->stream));
-  HIP_CHECK(hipStreamSynchronize(L.ctx->stream));  // h dies at scope exit
+  wait_stream(*L.ctx, L.ctx->stream);  // h dies at scope exit
   return L.g0.as<T>();
 }
 
@@ -829,6 +910,9 @@ void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
   hipStream_t s = c.stream;
   const bool ranks = sharded(L);
   const lda::StatMap lay = stat_layout(L);
+  if (L.tail_fault > 0 && --L.tail_fault == 0) {
+    throw Error(STC_ERR_STATE, "injected member failure between sstats and the reduce-scatter (STC_GROUP_STEP_FAULT)");
+  }
   const bool had_samp = L.samp_pending;
   if (L.samp_pending) {  // the next draw's counts (side stream) feed this step's collective / readback
     HIP_CHECK(hipStreamWaitEvent(s, L.ev_samp, 0));
@@ -949,9 +1033,11 @@ void train_finish(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
   if (st) {
     int64_t h4[4] = {0, 0, 0, 0};
     double ne = 0.0;
+    // a copy to pageable memory can block in the runtime: behind collectives, wait (polling) first
+    if (L.ctx->comm) wait_stream(*L.ctx, s);
     HIP_CHECK(hipMemcpyAsync(h4, L.stats4.p, sizeof(h4), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(&ne, L.small.as<double>() + L.k, sizeof(double), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(*L.ctx, s);
     st->batch_docs = n;
     st->batch_entries = E;
     st->inner_iters = h4[0];
@@ -1005,7 +1091,7 @@ void step_ids(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, s
 void settle_side(stc_lda& L) {
   if (!L.samp_pending) return;
   L.ctx->use();
-  HIP_CHECK(hipStreamSynchronize(L.side));
+  wait_stream(*L.ctx, L.side);
   L.samp_pending = false;
   L.pre_inflight = false;
   L.pre_valid = false;
@@ -1066,13 +1152,13 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
   const bool prefetched = L.pre_valid && L.pre_draw == draw;
   const bool on_side = prefetched && L.prep_side && L.side && L.ev_est;
   if (prefetched) {
-    HIP_CHECK(hipEventSynchronize(L.ev_pre));
+    wait_event(*L.ctx, L.ev_pre);
     std::copy(L.hpre, L.hpre + 4, cnt);
   } else {
     sample_draw(L, draw, s, &L.scan_tmp);
     if (c.coll()) coll_all_reduce(c, L.dcnt.as<int64_t>() + 3, 1, ncclInt64, s);
     HIP_CHECK(hipMemcpyAsync(L.hcnt, L.dcnt.p, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(*L.ctx, s);
     std::copy(L.hcnt, L.hcnt + 4, cnt);
   }
   L.pre_valid = false;
@@ -1121,8 +1207,9 @@ void estep_only(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0,
   ensure_order(L);
   hipStream_t s = L.ctx->stream;
   const Part p = upload_members<T>(L, ids, n);
+  // γ₀ drawn inside the E-step kernel when not injected (no n×k buffer: ADVICE r5); the pre-drawn form
+  // (gen_gamma0) is used only by the training steps, where it was measured to help
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
-  if (!g0) g0 = gen_gamma0<T>(L, s, n, L.cfg.seed, L.iteration + 1, 0, 0);
   const bool t = L.timing;
   L.timing = false;
   estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1);
@@ -1130,7 +1217,7 @@ void estep_only(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0,
   if (gamma_out && n > 0) {
     std::vector<T> g((size_t)(n * L.k));
     HIP_CHECK(hipMemcpyAsync(g.data(), L.gamma.p, sizeof(T) * g.size(), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(*L.ctx, s);
     for (size_t j = 0; j < g.size(); ++j) gamma_out[j] = (double)g[j];
   }
   if (iters_out && n > 0) {
@@ -1142,7 +1229,7 @@ void estep_only(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0,
                                 L.dtmp.as<double>());
     HIP_CHECK(hipMemcpyAsync(stat_out, L.dtmp.p, sizeof(double) * L.V * L.k, hipMemcpyDeviceToHost, s));
   }
-  HIP_CHECK(hipStreamSynchronize(s));
+  wait_stream(*L.ctx, s);
 }
 
 template <typename T>
@@ -1158,8 +1245,7 @@ void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const
   L.bound.reserve(sizeof(double) * std::max<int64_t>(n, 1));
   L.scal.reserve(sizeof(double) * 8);
   const Part p = partition(L, docs.indptr.as<int64_t>(), nullptr, n);
-  const T* g0 = upload_gamma0<T>(L, gamma0, n);
-  if (!g0) g0 = gen_gamma0<T>(L, s, n, seed, 0, 1, base);
+  const T* g0 = upload_gamma0<T>(L, gamma0, n);  // nullptr: drawn inside the E-step kernel (as estep_only)
   lda::EStepArgs<T> a = estep_args<T>(L);
   a.indptr = docs.indptr.as<int64_t>();
   a.indices = docs.indices.as<int32_t>();
@@ -1179,7 +1265,7 @@ void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const
   if (gamma_out && n > 0) {
     std::vector<T> g((size_t)(n * L.k));
     HIP_CHECK(hipMemcpyAsync(g.data(), L.gamma.p, sizeof(T) * g.size(), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(*L.ctx, s);
     for (size_t j = 0; j < g.size(); ++j) gamma_out[j] = (double)g[j];
   }
   if (bound) {
@@ -1188,7 +1274,7 @@ void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const
     if (n > 0) lda::launch_sum_f64(s, L.bound.as<double>(), n, L.scal.as<double>());
     if (docs.nnz > 0) lda::launch_sum_vals<T>(s, docs.values.as<T>(), docs.nnz, L.scal.as<double>() + 1);
     HIP_CHECK(hipMemcpyAsync(h, L.scal.p, sizeof(double) * 2, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(*L.ctx, s);
     out4[0] = h[0];
     out4[1] = h[1];
   }
@@ -1201,7 +1287,7 @@ void gather_lambda(stc_lda& L) {
   Ctx& c = *L.ctx;
   const size_t cnt = (size_t)(L.Vs * L.k);
   coll_all_gather(c, L.lam.as<double>() + (size_t)c.rank * cnt, L.lam.p, cnt, ncclFloat64, c.stream);
-  HIP_CHECK(hipStreamSynchronize(c.stream));
+  wait_stream(c, c.stream);
   L.lam_stale = false;
 }
 
@@ -1228,7 +1314,7 @@ void topics_part(stc_lda& L, double* elem_part, double* norm_part) {
   std::vector<double> cs((size_t)L.k);
   HIP_CHECK(hipMemcpyAsync(&part, L.scal.as<double>() + 3, sizeof(double), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipMemcpyAsync(cs.data(), L.colsum.p, sizeof(double) * L.k, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipStreamSynchronize(s));
+  wait_stream(*L.ctx, s);
   // sumEta = η·V (Dirichlet normaliser of q(β_k|λ_k) minus that of p(β_k|η))
   const double lg_sum_eta = std::lgamma(L.eta * (double)L.V);
   double norm = 0.0;
@@ -1244,7 +1330,7 @@ void allreduce_host(Ctx& c, double* x, int64_t n) {
   HIP_CHECK(hipMemcpyAsync(d.p, x, sizeof(double) * n, hipMemcpyHostToDevice, c.stream));
   coll_all_reduce(c, d.p, (size_t)n, ncclFloat64, c.stream);
   HIP_CHECK(hipMemcpyAsync(x, d.p, sizeof(double) * n, hipMemcpyDeviceToHost, c.stream));
-  HIP_CHECK(hipStreamSynchronize(c.stream));
+  wait_stream(c, c.stream);
 }
 
 void check_csr_host(int64_t rows, int64_t cols, const int64_t* indptr, const int32_t* indices) {
@@ -1299,6 +1385,8 @@ int stc_init(int device, stc_ctx** out) {
     if (tm && tm[0] >= '0' && tm[0] <= '2' && tm[1] == 0) c->tf_mode = tm[0] - '0';
     const char* tf = std::getenv("STC_TF_FAULT");  // test knob
     c->tf_force_fault = tf && tf[0] == '1';
+    const char* ct = std::getenv("STC_COLL_TIMEOUT_MS");  // the deadline of a wait behind RCCL collectives
+    if (ct && std::atoll(ct) > 0) c->coll_timeout_ms = std::atoll(ct);
     const char* nc = std::getenv("STC_IDF_NO_CACHE");  // A/B knob: plain idf gathers in the transform
     c->idf_cache = !(nc && nc[0] == '1');
     *out = c.release();
@@ -1313,7 +1401,9 @@ int stc_destroy(stc_ctx* ctx) {
       g_live.erase(ctx);
     }
     (void)hipSetDevice(ctx->device);
-    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    // an aborted communicator is already freed; a live one is destroyed (a group's members first settle
+    // their streams in stc_group_destroy, so nothing of it is still queued)
+    if (ctx->comm && !ctx->comm_aborted.load()) (void)ncclCommDestroy(ctx->comm);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
   });
@@ -1323,7 +1413,7 @@ int stc_synchronize(stc_ctx* ctx) {
   return guard([&] {
     STC_REQUIRE(ctx, "ctx");
     ctx->use();
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    wait_stream(*ctx, ctx->stream);
   });
 }
 
@@ -1385,15 +1475,15 @@ int stc_dcsr_upload(stc_ctx* ctx, int64_t n_rows, int64_t n_cols, const int64_t*
       HIP_CHECK(hipMemcpyAsync(m->indices.p, indices, 4 * nnz, hipMemcpyHostToDevice, ctx->stream));
       if (value_dtype == STC_F64) {
         HIP_CHECK(hipMemcpyAsync(m->values.p, values, 8 * nnz, hipMemcpyHostToDevice, ctx->stream));
-        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        wait_stream(*ctx, ctx->stream);
       } else {
         std::vector<float> f((size_t)nnz);
         for (int64_t e = 0; e < nnz; ++e) f[(size_t)e] = (float)values[e];
         HIP_CHECK(hipMemcpyAsync(m->values.p, f.data(), 4 * nnz, hipMemcpyHostToDevice, ctx->stream));
-        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        wait_stream(*ctx, ctx->stream);
       }
     }
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    wait_stream(*ctx, ctx->stream);
     *out = m.release();
   });
 }
@@ -1421,11 +1511,11 @@ int stc_dcsr_download(stc_ctx* ctx, const stc_dcsr* m, int64_t* indptr, int32_t*
       } else {
         std::vector<float> f((size_t)m->nnz);
         HIP_CHECK(hipMemcpyAsync(f.data(), m->values.p, 4 * m->nnz, hipMemcpyDeviceToHost, s));
-        HIP_CHECK(hipStreamSynchronize(s));
+        wait_stream(*ctx, s);
         for (int64_t e = 0; e < m->nnz; ++e) values[e] = f[(size_t)e];
       }
     }
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(*ctx, s);
   });
 }
 
@@ -1433,13 +1523,14 @@ int stc_dcsr_free(stc_dcsr* m) {
   return guard([&] {
     if (!m) return;
     if (m->device >= 0) (void)hipSetDevice(m->device);
+    // every queued reader first — the context's stream and any other (an LDA handle's side stream sampling
+    // from this corpus): a recycled buffer is rewritten by the next taker, so the implicit device
+    // synchronisation hipFree gives is kept — outside the process-wide lock, so frees and
+    // creates in other threads (a group's members, other devices) do not queue behind this drain
+    if (m->device >= 0) (void)hipDeviceSynchronize();
     {  // hand the allocations back to the context that made it, if it still exists (Recycler)
       std::lock_guard<std::mutex> lk(g_live_mu);
       if (m->ctx && g_live.count(static_cast<stc_ctx*>(m->ctx)) && m->ctx->device == m->device) {
-        // every queued reader first — the context's stream and any other (an LDA handle's side stream
-        // sampling from this corpus): a recycled buffer is rewritten by the next taker, so the implicit
-        // device synchronisation hipFree used to give is kept
-        (void)hipDeviceSynchronize();
         m->ctx->recycle.put(m->indices);
         m->ctx->recycle.put(m->values);
         m->ctx->recycle.put(m->indptr);
@@ -1490,13 +1581,13 @@ int stc_tokens_upload(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const 
     t->device = ctx->device;
     TokenUpload u;
     upload_tokens(*ctx, u, utf8, n_bytes, tok_off, n_tok, doc_off, n_docs);
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    wait_stream(*ctx, ctx->stream);
     std::swap(t->utf8.p, u.utf8.p);
     std::swap(t->utf8.bytes, u.utf8.bytes);
     if (n_bytes + kHashPad <= (int64_t(1) << 32)) {  // u32 offsets: half the bytes HashingTF reads for them
       t->tok_off.reserve(4 * (n_tok + 1));
       hashing::narrow_offsets(*ctx, u.tok_off.as<int64_t>(), n_tok + 1, t->tok_off.as<uint32_t>());
-      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      wait_stream(*ctx, ctx->stream);
       t->off32 = true;
     } else {
       std::swap(t->tok_off.p, u.tok_off.p);
@@ -1554,7 +1645,7 @@ int stc_hash_tokens(stc_ctx* ctx, const uint8_t* utf8, int64_t n_bytes, const in
     hashing::hash_tokens(*ctx, u.utf8.as<uint8_t>(), u.tok_off.as<int64_t>(), n_tok, num_features,
                          hash_variant, out.as<int32_t>());
     if (n_tok) HIP_CHECK(hipMemcpyAsync(idx_out, out.p, 4 * n_tok, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    wait_stream(*ctx, ctx->stream);
   });
 }
 
@@ -1618,12 +1709,18 @@ int stc_tokenize(stc_ctx* ctx, const uint8_t* text, int64_t n_bytes, const int64
                  int64_t n_docs, uint8_t* utf8_out, int64_t utf8_cap, int64_t* n_out_bytes,
                  int64_t* tok_off_out, int64_t* n_tok_out, int64_t* doc_off_out) {
   return guard([&] {
-    STC_REQUIRE(ctx && n_out_bytes && n_tok_out && tok_off_out && doc_off_out && (utf8_out || utf8_cap == 0),
-                "ctx/outputs");
+    STC_REQUIRE(ctx && n_out_bytes, "ctx/n_out_bytes");
     STC_REQUIRE(utf8_cap >= 0, "utf8_cap must be >= 0");
+    const bool query = utf8_out == nullptr;  // the size query: *n_out_bytes (and *n_tok_out) only
+    STC_REQUIRE(query ? utf8_cap == 0 : (n_tok_out && tok_off_out && doc_off_out), "outputs");
     ctx->use();
     Tokens t;
     run_tokenizer(*ctx, t, text, n_bytes, text_off, n_docs);
+    if (query) {
+      *n_out_bytes = t.n_bytes;
+      if (n_tok_out) *n_tok_out = t.n_tok;
+      return;
+    }
     // the lower-cased blob can outgrow the input (İ → i̇, Ⱥ → ⱥ: 2 → 3 bytes); its size is known from the
     // count pass, so a short buffer is refused before anything is copied (*n_out_bytes = the size needed)
     *n_out_bytes = t.n_bytes;
@@ -1634,7 +1731,7 @@ int stc_tokenize(stc_ctx* ctx, const uint8_t* text, int64_t n_bytes, const int64
     if (t.n_bytes) HIP_CHECK(hipMemcpyAsync(utf8_out, t.utf8.p, t.n_bytes, hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(tok_off_out, t.tok_off.p, 8 * (t.n_tok + 1), hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipMemcpyAsync(doc_off_out, t.doc_off.p, 8 * (n_docs + 1), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(*ctx, s);
     *n_out_bytes = t.n_bytes;
     *n_tok_out = t.n_tok;
   });
@@ -1694,7 +1791,7 @@ void idf_fit_impl(Ctx& c, const DCsr& tf, int64_t min_doc_freq, DevBuf& df, DevB
     coll_all_reduce(c, mm.p, 1, ncclInt64, s);
     coll_group_end(c);
     HIP_CHECK(hipMemcpyAsync(&m, mm.p, 8, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(c, s);
   }
   idf::finalize(c, df.as<int64_t>(), tf.cols, m, min_doc_freq, idf.as<double>());
 }
@@ -1716,7 +1813,7 @@ int stc_idf_fit(stc_ctx* ctx, const stc_dcsr* tf, int64_t min_doc_freq, double* 
     idf_fit_impl(*ctx, *tf, min_doc_freq, df, idf, m);
     HIP_CHECK(hipMemcpyAsync(idf_out, idf.p, 8 * tf->cols, hipMemcpyDeviceToHost, s));
     if (df_out) HIP_CHECK(hipMemcpyAsync(df_out, df.p, 8 * tf->cols, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(*ctx, s);
     if (m_out) *m_out = m;
   });
 }
@@ -1745,7 +1842,7 @@ int stc_idf_get(stc_ctx* ctx, const stc_didf* md, double* idf_out, int64_t* df_o
     hipStream_t s = ctx->stream;
     if (idf_out) HIP_CHECK(hipMemcpyAsync(idf_out, md->idf.p, 8 * md->cols, hipMemcpyDeviceToHost, s));
     if (df_out) HIP_CHECK(hipMemcpyAsync(df_out, md->df.p, 8 * md->cols, hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(*ctx, s);
     if (m_out) *m_out = md->m;
   });
 }
@@ -1766,7 +1863,7 @@ int stc_idf_transform_dev(stc_ctx* ctx, stc_dcsr* tf, const stc_didf* md, double
     STC_REQUIRE(zero_floor >= 0.0, "zero_floor must be >= 0");
     ctx->use();
     idf::transform(*ctx, *tf, md->idf.as<double>(), zero_floor, &md->cache);
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    wait_stream(*ctx, ctx->stream);
   });
 }
 
@@ -1774,10 +1871,10 @@ int stc_didf_free(stc_didf* md) {
   return guard([&] {
     if (!md) return;
     (void)hipSetDevice(md->device);
+    (void)hipDeviceSynchronize();  // queued readers of the model first, outside the lock (as stc_dcsr_free)
     {  // back to the context that made it, if it still exists (Recycler)
       std::lock_guard<std::mutex> lk(g_live_mu);
       if (md->ctx && g_live.count(static_cast<stc_ctx*>(md->ctx)) && md->ctx->device == md->device) {
-        (void)hipDeviceSynchronize();  // queued readers of the model first (as stc_dcsr_free)
         md->ctx->recycle.put(md->idf);
         md->ctx->recycle.put(md->df);
       }
@@ -1796,7 +1893,7 @@ int stc_idf_transform(stc_ctx* ctx, stc_dcsr* tf, const double* idf, double zero
     d.reserve(8 * tf->cols);
     HIP_CHECK(hipMemcpyAsync(d.p, idf, 8 * tf->cols, hipMemcpyHostToDevice, ctx->stream));
     idf::transform(*ctx, *tf, d.as<double>(), zero_floor);
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    wait_stream(*ctx, ctx->stream);
   });
 }
 
@@ -1901,7 +1998,7 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->cum2.reserve(8 * 2);
     HIP_CHECK(hipMemsetAsync(L->cum2.p, 0, 16, ctx->stream));
     HIP_CHECK(hipMemcpyAsync(L->alpha.p, alpha.data(), 8 * L->k, hipMemcpyHostToDevice, ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    wait_stream(*ctx, ctx->stream);
     for (auto& s : L->ev)
       for (auto& e : s) HIP_CHECK(hipEventCreate(&e));
     *out = L.release();
@@ -1912,8 +2009,18 @@ int stc_lda_destroy(stc_lda* lda) {
   return guard([&] {
     if (!lda) return;
     (void)hipSetDevice(lda->ctx->device);
-    (void)hipStreamSynchronize(lda->ctx->stream);
-    if (lda->side) (void)hipStreamSynchronize(lda->side);
+    // queued work first (with a communicator: a bounded wait; a collective that never completes is
+    // aborted with its communicator, which releases its kernels, so the destroy returns)
+    Ctx& c = *lda->ctx;
+    for (hipStream_t q : {c.stream, lda->side, lda->cstream}) {
+      if (!q) continue;
+      try {
+        wait_stream(c, q);
+      } catch (const Error&) {
+        abort_comm(c);
+      }
+      (void)hipStreamSynchronize(q);
+    }
     delete lda;
   });
 }
@@ -1945,7 +2052,7 @@ int stc_lda_init_random(stc_lda* L, uint64_t seed) {
     L->iteration = 0;
     L->draws = 0;  // a fresh generator, as Spark's initialize()
     L->pre_valid = false;
-    HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+    wait_stream(*L->ctx, L->ctx->stream);
   });
 }
 
@@ -1965,7 +2072,7 @@ int stc_lda_set_topics(stc_lda* L, const double* topics, int layout) {
     HIP_CHECK(hipMemcpyAsync(L->lam.p, h.data(), 8 * n, hipMemcpyHostToDevice, L->ctx->stream));
     L->lam_stale = false;
     refresh(*L);
-    HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+    wait_stream(*L->ctx, L->ctx->stream);
   });
 }
 
@@ -1979,11 +2086,11 @@ int stc_lda_get_topics(stc_lda* L, double* out, int layout) {
     const int64_t n = L->V * L->k;
     if (layout == STC_LAYOUT_VK) {
       HIP_CHECK(hipMemcpyAsync(out, L->lam.p, 8 * n, hipMemcpyDeviceToHost, L->ctx->stream));
-      HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+      wait_stream(*L->ctx, L->ctx->stream);
     } else {
       std::vector<double> h((size_t)n);
       HIP_CHECK(hipMemcpyAsync(h.data(), L->lam.p, 8 * n, hipMemcpyDeviceToHost, L->ctx->stream));
-      HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+      wait_stream(*L->ctx, L->ctx->stream);
       for (int64_t v = 0; v < L->V; ++v)
         for (int t = 0; t < L->k; ++t) out[(int64_t)t * L->V + v] = h[(size_t)(v * L->k + t)];
     }
@@ -1996,7 +2103,7 @@ int stc_lda_set_alpha(stc_lda* L, const double* alpha) {
     for (int t = 0; t < L->k; ++t) STC_REQUIRE(alpha[t] >= 0, "alpha entries must be >= 0");
     L->ctx->use();
     HIP_CHECK(hipMemcpyAsync(L->alpha.p, alpha, 8 * L->k, hipMemcpyHostToDevice, L->ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+    wait_stream(*L->ctx, L->ctx->stream);
   });
 }
 
@@ -2005,7 +2112,7 @@ int stc_lda_get_alpha(stc_lda* L, double* alpha_out) {
     STC_REQUIRE(L && alpha_out, "lda/alpha_out");
     L->ctx->use();
     HIP_CHECK(hipMemcpyAsync(alpha_out, L->alpha.p, 8 * L->k, hipMemcpyDeviceToHost, L->ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+    wait_stream(*L->ctx, L->ctx->stream);
   });
 }
 
@@ -2146,7 +2253,7 @@ int stc_lda_describe(stc_lda* L, int32_t max_terms, int32_t* idx_out, double* we
       HIP_CHECK(hipMemcpyAsync(weight_out + (int64_t)t * N, kv_s.as<double>() + (int64_t)t * L->V, 8 * N,
                                hipMemcpyDeviceToHost, s));
     }
-    HIP_CHECK(hipStreamSynchronize(s));
+    wait_stream(*L->ctx, s);
     for (int t = 0; t < L->k; ++t)  // normalize(topic, 1.0): v / ‖v‖₁ (λ > 0)
       for (int j = 0; j < N; ++j) weight_out[(int64_t)t * N + j] /= cs[(size_t)t];
   });
@@ -2162,11 +2269,18 @@ int stc_lda_enable_timing(stc_lda* L, int on) {
   });
 }
 
+int stc_lda_kernel_counts(stc_lda* L, int64_t out[STC_KC_N]) {
+  return guard([&] {
+    STC_REQUIRE(L && out, "lda/out");
+    std::copy(L->kcount, L->kcount + STC_KC_N, out);
+  });
+}
+
 int stc_lda_phase_times(stc_lda* L, double* ms_out, int64_t* steps_out) {
   return guard([&] {
     STC_REQUIRE(L && ms_out, "lda/ms_out");
     L->ctx->use();
-    HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+    wait_stream(*L->ctx, L->ctx->stream);
     harvest_all(*L);
     for (int p = 0; p < 5; ++p) ms_out[p] = L->timed_steps ? L->acc_ms[p] / (double)L->timed_steps : 0.0;
     if (steps_out) *steps_out = L->timed_steps;
@@ -2179,7 +2293,7 @@ int stc_lda_counters(stc_lda* L, int64_t out[4]) {
     L->ctx->use();
     int64_t c2[2] = {0, 0};
     HIP_CHECK(hipMemcpyAsync(c2, L->cum2.p, 16, hipMemcpyDeviceToHost, L->ctx->stream));
-    HIP_CHECK(hipStreamSynchronize(L->ctx->stream));
+    wait_stream(*L->ctx, L->ctx->stream);
     out[0] = L->cum_docs;
     out[1] = L->cum_entries;
     out[2] = c2[0];
@@ -2206,6 +2320,12 @@ struct stc_group {
   int dtype = STC_F64;
   int transport = STC_TRANSPORT_NONE;  // how the members' collectives travel (stc_group_transport)
   bool threaded = false;               // run even a one-member call on its own host thread (STC_GROUP_RCCL)
+  // RCCL fault handling: a member's failure sets `abort` (every member's waits then throw instead of waiting
+  // on collectives the failed member never joins) and, after the call, aborts every member's communicator;
+  // the group is then `broken`: every later call but destroy fails with STC_ERR_STATE
+  std::atomic<bool> abort{false};
+  bool broken = false;
+  std::string broken_why;
   int n() const { return (int)ctx.size(); }
 };
 
@@ -2214,13 +2334,27 @@ namespace {
 void member_ok(int rc) {
   if (rc != STC_OK) throw Error(rc, stc_last_error());
 }
-// f(i) for every member on its own thread (device set); the first failure is rethrown here
+void require_usable(const stc_group& g) {
+  if (g.broken) throw Error(STC_ERR_STATE, "the group's RCCL communicator was aborted after a member failed (" +
+                                               g.broken_why + "): destroy the group and create a new one");
+}
+// f(i) for every member on its own thread (device set); the first failure is rethrown here.
+// In-process transport: a failure releases the members waiting in its barrier, and the group stays usable.
+// RCCL: a failure sets the group's abort flag, so every member's next wait throws instead of waiting for a
+// collective the failed member never enqueued; a member still blocked inside the runtime after a grace
+// period (a copy queued behind such a collective) has its communicator aborted by this thread, which
+// releases the collective's kernels; after the join every member's communicator is aborted and the group
+// is broken (STC_ERR_STATE from then on; stc_group_destroy returns).
 template <typename F>
 void for_members(stc_group& g, F f) {
+  require_usable(g);
   const int n = g.n();
+  const bool rccl = g.transport == STC_TRANSPORT_RCCL;
   std::vector<std::exception_ptr> err((size_t)n);
   std::mutex fm;
+  std::condition_variable fcv;
   int first = -1;  // the member that failed first (the others may only report "another member failed")
+  int running = n;
   auto run = [&](int i) {
     try {
       g.ctx[(size_t)i]->use();
@@ -2232,7 +2366,11 @@ void for_members(stc_group& g, F f) {
         if (first < 0) first = i;
       }
       if (g.local) g.local->fail();  // release the members waiting in a barrier
+      if (rccl) g.abort.store(true);
     }
+    std::lock_guard<std::mutex> lk(fm);
+    --running;
+    fcv.notify_all();
   };
   if (n == 1 && !g.threaded) {
     run(0);
@@ -2240,6 +2378,12 @@ void for_members(stc_group& g, F f) {
     std::vector<std::thread> th;
     th.reserve((size_t)n);
     for (int i = 0; i < n; ++i) th.emplace_back(run, i);
+    if (rccl) {
+      std::unique_lock<std::mutex> lk(fm);
+      fcv.wait(lk, [&] { return running == 0 || first >= 0; });
+      if (running > 0 && !fcv.wait_for(lk, std::chrono::seconds(5), [&] { return running == 0; }))
+        for (auto* c : g.ctx) abort_comm(*c);  // members still blocked behind the failed member's collectives
+    }
     for (auto& t : th) t.join();
   }
   if (g.local) {  // a failed call leaves the transport usable for the next one
@@ -2247,7 +2391,23 @@ void for_members(stc_group& g, F f) {
     g.local->broken = false;
     g.local->arrived = 0;
   }
-  if (first >= 0) std::rethrow_exception(err[(size_t)first]);
+  if (first >= 0) {
+    if (rccl) {
+      for (auto* c : g.ctx) {
+        c->use();
+        abort_comm(*c);
+      }
+      g.broken = true;
+      try {
+        std::rethrow_exception(err[(size_t)first]);
+      } catch (const std::exception& e) {
+        g.broken_why = "member " + std::to_string(first) + ": " + e.what();
+      } catch (...) {
+        g.broken_why = "member " + std::to_string(first);
+      }
+    }
+    std::rethrow_exception(err[(size_t)first]);
+  }
 }
 // contiguous row ranges of a host CSR, one per member, balanced by entries
 std::vector<int64_t> shard_rows(const int64_t* indptr, int64_t rows, int n) {
@@ -2334,10 +2494,19 @@ int stc_group_create(const int* device_ids, int n_devices, const stc_lda_config*
         g->ctx[(size_t)i]->rank = i;
       }
     }
+    for (auto* c : g->ctx) c->abort_flag = &g->abort;
+    // test knob STC_GROUP_STEP_FAULT=i[:s]: member i's s-th step (default the first) fails, after its E-step
+    // and sstats and before its reduce-scatter (its peers' collectives then never complete: the RCCL
+    // failure path)
+    const char* sf = getenv("STC_GROUP_STEP_FAULT");
+    const int step_fault = sf && sf[0] ? atoi(sf) : -1;
+    const char* sfc = sf ? std::strchr(sf, ':') : nullptr;
+    const int step_fault_at = sfc ? std::max(1, atoi(sfc + 1)) : 1;
     for (int i = 0; i < n_devices; ++i) {
       stc_lda* l = nullptr;
       member_ok(stc_lda_create(g->ctx[(size_t)i], cfg, &l));
       if (rccl1) l->force_coll = true;  // the sliced M-step and its collectives on a 1-rank communicator too
+      l->tail_fault = i == step_fault ? step_fault_at : 0;
       g->lda.push_back(l);
     }
     g->dtype = g->lda[0]->dtype;
@@ -2421,11 +2590,12 @@ int stc_group_set_corpus(stc_group* g, int64_t n_rows, int64_t n_cols, const int
 int stc_group_release_corpus(stc_group* g) {
   return guard([&] {
     STC_REQUIRE(g, "group");
+    require_usable(*g);
     for (int i = 0; i < g->n(); ++i) {
       stc_lda* l = g->lda[(size_t)i];
       g->ctx[(size_t)i]->use();
       settle_side(*l);
-      HIP_CHECK(hipStreamSynchronize(g->ctx[(size_t)i]->stream));
+      wait_stream(*g->ctx[(size_t)i], g->ctx[(size_t)i]->stream);
       l->corpus = nullptr;
       l->order_for = nullptr;
       l->pre_valid = false;
@@ -2464,6 +2634,7 @@ int stc_group_get_topics(stc_group* g, double* topics_out, int layout) {
 int stc_group_get_alpha(stc_group* g, double* alpha_out) {
   return guard([&] {
     STC_REQUIRE(g && alpha_out, "group/alpha_out");
+    require_usable(*g);
     g->ctx[0]->use();
     member_ok(stc_lda_get_alpha(g->lda[0], alpha_out));  // α is replicated on every member
   });
@@ -2479,10 +2650,11 @@ int stc_group_get_iteration(stc_group* g, int64_t* iteration_out) {
 int stc_group_synchronize(stc_group* g) {
   return guard([&] {
     STC_REQUIRE(g, "group");
+    require_usable(*g);
     for (int i = 0; i < g->n(); ++i) {
       g->ctx[(size_t)i]->use();
-      HIP_CHECK(hipStreamSynchronize(g->ctx[(size_t)i]->stream));
-      if (g->lda[(size_t)i]->side) HIP_CHECK(hipStreamSynchronize(g->lda[(size_t)i]->side));  // the next draw
+      wait_stream(*g->ctx[(size_t)i], g->ctx[(size_t)i]->stream);
+      if (g->lda[(size_t)i]->side) wait_stream(*g->ctx[(size_t)i], g->lda[(size_t)i]->side);  // the next draw
     }
   });
 }

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -169,6 +170,13 @@ struct Ctx {
   Recycler recycle;    // freed stc_dcsr allocations for the next outputs (stc_dcsr_free)
   DevBuf scratch[12];  // grow-only scratch of the featurisation kernels (hashing_tf.hip, idf.hip, api.hip IDF)
   DevBuf coll_tmp;    // the in-process all-reduce's staging buffer
+  // RCCL failure handling (api.hip wait_stream / wait_event): with a communicator, every wait on work that
+  // may hold a collective polls with a deadline instead of blocking in the runtime
+  const std::atomic<bool>* abort_flag = nullptr;  // the group's: set once any of its members has failed
+  std::atomic<bool> comm_aborted{false};          // comm was aborted (ncclCommAbort): never used again
+  int64_t coll_timeout_ms = 120000;               // STC_COLL_TIMEOUT_MS (read at stc_init)
+  bool in_group = false;                          // between ncclGroupStart and ncclGroupEnd
+  bool coll_enqueued = false;                     // a collective was ever enqueued (waits poll from then on)
   void use() const { HIP_CHECK(hipSetDevice(device)); }
   bool coll() const { return comm != nullptr || local != nullptr; }
 };

@@ -118,6 +118,7 @@ SIGNATURES = {
     "stc_lda_enable_timing": (_int, [_p, _int]),
     "stc_lda_phase_times": (_int, [_p, _pdbl, _pi64]),
     "stc_lda_counters": (_int, [_p, _pi64]),
+    "stc_lda_kernel_counts": (_int, [_p, _pi64]),
     "stc_group_create": (_int, [_pi32, _int, C.POINTER(LdaConfig), C.POINTER(_p)]),
     "stc_group_destroy": (_int, [_p]),
     "stc_group_size": (_int, [_p, _pi32]),

@@ -67,11 +67,19 @@ def _phase_times(lib, h):
             "steps": steps.value}
 
 
+# stc.h enum stc_kernel_count: the E-step kernel families stc_lda_kernel_counts counts launches of
+KERNEL_FAMILIES = ("k_estep_rows64", "k_estep_rows64_long", "k_estep_grid", "k_estep_wide", "k_estep_wide_mc",
+                   "k_estep_wide_tc", "k_estep_tgrid64", "team_fallback", "k_estep")
+
+
 def _counters(lib, h):
-    """stc_lda_counters of one handle (cumulative since creation)"""
+    """stc_lda_counters + stc_lda_kernel_counts of one handle (cumulative since creation)"""
     out = np.zeros(4, np.int64)
     L.check(lib.stc_lda_counters(h, L.ptr(out, C.c_int64)))
-    return {"docs": int(out[0]), "entries": int(out[1]), "inner_iters": int(out[2]), "cap_hits": int(out[3])}
+    kc = np.zeros(12, np.int64)
+    L.check(lib.stc_lda_kernel_counts(h, L.ptr(kc, C.c_int64)))
+    return {"docs": int(out[0]), "entries": int(out[1]), "inner_iters": int(out[2]), "cap_hits": int(out[3]),
+            "kernels": {f: int(kc[i]) for i, f in enumerate(KERNEL_FAMILIES)}}
 
 
 class LdaHandle:

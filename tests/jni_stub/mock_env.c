@@ -123,10 +123,100 @@ static int gpu_main(JNIEnv* env) {
   return 0;
 }
 
+/* GPU training mode (tests/test_gpu_jni_shim.py): the JNI calls HipOnlineLDAOptimizer makes
+ * (initialize → next × steps → getLDAModel, HipOnlineLDAOptimizer.scala:105-139) and those HipLocalLDAModel
+ * makes afterwards (describeTopics, logLikelihood), in the Scala code's order, over a corpus read from a
+ * binary file.  Input (little-endian): int64 n_dev, n_dev device ids, rows, cols, k, steps, seed, then
+ * double miniBatchFraction, then indptr[rows+1] (int64), indices[nnz] (int32), values[nnz] (double).
+ * Output file: λ (V×k doubles, the k×V row-major getLDAModel reads, LAYOUT_KV), α[k], η, iteration
+ * (as double), the per-step stats (steps×7 doubles), describe(10) indices (k×10 int32) and weights (k×10
+ * doubles), the bound over the training rows {bound, corpus, topics, tokens}, the transport. */
+static long long rd_i64(FILE* f) {
+  long long v = 0;
+  if (fread(&v, 8, 1, f) != 1) exit(3);
+  return v;
+}
+static int gpu_train_main(JNIEnv* env, const char* in_path, const char* out_path) {
+  FILE* f = fopen(in_path, "rb");
+  if (!f) return 2;
+  const long long nd = rd_i64(f);
+  jintArray dev = arr((jsize)nd, 4);
+  for (long long i = 0; i < nd; ++i) ((jint*)dev->data)[i] = (jint)rd_i64(f);
+  const long long rows = rd_i64(f), cols = rd_i64(f), k = rd_i64(f), steps = rd_i64(f), seed = rd_i64(f);
+  double frac = 0;
+  if (fread(&frac, 8, 1, f) != 1) return 3;
+  jlongArray ip = arr((jsize)(rows + 1), 8);
+  if (fread(ip->data, 8, (size_t)(rows + 1), f) != (size_t)(rows + 1)) return 3;
+  const long long nnz = ((jlong*)ip->data)[rows];
+  jintArray ix = arr((jsize)nnz, 4);
+  jdoubleArray vs = arr((jsize)nnz, 8);
+  if (fread(ix->data, 4, (size_t)nnz, f) != (size_t)nnz || fread(vs->data, 8, (size_t)nnz, f) != (size_t)nnz) return 3;
+  fclose(f);
+  /* initialize(): groupCreate (α = −1 ⇒ 1/k, η = −1 ⇒ 1/k), groupSetCorpus, groupInitRandom(seed) */
+  jdoubleArray alpha_in = arr(1, 8);
+  ((jdouble*)alpha_in->data)[0] = -1.0;
+  jlong g = FN(groupCreate)(env, NULL, dev, (jint)k, cols, alpha_in, -1.0, 1024.0, 0.51, frac, 100.0, 1, 0, seed, 1, 0);
+  report("groupCreate");
+  if (!g) return 1;
+  FN(groupSetCorpus)(env, NULL, g, rows, cols, ip, ix, vs);
+  report("groupSetCorpus");
+  FN(groupInitRandom)(env, NULL, g, seed);
+  report("groupInitRandom");
+  /* next() × steps (with the stats array, as a caller that logs them) */
+  jdoubleArray st = arr(7, 8);
+  double* stats = calloc((size_t)steps * 7, 8);
+  int next_ok = 1;
+  for (long long s = 0; s < steps; ++s) {
+    FN(groupNext)(env, NULL, g, st);
+    if (g_thrown) next_ok = 0;
+    report("groupNext");
+    memcpy(stats + 7 * s, st->data, 7 * 8);
+  }
+  /* getLDAModel(): topics (k×V row-major), α, η of member 0, then the corpus released */
+  jdoubleArray topics = arr((jsize)(cols * k), 8), alpha = arr((jsize)k, 8);
+  FN(groupGetTopics)(env, NULL, g, topics, 1 /* LAYOUT_KV */);
+  report("groupGetTopics");
+  FN(groupGetAlpha)(env, NULL, g, alpha);
+  report("groupGetAlpha");
+  const jdouble eta = FN(ldaGetEta)(env, NULL, FN(groupMember)(env, NULL, g, 0));
+  report("ldaGetEta");
+  const double iteration = (double)FN(groupGetIteration)(env, NULL, g);
+  report("groupGetIteration");
+  FN(groupReleaseCorpus)(env, NULL, g);
+  report("groupReleaseCorpus");
+  /* HipLocalLDAModel: describeTopics(10), logLikelihood over the training rows (γ₀ seed 9, ids from 0) */
+  jintArray didx = arr((jsize)(k * 10), 4);
+  jdoubleArray dw = arr((jsize)(k * 10), 8);
+  FN(groupDescribe)(env, NULL, g, 10, didx, dw);
+  report("groupDescribe");
+  jdoubleArray b = FN(groupBound)(env, NULL, g, rows, cols, ip, ix, vs, 9, 0, NULL);
+  report("groupBound");
+  const double tr = (double)FN(groupTransport)(env, NULL, g);
+  FN(groupDestroy)(env, NULL, g);
+  report("groupDestroy");
+  FILE* o = fopen(out_path, "wb");
+  if (!o) return 2;
+  fwrite(topics->data, 8, (size_t)(cols * k), o);
+  fwrite(alpha->data, 8, (size_t)k, o);
+  fwrite(&eta, 8, 1, o);
+  fwrite(&iteration, 8, 1, o);
+  fwrite(stats, 8, (size_t)steps * 7, o);
+  fwrite(didx->data, 4, (size_t)(k * 10), o);
+  fwrite(dw->data, 8, (size_t)(k * 10), o);
+  double bz[4] = {0, 0, 0, 0};
+  if (b) memcpy(bz, b->data, sizeof bz);
+  fwrite(bz, 8, 4, o);
+  fwrite(&tr, 8, 1, o);
+  fclose(o);
+  free(stats);
+  return next_ok ? 0 : 4;
+}
+
 int main(int argc, char** argv) {
   JNIEnv env_ = &table;
   JNIEnv* env = &env_;
   if (argc > 1 && strcmp(argv[1], "gpu") == 0) return gpu_main(env);
+  if (argc > 3 && strcmp(argv[1], "gpu_train") == 0) return gpu_train_main(env, argv[2], argv[3]);
   /* 3 tokens "ab","c","" in 2 documents */
   jbyteArray utf8 = arr(3, 1);
   memcpy(utf8->data, "abc", 3);

@@ -63,7 +63,7 @@ class FakeGroup:
     def counters(self):
         n = len(self.devices)
         return [{"docs": 10 * self.steps, "entries": 1000 * self.steps, "inner_iters": 50 * self.steps,
-                 "cap_hits": 0} for _ in range(n)]
+                 "cap_hits": 0, "kernels": {"k_estep_rows64": self.steps, "k_estep": 0}} for _ in range(n)]
 
     def phase_times(self):
         return [{"sample": 0.1, "estep": 1.0 + i, "sstats": 0.2, "allreduce": 0.3, "mstep": 0.1, "steps": 5}
@@ -104,6 +104,15 @@ def test_gpus_n_without_launcher_drives_a_group(monkeypatch, capsys):
     assert split["estep"]["algorithmic_bytes"] + split["sstats"]["algorithmic_bytes"] == pytest.approx(
         line["roofline"]["algorithmic_bytes_per_launch"])
     assert line["parity"].startswith("north-star bars met")  # the fp64 headline
+    # the kernel named is the one the library counted as launched in the timed steps
+    assert line["roofline"]["kernel"].startswith("k_estep_rows64_pers")
+
+
+def test_kernel_name_comes_from_the_launch_counters():
+    assert bench.kernel_name({"k_estep_wide": 20}).startswith("k_estep_wide (")
+    n = bench.kernel_name({"k_estep_tgrid64": 19, "k_estep_wide": 1, "team_fallback": 1})
+    assert n.startswith("k_estep_tgrid64") and "team_fallback" in n
+    assert bench.kernel_name({}) == "no E-step launch in the timed steps"
 
 
 def test_group_launch_at_one_gpu(monkeypatch, capsys):

@@ -373,3 +373,115 @@ def test_chunked_reduce_scatter_long_runs(ctx, monkeypatch, dtype):
     for a, b in zip(out["4"][:2], out["1"][:2]):
         np.testing.assert_array_equal(a, b)
     assert out["4"][2] == out["1"][2]
+
+
+# ---- the RCCL group is fail-safe before the first multi-GPU run.  A member that throws
+# mid-step leaves its peers' collectives without a partner; the group must abort every communicator
+# (ncclCommAbort), report the failure, refuse later calls and still be destroyable, and a stuck wait must
+# end at a deadline (STC_COLL_TIMEOUT_MS) instead of hanging the process.
+
+def _destroy_rc(g):
+    rc = g.lib.stc_group_destroy(g.handle)
+    g.handle = None
+    return rc
+
+
+def test_rccl_group_member_failure_aborts_and_a_new_group_trains_bitwise(ctx, monkeypatch):
+    """STC_GROUP_STEP_FAULT=0:3 — the member thread throws on its third step, after E-step + sstats and
+    before the reduce-scatter: that call returns the error, the communicator is aborted, every later call
+    is STC_ERR_STATE, stc_group_destroy returns 0; then a fresh RCCL group trains bit-identically to a
+    plain group (as test_rccl_group_next_bitwise_equals_the_plain_group)."""
+    import time
+
+    import stc
+
+    rng = np.random.default_rng(5)
+    D, V, k = 400, 3000, 9
+    corpus = random_corpus(rng, D, V, 1, 50, empty_every=9)
+    monkeypatch.setenv("STC_GROUP_RCCL", "1")
+    monkeypatch.setenv("STC_GROUP_STEP_FAULT", "0:3")
+    g = stc.LdaGroup([0], k, V, dtype="f64", mini_batch_fraction=0.2, seed=4, optimize_doc_concentration=True)
+    assert g.transport() == "rccl"
+    g.set_corpus(corpus)
+    g.init_random(6)
+    g.next()
+    g.next(stats=False)
+    with pytest.raises(stc.StcError) as e:
+        g.next()
+    assert e.value.code == stc.STC_ERR_STATE and "STC_GROUP_STEP_FAULT" in str(e.value)
+    for call in (g.next, g.topics, g.alpha, g.synchronize):
+        with pytest.raises(stc.StcError) as e:
+            call()
+        assert e.value.code == stc.STC_ERR_STATE and "aborted" in str(e.value)
+    assert g.transport() == "rccl"  # (introspection still answers)
+    t0 = time.perf_counter()
+    assert _destroy_rc(g) == 0
+    assert time.perf_counter() - t0 < 30
+    monkeypatch.delenv("STC_GROUP_STEP_FAULT")
+    runs = []
+    for knob in ("0", "1"):
+        monkeypatch.setenv("STC_GROUP_RCCL", knob)
+        with stc.LdaGroup([0], k, V, dtype="f64", mini_batch_fraction=0.2, seed=4,
+                          optimize_doc_concentration=True) as g2:
+            g2.set_corpus(corpus)
+            g2.init_random(6)
+            for _ in range(6):
+                g2.next(stats=False)
+            runs.append((g2.topics(), g2.alpha(), g2.iteration()))
+    (t0_, a0, i0), (t1, a1, i1) = runs
+    assert i0 == i1 == 6
+    np.testing.assert_array_equal(t1, t0_)
+    np.testing.assert_array_equal(a1, a0)
+
+
+def test_rccl_group_wait_deadline_aborts(ctx, monkeypatch):
+    """STC_COLL_TIMEOUT_MS=1: a step whose device work outlasts the deadline ends as STC_ERR_RCCL (the wait
+    behind the collectives gave up and aborted the communicator) instead of blocking; the group is then
+    refused and destroyable."""
+    import stc
+
+    rng = np.random.default_rng(6)
+    D, V, k = 20000, 4096, 40
+    corpus = random_corpus(rng, D, V, 60, 200)
+    monkeypatch.setenv("STC_GROUP_RCCL", "1")
+    monkeypatch.setenv("STC_COLL_TIMEOUT_MS", "1")
+    g = stc.LdaGroup([0], k, V, dtype="f64", mini_batch_fraction=1.0, seed=4)
+    g.set_corpus(corpus)
+    g.init_random(6)
+    with pytest.raises(stc.StcError) as e:
+        for _ in range(3):
+            g.next()
+    assert e.value.code == stc.STC_ERR_RCCL and "STC_COLL_TIMEOUT_MS" in str(e.value)
+    with pytest.raises(stc.StcError) as e:
+        g.next()
+    assert e.value.code == stc.STC_ERR_STATE
+    assert _destroy_rc(g) == 0
+
+
+def test_rank_communicator_wait_deadline_aborts(monkeypatch):
+    """The torchrun "ranks" form (one context per process, stc_comm_init): the same deadline on its waits —
+    a step that outlasts STC_COLL_TIMEOUT_MS raises STC_ERR_RCCL, the communicator is aborted, a later step
+    is STC_ERR_STATE, and the handle and context still free."""
+    import stc
+
+    rng = np.random.default_rng(7)
+    D, V, k = 20000, 4096, 40
+    corpus = random_corpus(rng, D, V, 60, 200)
+    monkeypatch.setenv("STC_COLL_TIMEOUT_MS", "1")
+    monkeypatch.setenv("STC_COLLECTIVE_MSTEP", "1")
+    c1 = stc.Context(0)
+    c1.comm_init(stc.Context.unique_id(), 1, 0)
+    h = stc.LdaHandle(c1, k, V, mini_batch_fraction=1.0, seed=4, dtype="f64")
+    d = stc.DeviceCsr.upload(c1, corpus, stc.STC_F64)
+    h.set_corpus(d, D)
+    h.init_random(6)
+    with pytest.raises(stc.StcError) as e:
+        for _ in range(3):
+            h.next()
+    assert e.value.code == stc.STC_ERR_RCCL
+    with pytest.raises(stc.StcError) as e:
+        h.next()
+    assert e.value.code == stc.STC_ERR_STATE
+    h.close()
+    d.free()
+    c1.close()

