@@ -155,7 +155,8 @@ static int gpu_train_main(JNIEnv* env, const char* in_path, const char* out_path
   /* initialize(): groupCreate (α = −1 ⇒ 1/k, η = −1 ⇒ 1/k), groupSetCorpus, groupInitRandom(seed) */
   jdoubleArray alpha_in = arr(1, 8);
   ((jdouble*)alpha_in->data)[0] = -1.0;
-  jlong g = FN(groupCreate)(env, NULL, dev, (jint)k, cols, alpha_in, -1.0, 1024.0, 0.51, frac, 100.0, 1, 0, seed, 1, 0);
+  /* sampleWithReplacement = true: HipOnlineLDAOptimizer's (and Spark's) default; optimizeDocConcentration = true: ml LDA's */
+  jlong g = FN(groupCreate)(env, NULL, dev, (jint)k, cols, alpha_in, -1.0, 1024.0, 0.51, frac, 100.0, 1, 1, seed, 1, 0);
   report("groupCreate");
   if (!g) return 1;
   FN(groupSetCorpus)(env, NULL, g, rows, cols, ip, ix, vs);

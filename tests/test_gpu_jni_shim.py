@@ -83,7 +83,8 @@ def _train_through_shim(tmp_path, corpus, devices, k, steps, seed, frac, env=Non
     out = subprocess.run([_mock_exe(tmp_path), "gpu_train", str(inp), str(outp)], capture_output=True, text=True,
                          timeout=240, env=run_env)
     assert out.returncode == 0, out.stdout + out.stderr
-    calls = [line.split("\t") for line in out.stdout.strip().splitlines()]
+    # (RCCL prints its version banner to stdout: only the mock's three-field report lines)
+    calls = [line.split("\t") for line in out.stdout.strip().splitlines() if line.count("\t") == 2]
     for c in calls:
         assert c[1:] == ["-", "-"], c  # no Java exception from any wrapper
     V = corpus.num_cols
