@@ -119,7 +119,7 @@ def estep_sources_sha():
 
 # the featurisation kernels' sources: its PMC entry counts only if measured on these exact files
 FEAT_SOURCES = ("hashing_tf.hip", "idf.hip", "stc_internal.h")
-FEAT_PMC = os.path.join(ROOT, "profiles", "r04_featurisation_pmc.json")
+FEAT_PMC = os.path.join(ROOT, "profiles", "r06_featurisation_pmc.json")
 
 
 def feat_sources_sha():
