@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define STC_ABI_VERSION 1
+#define STC_ABI_VERSION 2  /* 2: stc_lda_config.mixed_resolve_iters, STC_MIXED */
 
 enum stc_status {
   STC_OK = 0,
@@ -68,7 +68,16 @@ enum stc_hash_variant {
   STC_HASH_SPARK24 = 1   /* Spark 2.4.x hashUnsafeBytes: per-byte sign-extended tail */
 };
 
-enum stc_dtype { STC_F32 = 0, STC_F64 = 1 };
+enum stc_dtype {
+  STC_F32 = 0,
+  STC_F64 = 1,
+  /* an LDA dtype only (stc_lda_config.dtype; the corpus CSR is STC_F64): the fp32 E-step for every document,
+   * then the documents whose fp32 fixed point took more than mixed_resolve_iters iterations — the slowly
+   * contracting ones, where fp32 rounding moves the stopping iterate — re-solved from the same γ₀ in fp64
+   * (expElogβ' kept in both precisions); sstats, stat and the expElogβ' the E-step reads in fp32, λ / α /
+   * colsum / the bound in fp64.  Inference (bound, topicDistribution) runs in fp64. */
+  STC_MIXED = 2
+};
 
 enum stc_layout {
   STC_LAYOUT_VK = 0, /* V×k row-major: topicsMatrix(v, t) at [v*k + t] */
@@ -201,8 +210,10 @@ typedef struct stc_lda_config {
   int32_t optimize_doc_concentration; /* ml.LDA default 1, mllib default 0 */
   int32_t sample_with_replacement;    /* mllib default 1 */
   uint64_t seed;                 /* λ₀ / membership / γ₀ counter-RNG seed */
-  int32_t dtype;                 /* STC_F64 (default: Spark's Double E-step) or STC_F32 */
+  int32_t dtype;                 /* STC_F64 (default: Spark's Double E-step), STC_F32 or STC_MIXED */
   int32_t max_inner_iter;        /* E-step safety cap (upstream has none); 0 ⇒ 100000 */
+  int32_t mixed_resolve_iters;   /* STC_MIXED: re-solve in fp64 the documents past this many fp32 iterations
+                                    (0 ⇒ 500) */
 } stc_lda_config;
 
 /* fills the upstream defaults (ml.clustering.LDA) */
@@ -285,6 +296,8 @@ enum stc_kernel_count {
   STC_KC_TGRID64 = 6,       /* k_estep_tgrid64: fp64, the topics split, the rows64 grid in each member */
   STC_KC_TEAM_FALLBACK = 7, /* team launches re-run on k_estep_wide after a co-residency timeout */
   STC_KC_WORKGROUP = 8,     /* k_estep: documents past the fast kernels' row capacity */
+  STC_KC_MIXED_RESOLVES = 9, /* STC_MIXED: fp64 re-solve passes launched (documents past the threshold) */
+  STC_KC_MIXED_DOCS = 10,   /* STC_MIXED: documents re-solved in fp64 */
   STC_KC_N = 12
 };
 int stc_lda_kernel_counts(stc_lda* lda, int64_t out[12]);

@@ -67,6 +67,16 @@ struct stc_lda {
       nonempty, r, keys, vals, skeys, svals, stat, headbuf, tailbuf, sort_tmp, scan_tmp,
       stats4, cum2, bound, dtmp, lpart;
   DevBuf g0gen;  // γ₀ drawn ahead of the E-step (lda::launch_gamma0) when the caller injects none
+  // STC_MIXED (dtype reported STC_F32 inside the library; `mixed` set): the fp32 E-step, then the documents past
+  // mixed_thr fp32 iterations re-solved in fp64 (mixed_resolve) from Bp64, the fp64 expElogβ' rows the M-step
+  // writes beside Bp, and the corpus's fp64 values; vals32 is the fp32 copy the fp32 E-step reads
+  bool mixed = false;
+  int mixed_thr = 500;
+  int P64 = 0, lds_rows64 = 0;  // the fp64 workgroup kernel's LDS pitch / rows at this kp
+  int64_t cap64 = 0;            // the fp64 fast kernels' row capacity (longer documents: the workgroup kernel)
+  DevBuf Bp64, vals32, m_batch, m_orig, m_bptr, m_slot, m_cnt, eth64, elogth64, r64, keys64, vals64, gamma64, g0_64;
+  const DCsr* vals32_for = nullptr;
+  int32_t* hmcnt = nullptr;     // pinned: the two list counts
   DevBuf s_counts, s_weights, s_short, s_cincl, s_wincl, s_sincl;
   // the next draw is sampled on a side stream, concurrently with this step's E-step (it reads only
   // indptr and writes only the s_* buffers, which this step's fill_batch has consumed)
@@ -138,6 +148,7 @@ struct stc_lda {
       for (auto& e : s)
         if (e) (void)hipEventDestroy(e);
     if (hcnt) (void)hipHostFree(hcnt);
+    if (hmcnt) (void)hipHostFree(hmcnt);
     if (hpre) (void)hipHostFree(hpre);
     if (htmo) (void)hipHostFree(htmo);
     if (ev_pre) (void)hipEventDestroy(ev_pre);
@@ -430,6 +441,7 @@ void ensure_layout(stc_lda& L) {
     std::swap(tmp.bytes, L.lam.bytes);
   }
   L.Bp.reserve(L.tsize * vpad * L.kp);
+  if (L.mixed) L.Bp64.reserve(8 * vpad * L.kp);
   L.stat.reserve(L.tsize * vpad * L.kp);
   L.logscale.reserve(8 * vpad);
   L.colpart.reserve(8 * (vpad / RB) * L.k);
@@ -450,7 +462,8 @@ template <typename T>
 void refresh_model(stc_lda& L) {
   hipStream_t s = L.ctx->stream;
   lda::launch_lambda_eeb<T>(s, false, L.lam.as<double>(), nullptr, L.Bp.as<T>(), L.logscale.as<double>(), L.V,
-                            L.k, L.kp, 0.0, 0.0, 0.0, nullptr, L.colpart.as<double>(), L.nblocks_m);
+                            L.k, L.kp, 0.0, 0.0, 0.0, nullptr, L.colpart.as<double>(), L.nblocks_m,
+                            L.mixed ? L.Bp64.as<double>() : nullptr);
   lda::launch_colsum_reduce(s, L.colpart.as<double>(), L.nblocks_m, L.k, nullptr, L.colsum.as<double>(),
                             L.psic.as<double>());
   L.has_topics = true;
@@ -542,6 +555,13 @@ lda::EStepArgs<T> estep_args(stc_lda& L) {
   a.P = L.P;
   a.lds_rows = L.lds_rows;
   a.Bp = L.Bp.as<T>();
+  if constexpr (std::is_same<T, double>::value) {
+    if (L.mixed) {  // the fp64 re-solve / inference of a mixed handle: the fp64 rows and workgroup shape
+      a.Bp = L.Bp64.as<double>();
+      a.P = L.P64;
+      a.lds_rows = L.lds_rows64;
+    }
+  }
   a.logscale = L.logscale.as<double>();
   a.psic = L.psic.as<double>();
   a.alpha = L.alpha.as<double>();
@@ -708,7 +728,8 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
     lda::EStepArgs<T> w = a;
     w.slot0 = 0;
     w.n = n_short;
-    const TeamChoice tc = use_wide(L.k, L.dtype) && !bound ? team_choice<T>(L, mean_rows, m.max_row) : TeamChoice{};
+    const int dt = std::is_same<T, float>::value ? STC_F32 : STC_F64;  // (a mixed handle runs both)
+    const TeamChoice tc = use_wide(L.k, dt) && !bound ? team_choice<T>(L, mean_rows, m.max_row) : TeamChoice{};
     const bool team = tc.P > 1 && launch_wide_team<T>(L, w, stats, tc);
     if (team) {  // launched (a grid that could not be resident falls through to the one-CU kernel)
       L.kcount[tc.grid ? STC_KC_TGRID64 : tc.topics ? STC_KC_WIDE_TC : STC_KC_WIDE_MC] += 1;
@@ -720,7 +741,7 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
         L.kcount[STC_KC_WIDE] += 1;
         lda::launch_estep_wide<T>(s, w, stats, bound);
       }
-    } else if (use_wide(L.k, L.dtype)) {
+    } else if (use_wide(L.k, dt)) {
       L.kcount[STC_KC_WIDE] += 1;
       lda::launch_estep_wide<T>(s, w, stats, bound);
     } else if constexpr (std::is_same<T, float>::value) {
@@ -762,6 +783,18 @@ const T* upload_gamma0(stc_lda& L, const double* gamma0, int64_t n) {
   return L.g0.as<T>();
 }
 
+// the CSR value dtype a handle reads (a mixed handle: the fp64 values, and an fp32 copy it makes itself)
+int corpus_dtype(const stc_lda& L) { return L.mixed ? STC_F64 : L.dtype; }
+
+// STC_MIXED with an injected γ₀: its fp64 copy for the re-solve (the fp32 E-step reads the rounded one)
+const double* mixed_gamma0(stc_lda& L, const double* gamma0, int64_t n) {
+  if (!L.mixed || !gamma0 || n == 0) return nullptr;
+  L.g0_64.reserve(sizeof(double) * n * L.k);
+  HIP_CHECK(hipMemcpyAsync(L.g0_64.p, gamma0, sizeof(double) * n * L.k, hipMemcpyHostToDevice, L.ctx->stream));
+  wait_stream(*L.ctx, L.ctx->stream);  // (the caller's buffer)
+  return L.g0_64.as<double>();
+}
+
 // a step's M-step is sharded over the ranks (reduce-scatter, slice update, all-gather)
 bool sharded(const stc_lda& L) { return L.ctx->coll() && (L.ctx->n_ranks > 1 || L.force_coll); }
 
@@ -800,13 +833,89 @@ const T* gen_gamma0(stc_lda& L, hipStream_t s, int64_t n, uint64_t seed, int64_t
 // L.small and the term-sorted sstats SpMM into L.stat (V×kp, row-scaled).  split: a training step of a
 // sharded handle — stat in the sub-chunk layout, one sstats launch per sub-chunk (ev_ss[j] after each).
 template <typename T>
+void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int64_t n_short, bool stats,
+                  bool bound, double mean_rows);
+
+// STC_MIXED: after the fp32 E-step over the n slots, the documents whose fp32 fixed point took more than
+// mixed_thr iterations are re-solved in fp64 — the same γ₀ (the training key drawn in the kernel, or the
+// injected fp64 γ₀ g0_64), the fp64 expElogβ' rows (Bp64) and the corpus's fp64 values — and their eθ',
+// E[log θ], r, sstats sort values, iteration counts (and γ) replace the fp32 ones before logphat and
+// sstats read them.  One host readback (the two list counts) sizes the fp64 launches.  Why the fp32
+// iteration count selects them: DESIGN.md §4 (mixed mode).
+void mixed_resolve(stc_lda& L, int64_t n, int64_t E, int64_t iteration, const double* g0_64, bool want_gamma) {
+  if (n == 0) return;
+  const DCsr& m = *L.corpus;
+  hipStream_t s = L.ctx->stream;
+  L.m_batch.reserve(4 * n);
+  L.m_orig.reserve(4 * n);
+  L.m_slot.reserve(4 * n);
+  L.m_bptr.reserve(8 * n);
+  L.m_cnt.reserve(2 * sizeof(int32_t));
+  if (!L.hmcnt) HIP_CHECK(hipHostMalloc((void**)&L.hmcnt, 2 * sizeof(int32_t), hipHostMallocDefault));
+  lda::launch_mixed_list(s, m.indptr.as<int64_t>(), L.batch.as<int32_t>(), L.orig.as<int32_t>(), L.bptr.as<int64_t>(),
+                         L.iters.as<int32_t>(), L.nonempty.as<int32_t>(), n, L.mixed_thr, L.cap64,
+                         L.m_batch.as<int32_t>(), L.m_orig.as<int32_t>(), L.m_bptr.as<int64_t>(), L.m_slot.as<int32_t>(),
+                         L.m_cnt.as<int32_t>());
+  HIP_CHECK(hipMemcpyAsync(L.hmcnt, L.m_cnt.p, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  wait_stream(*L.ctx, s);
+  const int ms = L.hmcnt[0], ml = L.hmcnt[1];
+  if (ms + ml == 0) return;
+  L.kcount[STC_KC_MIXED_RESOLVES] += 1;
+  L.kcount[STC_KC_MIXED_DOCS] += ms + ml;
+  L.eth64.reserve(8 * n * L.kp);
+  L.elogth64.reserve(8 * n * L.k);
+  L.r64.reserve(8 * std::max<int64_t>(E, 1));
+  L.keys64.reserve(4 * std::max<int64_t>(E, 1));
+  L.vals64.reserve(8 * std::max<int64_t>(E, 1));
+  if (want_gamma) L.gamma64.reserve(8 * n * L.k);
+  lda::EStepArgs<double> a = estep_args<double>(L);  // Bp64 and the fp64 workgroup shape
+  a.indptr = m.indptr.as<int64_t>();
+  a.indices = m.indices.as<int32_t>();
+  a.values = m.values.as<double>();
+  a.gamma0 = g0_64;
+  a.iteration = iteration;
+  a.key_mode = 0;
+  a.gamma = want_gamma ? L.gamma64.as<double>() : nullptr;
+  a.r = L.r64.as<double>();
+  a.keys = L.keys64.as<uint32_t>();  // (the fp64 sort values are the fp64 layout's: scratch, rewritten by the fixup)
+  a.vals = L.vals64.as<uint64_t>();
+  a.iters = L.iters.as<int32_t>();
+  a.nonempty = L.nonempty.as<int32_t>();
+  const double mean_rows = (double)E / (double)n;
+  if (ms > 0) {  // the documents the fp64 fast kernels hold
+    lda::EStepArgs<double> w = a;
+    w.batch = L.m_batch.as<int32_t>();
+    w.orig = L.m_orig.as<int32_t>();
+    w.bptr = L.m_bptr.as<int64_t>();
+    w.eth = L.eth64.as<double>();
+    w.elogth = L.elogth64.as<double>();
+    launch_split<double>(L, m, w, ms, ms, true, false, mean_rows);
+  }
+  if (ml > 0) {  // the longer ones: the workgroup kernel
+    const int64_t off = n - ml;
+    lda::EStepArgs<double> w = a;
+    w.batch = L.m_batch.as<int32_t>() + off;
+    w.orig = L.m_orig.as<int32_t>() + off;
+    w.bptr = L.m_bptr.as<int64_t>() + off;
+    w.eth = L.eth64.as<double>() + off * L.kp;
+    w.elogth = L.elogth64.as<double>() + off * L.k;
+    launch_split<double>(L, m, w, ml, 0, true, false, mean_rows);
+  }
+  lda::launch_mixed_fixup(s, m.indptr.as<int64_t>(), L.m_batch.as<int32_t>(), L.m_orig.as<int32_t>(),
+                          L.m_bptr.as<int64_t>(), L.m_slot.as<int32_t>(), n, ms, ml, L.k, L.kp, L.eth64.as<double>(),
+                          L.elogth64.as<double>(), L.r64.as<double>(), want_gamma ? L.gamma64.as<double>() : nullptr,
+                          L.eth.as<float>(), L.elogth.as<float>(), L.r.as<float>(), L.vals.as<uint64_t>(),
+                          want_gamma ? L.gamma.as<float>() : nullptr);
+}
+
+template <typename T>
 void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T* g0, int64_t iteration,
-                     bool split = false) {
+                     bool split = false, const double* g0_64 = nullptr, bool want_gamma = false) {
   hipStream_t s = L.ctx->stream;
   lda::EStepArgs<T> a = estep_args<T>(L);
   a.indptr = L.corpus->indptr.as<int64_t>();
   a.indices = L.corpus->indices.as<int32_t>();
-  a.values = L.corpus->values.as<T>();
+  a.values = L.mixed ? L.vals32.as<T>() : L.corpus->values.as<T>();
   a.batch = L.batch.as<int32_t>();
   a.orig = L.orig.as<int32_t>();
   a.bptr = L.bptr.as<int64_t>();
@@ -824,6 +933,9 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   a.nonempty = L.nonempty.as<int32_t>();
   record(L, 1);
   launch_split<T>(L, *L.corpus, a, n, n_short, true, false, n > 0 ? (double)E / (double)n : 0.0);
+  if constexpr (std::is_same<T, float>::value) {
+    if (L.mixed) mixed_resolve(L, n, E, iteration, g0_64, want_gamma);
+  }
   if (L.ev_est) HIP_CHECK(hipEventRecord(L.ev_est, s));  // the batch buffers are free (next_impl)
   record(L, 2);
   // logphat first: its all-reduce rides with the first stat sub-chunk of a sharded step
@@ -868,7 +980,8 @@ void mstep_slice(stc_lda& L, int r, double rho, double scale, const double* gate
   const int64_t nbs = L.Vs / lda::kRowsPerBlock;
   lda::launch_lambda_eeb<T>(L.ctx->stream, true, L.lam.as<double>() + v0 * L.k, L.stat.as<T>() + v0 * L.kp,
                             L.Bp.as<T>() + v0 * L.kp, L.logscale.as<double>() + v0, vn, L.k, L.kp, rho, scale,
-                            L.eta, gate, L.colpart.as<double>() + (int64_t)r * nbs * L.k, nbs);
+                            L.eta, gate, L.colpart.as<double>() + (int64_t)r * nbs * L.k, nbs,
+                            L.mixed ? L.Bp64.as<double>() + v0 * L.kp : nullptr);
 }
 // the same pass over sub-chunk j of slice r, whose summed stat rows sit at the sub-chunk layout's
 // physical rows (stat_layout); λ / expElogβ' / logscale / colsum partials at their canonical rows
@@ -880,7 +993,7 @@ void mstep_sub(stc_lda& L, const lda::StatMap& m, int r, int j, double rho, doub
   lda::launch_lambda_eeb<T>(L.ctx->stream, true, L.lam.as<double>() + v0 * L.k, L.stat.as<T>() + phys * L.kp,
                             L.Bp.as<T>() + v0 * L.kp, L.logscale.as<double>() + v0, vn, L.k, L.kp, rho, scale,
                             L.eta, gate, L.colpart.as<double>() + (v0 / lda::kRowsPerBlock) * L.k,
-                            w / lda::kRowsPerBlock);
+                            w / lda::kRowsPerBlock, L.mixed ? L.Bp64.as<double>() + v0 * L.kp : nullptr);
 }
 
 // [U] submitMiniBatch tail: the stats merge (treeReduce ≙ RCCL), updateLambda, updateAlpha.
@@ -953,6 +1066,7 @@ void train_tail(stc_lda& L, int64_t n, int64_t E, stc_step_stats* st) {
     coll_group_start(c);
     coll_all_gather(c, L.colpart.as<double>() + (size_t)c.rank * nbs * L.k, L.colpart.p, nbs * L.k, ncclFloat64, s);
     coll_all_gather(c, L.Bp.as<T>() + (size_t)c.rank * cnt, L.Bp.p, cnt, RcclType<T>::v, s);
+    if (L.mixed) coll_all_gather(c, L.Bp64.as<double>() + (size_t)c.rank * cnt, L.Bp64.p, cnt, ncclFloat64, s);
     coll_all_gather(c, L.logscale.as<double>() + (size_t)c.rank * L.Vs, L.logscale.p, (size_t)L.Vs, ncclFloat64, s);
     coll_group_end(c);
     lda::launch_colsum_reduce(s, L.colpart.as<double>(), nb_all, L.k, gate, L.colsum.as<double>(),
@@ -1010,6 +1124,7 @@ void train_tail_split(stc_lda& L, const lda::StatMap& lay, bool had_samp, int64_
   coll_group_start(c);
   coll_all_gather(c, L.colpart.as<double>() + (size_t)c.rank * nbs * L.k, L.colpart.p, nbs * L.k, ncclFloat64, s);
   coll_all_gather(c, L.Bp.as<T>() + (size_t)c.rank * cnt, L.Bp.p, cnt, RcclType<T>::v, s);
+  if (L.mixed) coll_all_gather(c, L.Bp64.as<double>() + (size_t)c.rank * cnt, L.Bp64.p, cnt, ncclFloat64, s);
   coll_all_gather(c, L.logscale.as<double>() + (size_t)c.rank * L.Vs, L.logscale.p, (size_t)L.Vs, ncclFloat64, s);
   coll_group_end(c);
   lda::launch_colsum_reduce(s, L.colpart.as<double>(), L.shards * (int64_t)nbs, L.k, gate, L.colsum.as<double>(),
@@ -1081,7 +1196,7 @@ void step_ids(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0, s
   if (L.timing) harvest_all(L);  // partition() drained the stream
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
   if (!g0) g0 = gen_gamma0<T>(L, L.ctx->stream, n, L.cfg.seed, L.iteration + 1, 0, 0);
-  estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1, true);
+  estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1, true, mixed_gamma0(L, gamma0, n));
   train_tail<T>(L, n, p.E, st);
 }
 
@@ -1212,7 +1327,7 @@ void estep_only(stc_lda& L, const int64_t* ids, int64_t n, const double* gamma0,
   const T* g0 = upload_gamma0<T>(L, gamma0, n);
   const bool t = L.timing;
   L.timing = false;
-  estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1);
+  estep_and_stats<T>(L, n, p.n_short, p.E, g0, L.iteration + 1, false, mixed_gamma0(L, gamma0, n), gamma_out != nullptr);
   L.timing = t;
   if (gamma_out && n > 0) {
     std::vector<T> g((size_t)(n * L.k));
@@ -1237,7 +1352,7 @@ void infer_impl(stc_lda& L, const DCsr& docs, uint64_t seed, int64_t base, const
                 bool bound, double* gamma_out, double* out4 /* corpus, tokens */) {
   if (!L.has_topics) throw Error(STC_ERR_STATE, "no topics: call stc_lda_init_random or stc_lda_set_topics");
   STC_REQUIRE(docs.cols == L.V, "document vectors must have vocab_size columns");
-  STC_REQUIRE(docs.dtype == L.dtype, "document CSR dtype must match the LDA dtype");
+  STC_REQUIRE(docs.dtype == corpus_dtype(L), "document CSR dtype must match the LDA dtype (STC_F64 for STC_MIXED)");
   hipStream_t s = L.ctx->stream;
   const int64_t n = docs.rows;
   ensure_batch<T>(L, n, 0);
@@ -1929,7 +2044,8 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     STC_REQUIRE(cfg->mini_batch_fraction > 0.0 && cfg->mini_batch_fraction <= 1.0,
                 "miniBatchFraction must be in range (0,1]");
     STC_REQUIRE(cfg->gamma_shape > 1.0 / 3.0, "gammaShape must be > 1/3");
-    STC_REQUIRE(cfg->dtype == STC_F32 || cfg->dtype == STC_F64, "dtype");
+    STC_REQUIRE(cfg->dtype == STC_F32 || cfg->dtype == STC_F64 || cfg->dtype == STC_MIXED, "dtype");
+    STC_REQUIRE(cfg->mixed_resolve_iters >= 0, "mixed_resolve_iters must be >= 0");
     STC_REQUIRE(cfg->max_inner_iter >= 0, "max_inner_iter must be >= 0");
     ctx->use();
     auto L = std::make_unique<stc_lda>();
@@ -1938,18 +2054,27 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     if (L->cfg.max_inner_iter == 0) L->cfg.max_inner_iter = 100000;
     L->k = cfg->k;
     L->V = cfg->vocab_size;
-    L->dtype = cfg->dtype;
-    L->tsize = cfg->dtype == STC_F32 ? 4 : 8;
-    const int W = cfg->dtype == STC_F32 ? 4 : 2;
+    // STC_MIXED: the fp32 pipeline (dtype STC_F32 inside the library) plus the fp64 re-solve (mixed_resolve)
+    L->mixed = cfg->dtype == STC_MIXED;
+    L->dtype = L->mixed ? STC_F32 : cfg->dtype;
+    L->mixed_thr = cfg->mixed_resolve_iters > 0 ? cfg->mixed_resolve_iters : 500;
+    L->tsize = L->dtype == STC_F32 ? 4 : 8;
+    const int W = L->dtype == STC_F32 ? 4 : 2;
     L->kp = (int)ceil_div(L->k, W) * W;
     L->P = ((L->kp / W) % 2 == 1) ? L->kp : L->kp + W;  // P/W odd: conflict-free b128 rows
-    L->lds_rows = cfg->dtype == STC_F32 ? lda::estep_lds_rows<float>(L->k, L->kp, L->P)
-                                        : lda::estep_lds_rows<double>(L->k, L->kp, L->P);
+    L->lds_rows = L->dtype == STC_F32 ? lda::estep_lds_rows<float>(L->k, L->kp, L->P)
+                                      : lda::estep_lds_rows<double>(L->k, L->kp, L->P);
+    if (L->mixed) {  // the fp64 workgroup kernel's shape at the fp32 row pitch, and the fp64 fast-kernel capacity
+      L->P64 = ((L->kp / 2) % 2 == 1) ? L->kp : L->kp + 2;
+      L->lds_rows64 = lda::estep_lds_rows<double>(L->k, L->kp, L->P64);
+      const int c64 = use_wide(L->k, STC_F64) ? lda::wide_row_cap(L->k) : lda::rows64_row_cap(L->k);
+      L->cap64 = c64 > 0 ? c64 : -1;
+    }
     const char* nw = std::getenv("STC_DISABLE_WAVE");
     // docs with nnz <= wave_cap run the register-resident kernel (fp32: lda_grid.hip, fp64:
     // lda_rows64.hip), the rest the workgroup kernel (lda.hip); −1: no slot is "short" (not even empty)
     const int cap = use_wide(L->k, L->dtype) ? lda::wide_row_cap(L->k)
-                    : cfg->dtype == STC_F32 ? lda::grid_row_cap(L->k) : lda::rows64_row_cap(L->k);
+                    : L->dtype == STC_F32 ? lda::grid_row_cap(L->k) : lda::rows64_row_cap(L->k);
     L->wave_cap = (!(nw && nw[0] == '1') && cap > 0) ? cap : -1;
     // α / η resolution ([U] OnlineLDAOptimizer.initialize)
     std::vector<double> alpha((size_t)L->k);
@@ -2030,11 +2155,18 @@ int stc_lda_set_corpus(stc_lda* L, const stc_dcsr* corpus, int64_t corpus_size_t
     STC_REQUIRE(L && corpus, "lda/corpus");
     STC_REQUIRE(corpus->ctx == L->ctx, "the corpus belongs to another stc_ctx than the LDA handle");
     STC_REQUIRE(corpus->cols == L->V, "corpus must have vocab_size columns");
-    STC_REQUIRE(corpus->dtype == L->dtype, "corpus value dtype must match the LDA dtype");
+    STC_REQUIRE(corpus->dtype == corpus_dtype(*L), "corpus value dtype must match the LDA dtype (STC_F64 for STC_MIXED)");
     STC_REQUIRE(corpus->rows < (int64_t(1) << 31), "at most 2^31-1 documents per rank");
     STC_REQUIRE(corpus_size_total >= corpus->rows && corpus_size_total > 0,
                 "corpus_size_total must be >= this rank's rows and > 0");
     settle_side(*L);  // a draw still being sampled reads the previous corpus
+    if (L->mixed) {  // the fp32 copy of the values the fp32 E-step reads
+      L->ctx->use();
+      L->vals32.reserve(4 * std::max<int64_t>(corpus->nnz, 1));
+      lda::launch_to_f32(L->ctx->stream, corpus->values.as<double>(), L->vals32.as<float>(), corpus->nnz);
+      wait_stream(*L->ctx, L->ctx->stream);
+      L->vals32_for = corpus;
+    }
     L->corpus = corpus;
     L->corpus_total = corpus_size_total;
     L->pre_valid = false;  // a prefetched draw sampled the previous corpus
@@ -2176,7 +2308,7 @@ int stc_lda_bound(stc_lda* L, const stc_dcsr* docs, uint64_t gamma_seed, int64_t
     double h[3] = {0, 0, 0};
     double norm = 0;
     const bool sharded = L->lam_stale;
-    if (L->dtype == STC_F32) {
+    if (L->dtype == STC_F32 && !L->mixed) {  // (a mixed handle infers in fp64)
       infer_impl<float>(*L, *docs, gamma_seed, doc_id_base, gamma0, true, nullptr, h);
       topics_part<float>(*L, h + 2, &norm);
     } else {
@@ -2200,7 +2332,7 @@ int stc_lda_topic_distribution(stc_lda* L, const stc_dcsr* docs, uint64_t gamma_
     STC_REQUIRE(L && docs && (out || docs->rows == 0), "lda/docs/out");
     STC_REQUIRE(docs->ctx == L->ctx, "the documents belong to another stc_ctx than the LDA handle");
     L->ctx->use();
-    if (L->dtype == STC_F32)
+    if (L->dtype == STC_F32 && !L->mixed)  // (a mixed handle infers in fp64)
       infer_impl<float>(*L, *docs, gamma_seed, doc_id_base, gamma0, false, out, nullptr);
     else
       infer_impl<double>(*L, *docs, gamma_seed, doc_id_base, gamma0, false, out, nullptr);
@@ -2509,7 +2641,7 @@ int stc_group_create(const int* device_ids, int n_devices, const stc_lda_config*
       l->tail_fault = i == step_fault ? step_fault_at : 0;
       g->lda.push_back(l);
     }
-    g->dtype = g->lda[0]->dtype;
+    g->dtype = corpus_dtype(*g->lda[0]);  // the shards' value dtype
     g->row0.assign((size_t)n_devices + 1, 0);
     cleanup.g = nullptr;
     *out = g.release();

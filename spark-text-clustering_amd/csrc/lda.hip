@@ -696,7 +696,7 @@ __global__ __launch_bounds__(256, 5) void k_lambda_eeb(double* __restrict__ lam,
                                                     T* __restrict__ Bp, double* __restrict__ logscale,
                                                     int64_t V, int k, int kp, double rho, double scale,
                                                     double eta, const double* __restrict__ gate,
-                                                    double* __restrict__ colpart) {
+                                                    double* __restrict__ colpart, double* __restrict__ Bp64) {
   if (gate && !(gate[0] > 0.0)) return;  // Spark: no non-empty docs ⇒ no update
   __shared__ double s_acc[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -742,6 +742,15 @@ __global__ __launch_bounds__(256, 5) void k_lambda_eeb(double* __restrict__ lam,
       const int t = lane + 64 * q;
       if (t < kp) br[t] = t < k ? exp_scaled(e[q] - m, T()) : T(0);
     }
+    if constexpr (sizeof(T) == 4) {  // STC_MIXED: the fp64 rows of the re-solve, at the same m_v
+      if (Bp64) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const int t = lane + 64 * q;
+          if (t < kp) Bp64[v * kp + t] = t < k ? exp(e[q] - m) : 0.0;
+        }
+      }
+    }
     if (lane == 0) logscale[v] = m;
   }
 #pragma unroll
@@ -765,7 +774,7 @@ __global__ __launch_bounds__(256) void k_lambda_eeb_wide(double* __restrict__ la
                                                          T* __restrict__ Bp, double* __restrict__ logscale,
                                                          int64_t V, int k, int kp, double rho, double scale,
                                                          double eta, const double* __restrict__ gate,
-                                                         double* __restrict__ colpart) {
+                                                         double* __restrict__ colpart, double* __restrict__ Bp64) {
   if (gate && !(gate[0] > 0.0)) return;
   __shared__ double s_max[2][4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -818,6 +827,15 @@ __global__ __launch_bounds__(256) void k_lambda_eeb_wide(double* __restrict__ la
       const int t = tid + 256 * q;
       if (t < kp) br[t] = t < k ? exp_scaled(e[q] - m, T()) : T(0);
     }
+    if constexpr (sizeof(T) == 4) {  // STC_MIXED: the fp64 rows of the re-solve, at the same m_v
+      if (Bp64) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const int t = tid + 256 * q;
+          if (t < kp) Bp64[v * kp + t] = t < k ? exp(e[q] - m) : 0.0;
+        }
+      }
+    }
     if (tid == 0) logscale[v] = m;
   }
 #pragma unroll
@@ -830,7 +848,7 @@ __global__ __launch_bounds__(256) void k_lambda_eeb_wide(double* __restrict__ la
 template <typename T>
 void launch_lambda_eeb(hipStream_t s, bool update, double* lam, const T* stat, T* Bp, double* logscale,
                        int64_t V, int k, int kp, double rho, double scale, double eta, const double* gate,
-                       double* colpart, int64_t nblocks) {
+                       double* colpart, int64_t nblocks, double* Bp64) {
   if (nblocks <= 0) return;
   if (kp > 256) {  // a row per workgroup
     const int qw = (kp + 255) / 256;
@@ -838,10 +856,12 @@ void launch_lambda_eeb(hipStream_t s, bool update, double* lam, const T* stat, T
   do {                                                                                                   \
     if (update)                                                                                          \
       k_lambda_eeb_wide<T, QQ, true><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, logscale, V, k, kp, \
-                                                                        rho, scale, eta, gate, colpart);  \
+                                                                        rho, scale, eta, gate, colpart,   \
+                                                                        Bp64);                           \
     else                                                                                                 \
       k_lambda_eeb_wide<T, QQ, false><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, logscale, V, k,    \
-                                                                         kp, rho, scale, eta, gate, colpart); \
+                                                                         kp, rho, scale, eta, gate, colpart, \
+                                                                         Bp64);                          \
   } while (0)
     if (qw <= 2) STC_LEEBW(2);
     else if (qw <= 4) STC_LEEBW(4);
@@ -857,10 +877,10 @@ void launch_lambda_eeb(hipStream_t s, bool update, double* lam, const T* stat, T
   do {                                                                                                  \
     if (update)                                                                                         \
       k_lambda_eeb<T, QQ, true><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, logscale, V, k, kp,   \
-                                                                   rho, scale, eta, gate, colpart);    \
+                                                                   rho, scale, eta, gate, colpart, Bp64); \
     else                                                                                                \
       k_lambda_eeb<T, QQ, false><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, logscale, V, k, kp,  \
-                                                                    rho, scale, eta, gate, colpart);   \
+                                                                    rho, scale, eta, gate, colpart, Bp64); \
   } while (0)
   if (q <= 1) STC_LEEB(1);
   else if (q <= 2) STC_LEEB(2);
@@ -1368,6 +1388,84 @@ void launch_gamma0(hipStream_t s, const int32_t* batch, const int32_t* orig, int
   KERNEL_CHECK();
 }
 
+// ---- STC_MIXED: the fp64 re-solve of the fp32 E-step's slowly converging documents -------------------
+// slots whose member is non-empty and took more than `thr` fp32 iterations: those with nnz ≤ cap64 (the fp64
+// fast kernels' row capacity) from position 0 up (count cnt[0]), the others from position n − 1 down
+// (count cnt[1]); each position holds the slot's row, member, entry offset and the slot itself.  The order
+// within a list is the atomics' (every document's outputs are its own, so results do not depend on it).
+__global__ void k_mixed_list(const int64_t* __restrict__ indptr, const int32_t* __restrict__ batch,
+                             const int32_t* __restrict__ orig, const int64_t* __restrict__ bptr,
+                             const int32_t* __restrict__ iters, const int32_t* __restrict__ nonempty, int64_t n,
+                             int thr, int64_t cap64, int32_t* __restrict__ lbatch, int32_t* __restrict__ lorig,
+                             int64_t* __restrict__ lbptr, int32_t* __restrict__ lslot, int32_t* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t mem = orig ? orig[i] : (int32_t)i;
+  if (!nonempty[mem] || iters[mem] <= thr) return;
+  const int64_t row = batch ? batch[i] : i;
+  const int64_t nnz = indptr[row + 1] - indptr[row];
+  const int64_t j = nnz <= cap64 ? (int64_t)atomicAdd(&cnt[0], 1) : n - 1 - (int64_t)atomicAdd(&cnt[1], 1);
+  lbatch[j] = (int32_t)row;
+  lorig[j] = mem;
+  lbptr[j] = bptr ? bptr[i] : indptr[row];
+  lslot[j] = (int32_t)i;
+}
+void launch_mixed_list(hipStream_t s, const int64_t* indptr, const int32_t* batch, const int32_t* orig,
+                       const int64_t* bptr, const int32_t* iters, const int32_t* nonempty, int64_t n, int thr,
+                       int64_t cap64, int32_t* lbatch, int32_t* lorig, int64_t* lbptr, int32_t* lslot, int32_t* cnt) {
+  HIP_CHECK(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), s));
+  if (n <= 0) return;
+  k_mixed_list<<<(unsigned)ceil_div(n, (int64_t)256), 256, 0, s>>>(indptr, batch, orig, bptr, iters, nonempty, n, thr,
+                                                                  cap64, lbatch, lorig, lbptr, lslot, cnt);
+  KERNEL_CHECK();
+}
+// the re-solved documents' fp64 outputs into the fp32 step buffers: eθ' and E[log θ] per slot, r and the
+// sstats sort value (slot, fp32 r) per entry, γ per member (when given); one workgroup per listed document
+// (list positions [0, ms) and [n − ml, n))
+__global__ __launch_bounds__(256) void k_mixed_fixup(const int64_t* __restrict__ indptr, const int32_t* __restrict__ lbatch,
+                                                     const int32_t* __restrict__ lorig, const int64_t* __restrict__ lbptr,
+                                                     const int32_t* __restrict__ lslot, int64_t n, int ms, int ml, int k,
+                                                     int kp, const double* __restrict__ eth64,
+                                                     const double* __restrict__ elogth64, const double* __restrict__ r64,
+                                                     const double* __restrict__ gamma64, float* __restrict__ eth,
+                                                     float* __restrict__ elogth, float* __restrict__ r,
+                                                     uint64_t* __restrict__ vals, float* __restrict__ gamma) {
+  const int jj = blockIdx.x;
+  const int64_t j = jj < ms ? jj : n - ml + (jj - ms);
+  const int64_t slot = lslot[j], mem = lorig[j], row = lbatch[j], e0 = lbptr[j];
+  const int64_t nnz = indptr[row + 1] - indptr[row];
+  for (int t = threadIdx.x; t < kp; t += blockDim.x) {
+    eth[slot * kp + t] = (float)eth64[j * kp + t];
+    if (t < k) {
+      elogth[slot * k + t] = (float)elogth64[j * k + t];
+      if (gamma) gamma[mem * k + t] = (float)gamma64[mem * k + t];
+    }
+  }
+  for (int64_t e = threadIdx.x; e < nnz; e += blockDim.x) {
+    const float rv = (float)r64[e0 + e];
+    r[e0 + e] = rv;
+    if (vals) vals[e0 + e] = entry_val<float>(slot, e0 + e, rv);
+  }
+}
+void launch_mixed_fixup(hipStream_t s, const int64_t* indptr, const int32_t* lbatch, const int32_t* lorig,
+                        const int64_t* lbptr, const int32_t* lslot, int64_t n, int ms, int ml, int k, int kp,
+                        const double* eth64, const double* elogth64, const double* r64, const double* gamma64,
+                        float* eth, float* elogth, float* r, uint64_t* vals, float* gamma) {
+  if (ms + ml <= 0) return;
+  k_mixed_fixup<<<(unsigned)(ms + ml), 256, 0, s>>>(indptr, lbatch, lorig, lbptr, lslot, n, ms, ml, k, kp, eth64,
+                                                    elogth64, r64, gamma64, eth, elogth, r, vals, gamma);
+  KERNEL_CHECK();
+}
+__global__ void k_to_f32(const double* __restrict__ in, float* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (float)in[i];
+}
+void launch_to_f32(hipStream_t s, const double* in, float* out, int64_t n) {
+  if (n <= 0) return;
+  k_to_f32<<<(unsigned)std::min<int64_t>(ceil_div(n, (int64_t)256), 65536), 256, 0, s>>>(in, out, n);
+  KERNEL_CHECK();
+}
+
 #define STC_INSTANTIATE(T)                                                                        \
   template void launch_gamma0<T>(hipStream_t, const int32_t*, const int32_t*, int64_t, int, uint64_t, int64_t, \
                                  int, int, int64_t, double, T*);                                  \
@@ -1377,7 +1475,7 @@ void launch_gamma0(hipStream_t s, const int32_t* batch, const int32_t* orig, int
   template void launch_sstats<T>(hipStream_t, const uint32_t*, const uint64_t*, int64_t, const T*, \
                                  const T*, int, T*, T*, T*, const StatMap&);                      \
   template void launch_lambda_eeb<T>(hipStream_t, bool, double*, const T*, T*, double*, int64_t, int, \
-                                     int, double, double, double, const double*, double*, int64_t);    \
+                                     int, double, double, double, const double*, double*, int64_t, double*); \
   template void launch_logphat<T>(hipStream_t, const T*, const int32_t*, int64_t, int, double*, double*);  \
   template void launch_topics_bound<T>(hipStream_t, const double*, const double*, int64_t, int,   \
                                        double, double*, int64_t);                                 \

@@ -178,10 +178,11 @@ void launch_gamma0(hipStream_t s, const int32_t* batch, const int32_t* orig, int
                    int64_t iteration, int rank, int key_mode, int64_t doc_id_base, double shape, T* out);
 
 // the fused M-step pass (update = true: λ update; both: expElogβ' rows, logscale, colsum partials)
+// Bp64 (STC_MIXED, T = float only; may be null): the same rows in fp64 at the same m_v, for the re-solve
 template <typename T>
 void launch_lambda_eeb(hipStream_t s, bool update, double* lam, const T* stat, T* Bp, double* logscale,
                        int64_t V, int k, int kp, double rho, double scale, double eta, const double* gate,
-                       double* colpart, int64_t nblocks);
+                       double* colpart, int64_t nblocks, double* Bp64 = nullptr);
 // colsum (block order), psic[0, k) = ψ(colsum), psic[k, 2k) = exp(−ψ(colsum))
 void launch_colsum_reduce(hipStream_t s, const double* colpart, int64_t nblocks, int k,
                           const double* gate, double* colsum, double* psic);
@@ -215,6 +216,17 @@ void launch_fill_batch(hipStream_t s, const int64_t* indptr, int64_t D, int64_t 
                        const int32_t* counts, const int32_t* count_incl,
                        const int32_t* short_incl, int64_t n_short, int32_t* batch_p,
                        int32_t* orig_p, int64_t* nnz_p);
+// STC_MIXED (api.hip mixed_resolve): the fp32 E-step's documents past `thr` iterations, listed for the fp64
+// re-solve (nnz ≤ cap64 from position 0 up, cnt[0]; the rest from n − 1 down, cnt[1]) ...
+void launch_mixed_list(hipStream_t s, const int64_t* indptr, const int32_t* batch, const int32_t* orig,
+                       const int64_t* bptr, const int32_t* iters, const int32_t* nonempty, int64_t n, int thr,
+                       int64_t cap64, int32_t* lbatch, int32_t* lorig, int64_t* lbptr, int32_t* lslot, int32_t* cnt);
+// ... and their fp64 outputs written back into the fp32 step buffers (γ when gamma is given)
+void launch_mixed_fixup(hipStream_t s, const int64_t* indptr, const int32_t* lbatch, const int32_t* lorig,
+                        const int64_t* lbptr, const int32_t* lslot, int64_t n, int ms, int ml, int k, int kp,
+                        const double* eth64, const double* elogth64, const double* r64, const double* gamma64,
+                        float* eth, float* elogth, float* r, uint64_t* vals, float* gamma);
+void launch_to_f32(hipStream_t s, const double* in, float* out, int64_t n);
 void launch_transpose_kv(hipStream_t s, const double* lam, int64_t V, int k, double* out_kv,
                          int32_t* idx_kv);
 template <typename T>

@@ -18,7 +18,12 @@ LIB_PATH = os.environ.get("STC_LIB") or os.path.join(_HERE, "libstc.so")
 
 STC_OK, STC_ERR_INVALID_ARG, STC_ERR_HIP, STC_ERR_RCCL, STC_ERR_OOM, STC_ERR_STATE = range(6)
 STC_HASH_STANDARD, STC_HASH_SPARK24 = 0, 1
-STC_F32, STC_F64 = 0, 1
+STC_F32, STC_F64, STC_MIXED = 0, 1, 2  # (STC_MIXED: an LDA dtype; its corpus CSR is STC_F64)
+
+
+def corpus_dtype(lda_dtype):
+    """the CSR value dtype an LDA handle of `lda_dtype` reads (STC_MIXED: fp64)"""
+    return STC_F64 if lda_dtype == STC_MIXED else lda_dtype
 STC_LAYOUT_VK, STC_LAYOUT_KV = 0, 1
 STC_TRANSPORT_NONE, STC_TRANSPORT_IN_PROCESS, STC_TRANSPORT_RCCL = 0, 1, 2
 
@@ -46,6 +51,7 @@ class LdaConfig(C.Structure):
         ("seed", _u64),
         ("dtype", _i32),
         ("max_inner_iter", _i32),
+        ("mixed_resolve_iters", _i32),
     ]
 
 

@@ -30,11 +30,12 @@ def _java_string_hash(s: str) -> int:
 
 
 ML_LDA_DEFAULT_SEED = _java_string_hash("org.apache.spark.ml.clustering.LDA")
-_DTYPES = {"f32": L.STC_F32, "float32": L.STC_F32, "f64": L.STC_F64, "float64": L.STC_F64}
+_DTYPES = {"f32": L.STC_F32, "float32": L.STC_F32, "f64": L.STC_F64, "float64": L.STC_F64, "mixed": L.STC_MIXED}
 
 
 def _lda_config(lib, k, vocab_size, doc_concentration, topic_concentration, tau0, kappa, mini_batch_fraction,
-                gamma_shape, optimize_doc_concentration, sample_with_replacement, seed, dtype, max_inner_iter):
+                gamma_shape, optimize_doc_concentration, sample_with_replacement, seed, dtype, max_inner_iter,
+                mixed_resolve_iters=0):
     """stc_lda_config from the Spark-ML parameters (returns the config and the α buffer it points to)."""
     cfg = L.LdaConfig()
     lib.stc_lda_config_default(C.byref(cfg))
@@ -55,6 +56,7 @@ def _lda_config(lib, k, vocab_size, doc_concentration, topic_concentration, tau0
     cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     cfg.dtype = _DTYPES[dtype] if isinstance(dtype, str) else int(dtype)
     cfg.max_inner_iter = int(max_inner_iter)
+    cfg.mixed_resolve_iters = int(mixed_resolve_iters)  # dtype "mixed": the fp64 re-solve threshold (0: 500)
     return cfg, alpha_buf
 
 
@@ -69,7 +71,7 @@ def _phase_times(lib, h):
 
 # stc.h enum stc_kernel_count: the E-step kernel families stc_lda_kernel_counts counts launches of
 KERNEL_FAMILIES = ("k_estep_rows64", "k_estep_rows64_long", "k_estep_grid", "k_estep_wide", "k_estep_wide_mc",
-                   "k_estep_wide_tc", "k_estep_tgrid64", "team_fallback", "k_estep")
+                   "k_estep_wide_tc", "k_estep_tgrid64", "team_fallback", "k_estep", "mixed_resolves", "mixed_docs")
 
 
 def _counters(lib, h):
@@ -88,11 +90,11 @@ class LdaHandle:
     def __init__(self, ctx: Context, k, vocab_size, doc_concentration=None, topic_concentration=-1.0,
                  tau0=1024.0, kappa=0.51, mini_batch_fraction=0.05, gamma_shape=100.0,
                  optimize_doc_concentration=True, sample_with_replacement=True, seed=0,
-                 dtype="f64", max_inner_iter=0):
+                 dtype="f64", max_inner_iter=0, mixed_resolve_iters=0):
         self.ctx = ctx
         cfg, self._alpha_buf = _lda_config(ctx.lib, k, vocab_size, doc_concentration, topic_concentration, tau0,
                                            kappa, mini_batch_fraction, gamma_shape, optimize_doc_concentration,
-                                           sample_with_replacement, seed, dtype, max_inner_iter)
+                                           sample_with_replacement, seed, dtype, max_inner_iter, mixed_resolve_iters)
         h = C.c_void_p()
         L.check(ctx.lib.stc_lda_create(ctx.handle, C.byref(cfg), C.byref(h)))
         self.handle = h
@@ -218,11 +220,11 @@ class LdaGroup:
 
     def __init__(self, devices, k, vocab_size, doc_concentration=None, topic_concentration=-1.0, tau0=1024.0,
                  kappa=0.51, mini_batch_fraction=0.05, gamma_shape=100.0, optimize_doc_concentration=True,
-                 sample_with_replacement=True, seed=0, dtype="f64", max_inner_iter=0):
+                 sample_with_replacement=True, seed=0, dtype="f64", max_inner_iter=0, mixed_resolve_iters=0):
         self.lib = L.load()
         cfg, self._alpha_buf = _lda_config(self.lib, k, vocab_size, doc_concentration, topic_concentration, tau0,
                                            kappa, mini_batch_fraction, gamma_shape, optimize_doc_concentration,
-                                           sample_with_replacement, seed, dtype, max_inner_iter)
+                                           sample_with_replacement, seed, dtype, max_inner_iter, mixed_resolve_iters)
         devs = np.ascontiguousarray(np.asarray(devices, np.int32))
         h = C.c_void_p()
         L.check(self.lib.stc_group_create(L.ptr(devs, C.c_int32), devs.size, C.byref(cfg), C.byref(h)))
@@ -354,7 +356,7 @@ class LdaGroup:
 def _as_device(ctx, data, dtype):
     if isinstance(data, DeviceCsr):
         return data, False
-    return DeviceCsr.upload(ctx, data, dtype), True
+    return DeviceCsr.upload(ctx, data, L.corpus_dtype(dtype)), True
 
 
 class LDAModel:

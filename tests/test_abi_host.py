@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     from stc import _lib
 
     assert set(_lib.SIGNATURES) == set(_declared_symbols())
-    assert lib.stc_abi_version() == 1
+    assert lib.stc_abi_version() == 2
 
 
 def test_library_is_gfx950_code():

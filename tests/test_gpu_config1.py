@@ -13,8 +13,10 @@ Spark's MT19937 draws (λ₀, minibatch membership, γ₀) cannot be replayed wi
 injected — identical inputs on both sides — and the GPU's 10 stc_lda_step calls are compared with
 the oracle's 10 submit_minibatch calls against the north-star bars (topicsMatrix within 1e-4
 relative, logPerplexity within 1e-5 relative, identical top-10 terms per topic): the fp64 path (Spark's
-precision) at 1e-9 / 1e-10 with identical top-10 terms; the fp32 path at 1e-3 on the topicsMatrix (see
-below), 1e-5 on logPerplexity, identical top-10 terms.
+precision) at 1e-9 / 1e-10 with identical top-10 terms; the mixed mode (STC_MIXED: the fp32 E-step, the
+documents past 500 fp32 iterations re-solved in fp64) at the north-star bars themselves, 1e-4 / 1e-5 with
+identical top-10 terms; the fp32 path at 1e-3 on the topicsMatrix (see below), 1e-5 on logPerplexity,
+identical top-10 terms.
 """
 import os
 
@@ -102,7 +104,9 @@ def test_config1_pipeline_hashing_idf_online_lda(ctx, oracle, books):
     # convergence, and the fp32 trajectory stops at a different iterate than the fp64 one: measured
     # 4.8e-4 relative on the topicsMatrix, so fp32 gets 1e-3 here (the fp64 path meets the north-star
     # 1e-4 bar by five orders of magnitude)
-    for dtype, tol_lam, tol_lp in (("f64", 1e-9, 1e-10), ("f32", 1e-3, 1e-5)):
+    # mixed: that book (and the two at ≈ 575 iterations) are re-solved in fp64, every other document keeps its
+    # fp32 E-step — the north-star bars hold (tools: the CPU emulation in DESIGN.md §4 predicts ≈ 2e-7)
+    for dtype, tol_lam, tol_lp in (("f64", 1e-9, 1e-10), ("mixed", 1e-4, 1e-5), ("f32", 1e-3, 1e-5)):
         h = stc.LdaHandle(ctx, K, NF, mini_batch_fraction=frac, optimize_doc_concentration=False, dtype=dtype)
         dc = stc.DeviceCsr.upload(ctx, corpus, stc.STC_F32 if dtype == "f32" else stc.STC_F64)
         h.set_corpus(dc, D)
@@ -118,4 +122,7 @@ def test_config1_pipeline_hashing_idf_online_lda(ctx, oracle, books):
         assert abs(lp - lp_o) / abs(lp_o) < tol_lp, (dtype, lp, lp_o)
         idx, _ = h.describe(10)
         assert np.array_equal(idx, idx_o), dtype
+        if dtype == "mixed":  # the slow books went through the fp64 re-solve
+            assert h.counters()["kernels"]["mixed_docs"] >= 3
+        print(f"config1 {dtype}: topicsMatrix rel {rel:.3e}, logPerplexity rel {abs(lp - lp_o) / abs(lp_o):.3e}")
         dc.free()
