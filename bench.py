@@ -495,6 +495,8 @@ def kernel_name(launched):
     if not fams:
         return "no E-step launch in the timed steps"
     main = max(fams, key=lambda f: fams[f])
+    if launched.get("mixed_resolves") and "k_estep_grid" in fams:  # mixed: the fp32 pass is the step's kernel
+        main = "k_estep_grid"
     extra = {f: n for f, n in launched.items() if f != main}
     return KERNEL_TEXT[main] + (f"; also launched: {extra}" if extra else "")
 

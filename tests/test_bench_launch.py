@@ -113,6 +113,9 @@ def test_kernel_name_comes_from_the_launch_counters():
     n = bench.kernel_name({"k_estep_tgrid64": 19, "k_estep_wide": 1, "team_fallback": 1})
     assert n.startswith("k_estep_tgrid64") and "team_fallback" in n
     assert bench.kernel_name({}) == "no E-step launch in the timed steps"
+    # mixed: the fp32 pass names the step, the fp64 re-solve is listed beside it
+    m = bench.kernel_name({"k_estep_rows64": 10, "k_estep_grid": 10, "mixed_resolves": 10, "mixed_docs": 6300})
+    assert m.startswith("k_estep_grid_pers") and "mixed_docs" in m
 
 
 def test_group_launch_at_one_gpu(monkeypatch, capsys):

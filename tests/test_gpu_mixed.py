@@ -42,12 +42,12 @@ def test_mixed_resolves_exactly_the_slow_documents(ctx, k):
     lam = rng.gamma(100.0, 0.01, size=(V, k))
     ids = rng.permutation(D)
     g0 = rng.gamma(100.0, 0.01, size=(D, k))
-    thr = 60
     h64, _ = _handle(ctx, corpus, k, "f64", lam)
     h32, _ = _handle(ctx, corpus, k, "f32", lam)
-    hm, _ = _handle(ctx, corpus, k, "mixed", lam, mixed_resolve_iters=thr)
     g64, _, it64 = h64.estep(ids, g0)
     g32, _, it32 = h32.estep(ids, g0)
+    thr = int(np.percentile(it32[it32 > 0], 60))  # about 40 % of the documents above it
+    hm, _ = _handle(ctx, corpus, k, "mixed", lam, mixed_resolve_iters=thr)
     c0 = hm.counters()["kernels"]
     gm, _, itm = hm.estep(ids, g0)
     c1 = hm.counters()["kernels"]
@@ -73,7 +73,7 @@ def test_mixed_training_steps_and_inference(ctx, oracle):
     corpus = random_corpus(rng, D, V, 1, 120, empty_every=19)
     lam0 = rng.gamma(100.0, 0.01, size=(V, k))
     hm, dm = _handle(ctx, corpus, k, "mixed", lam0, mini_batch_fraction=0.3, optimize_doc_concentration=True,
-                     mixed_resolve_iters=40)
+                     mixed_resolve_iters=300)
     alpha, eta = oracle.resolve_alpha_eta(k)
     st = oracle.OnlineLDAState(lam=lam0.T.copy(), alpha=alpha, eta=eta, corpus_size=D, mini_batch_fraction=0.3,
                                optimize_doc_concentration=True)
