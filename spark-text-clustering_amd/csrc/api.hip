@@ -916,6 +916,9 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   a.indptr = L.corpus->indptr.as<int64_t>();
   a.indices = L.corpus->indices.as<int32_t>();
   a.values = L.mixed ? L.vals32.as<T>() : L.corpus->values.as<T>();
+  // mixed: the fp32 pass stops a document at mixed_thr + 1 iterations — it is re-solved in fp64 anyway, so the
+  // fp32 iterations past the threshold (up to ≈ 300 per such document at the bench state) are not spent
+  if (L.mixed) a.max_iter = std::min(a.max_iter, L.mixed_thr + 1);
   a.batch = L.batch.as<int32_t>();
   a.orig = L.orig.as<int32_t>();
   a.bptr = L.bptr.as<int64_t>();
@@ -1307,8 +1310,19 @@ void next_impl(stc_lda& L, stc_step_stats* st) {
   sample_draw(L, draw + 1, L.side, &L.side_scan_tmp);
   HIP_CHECK(hipEventRecord(L.ev_samp, L.side));
   L.samp_pending = true;
-  L.pre_inflight = true;
   L.pre_draw = draw + 1;
+  if (c.coll()) {
+    L.pre_inflight = true;  // the global size rides on this step's collective (train_tail reads it back)
+  } else {
+    // one rank: the draw's size is already global — read it back on the side stream as soon as it is sampled
+    // (during this step's E-step), so the next call enqueues its batch preparation at once and the side stream
+    // builds it under this step's sstats and M-step; read back in train_tail, after the E-step and sstats, the
+    // preparation only started under the M-step and the next E-step waited for it (the "sample" phase, 0.29 ms)
+    HIP_CHECK(hipMemcpyAsync(L.hpre, L.dcnt.p, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, L.side));
+    HIP_CHECK(hipEventRecord(L.ev_pre, L.side));
+    L.pre_inflight = false;
+    L.pre_valid = true;
+  }
   estep_and_stats<T>(L, n, ns32, E, g0, L.iteration + 1, true);
   train_tail<T>(L, n, E, st);
   L.prep_side = true;
