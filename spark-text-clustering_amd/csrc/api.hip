@@ -121,6 +121,11 @@ struct stc_lda {
   hipStream_t cstream = nullptr;
   hipEvent_t ev_ss[16] = {}, ev_rs[16] = {};
   int64_t Vs = 0, vpad = 0;
+  // one rank: sstats stamps the rows it writes (rowstamp[v] = the step's id) and the M-step reads the other
+  // rows as zero, so stat is not cleared every step (V·kp·T bytes: 4.2 GB at config 5)
+  DevBuf rowstamp;
+  int32_t stamp_seq = 0, step_sid = 0;
+  bool step_stamped = false;
   bool lam_stale = false;  // rows outside this rank's slice are out of date (sharded M-step)
 
   // minibatch draws: Spark's next() advances its generator on every call, empty batches included
@@ -445,6 +450,11 @@ void ensure_layout(stc_lda& L) {
   L.stat.reserve(L.tsize * vpad * L.kp);
   L.logscale.reserve(8 * vpad);
   L.colpart.reserve(8 * (vpad / RB) * L.k);
+  if ((size_t)(4 * vpad) > L.rowstamp.bytes) {  // a new stamp array: no row is this step's
+    L.rowstamp.reserve(4 * vpad);
+    HIP_CHECK(hipMemsetAsync(L.rowstamp.p, 0xFF, L.rowstamp.bytes, L.ctx->stream));
+    L.stamp_seq = 0;
+  }
   L.shards = want;
   L.Vs = Vs;
   L.vpad = vpad;
@@ -951,7 +961,15 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
     HIP_CHECK(hipMemsetAsync(L.small.p, 0, sizeof(double) * (L.k + 1), s));
     HIP_CHECK(hipMemsetAsync(L.stats4.p, 0, sizeof(int64_t) * 4, s));
   }
-  HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.vpad * L.kp, s));  // padded rows stay zero
+  // a training step of one rank stamps its rows instead of clearing stat (the M-step reads unstamped rows as
+  // zero); sharded steps clear it — the reduce-scatter sums every row of every rank
+  L.step_stamped = split && !sharded(L);
+  if (L.step_stamped) {
+    L.stamp_seq = L.stamp_seq == INT32_MAX ? 0 : L.stamp_seq + 1;  // (never −1, the fresh array's value)
+    L.step_sid = L.stamp_seq;
+  } else {
+    HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.vpad * L.kp, s));  // padded rows stay zero
+  }
   if (E > 0) {
     size_t tb = L.sort_tmp.bytes;
     HIP_CHECK(term_sort(L.sort_tmp.p, tb, L.keys.as<uint32_t>(), L.skeys.as<uint32_t>(), L.vals.as<uint64_t>(),
@@ -960,7 +978,8 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   const lda::StatMap lay = split ? stat_layout(L) : lda::StatMap{};
   if (lay.nsub <= 1) {
     lda::launch_sstats<T>(s, L.skeys.as<uint32_t>(), L.svals.as<uint64_t>(), E, L.r.as<T>(), L.eth.as<T>(), L.kp,
-                          L.stat.as<T>(), L.headbuf.as<T>(), L.tailbuf.as<T>());
+                          L.stat.as<T>(), L.headbuf.as<T>(), L.tailbuf.as<T>(), lda::StatMap{},
+                          L.step_stamped ? L.rowstamp.as<int32_t>() : nullptr, L.step_sid);
   } else {
     for (int j = 0; j < lay.nsub; ++j) {
       lda::StatMap m = lay;
@@ -984,7 +1003,8 @@ void mstep_slice(stc_lda& L, int r, double rho, double scale, const double* gate
   lda::launch_lambda_eeb<T>(L.ctx->stream, true, L.lam.as<double>() + v0 * L.k, L.stat.as<T>() + v0 * L.kp,
                             L.Bp.as<T>() + v0 * L.kp, L.logscale.as<double>() + v0, vn, L.k, L.kp, rho, scale,
                             L.eta, gate, L.colpart.as<double>() + (int64_t)r * nbs * L.k, nbs,
-                            L.mixed ? L.Bp64.as<double>() + v0 * L.kp : nullptr);
+                            L.mixed ? L.Bp64.as<double>() + v0 * L.kp : nullptr,
+                            L.step_stamped ? L.rowstamp.as<int32_t>() + v0 : nullptr, L.step_sid);
 }
 // the same pass over sub-chunk j of slice r, whose summed stat rows sit at the sub-chunk layout's
 // physical rows (stat_layout); λ / expElogβ' / logscale / colsum partials at their canonical rows

@@ -381,7 +381,8 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
                                                 const T* __restrict__ r,
                                                 const T* __restrict__ eth, int kp, T* __restrict__ stat,
                                                 T* __restrict__ headbuf, T* __restrict__ tailbuf,
-                                                int64_t nchunks, StatMap map) {
+                                                int64_t nchunks, StatMap map, int32_t* __restrict__ stamp,
+                                                int32_t sid) {
   const int c0 = (int)blockIdx.y * 64 * Q;  // this slab's first topic column
   // kU entries in flight per wave: their (term, r, doc) are read out of the lanes that loaded them
   // (v_readlane: wave-uniform, so the eθ' row address is scalar) and their eθ' rows are all requested
@@ -410,9 +411,14 @@ __global__ __launch_bounds__(256) void k_sstats(const uint32_t* __restrict__ ske
       for (int q = 0; q < Q; ++q) acc[q] = T(0);
       return;
     }
-    if (v == first && start_mid) dst = headbuf + chunk * kp;
-    else if (v == last && cont) dst = tailbuf + chunk * kp;
-    else dst = stat + stat_row(map, v) * kp;
+    if (v == first && start_mid) {
+      dst = headbuf + chunk * kp;
+    } else if (v == last && cont) {
+      dst = tailbuf + chunk * kp;
+    } else {
+      dst = stat + stat_row(map, v) * kp;
+      if (stamp && blockIdx.y == 0 && lane == 0) stamp[v] = sid;  // row v holds this step's sums
+    }
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int col = c0 + lane + 64 * q;
@@ -517,7 +523,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
                                                int kp, T* __restrict__ stat,
                                                const T* __restrict__ headbuf,
                                                const T* __restrict__ tailbuf, int64_t nchunks,
-                                               StatMap map) {
+                                               StatMap map, int32_t* __restrict__ stamp, int32_t sid) {
   // the run's owner (the chunk where it starts) adds the partials of the chunks the run covers, in
   // chunk order: chunk by chunk up to a kTile boundary, then whole full tiles (k_fixup_tiles' sums),
   // then chunk by chunk to the run's end.  kG chunks / tiles are fetched at a time (keys and partials).
@@ -621,14 +627,17 @@ __global__ __launch_bounds__(256) void k_fixup(const uint32_t* __restrict__ skey
     const int col = c0 + lane + 64 * q;
     if (col < kp) stat[stat_row(map, last) * kp + col] = acc[q];
   }
+  if (stamp && blockIdx.y == 0 && lane == 0) stamp[last] = sid;
 }
 
 template <typename T, int Q>
 static void sstats_q(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, int64_t E,
-                     const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf, const StatMap& map) {
+                     const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf, const StatMap& map,
+                     int32_t* stamp, int32_t sid) {
   const int64_t nchunks = ceil_div(E, kChunk);
   const dim3 grid((unsigned)ceil_div(nchunks, 4), (unsigned)ceil_div(kp, 64 * Q));
-  k_sstats<T, Q><<<grid, 256, 0, s>>>(skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, nchunks, map);
+  k_sstats<T, Q><<<grid, 256, 0, s>>>(skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, nchunks, map, stamp,
+                                      sid);
   KERNEL_CHECK();
   const int64_t ntiles = ceil_div(nchunks, (int64_t)kTile);
   if (ntiles > 1) {
@@ -636,14 +645,16 @@ static void sstats_q(hipStream_t s, const uint32_t* skeys, const uint64_t* svals
                                                                                    nchunks, map);
     KERNEL_CHECK();
   }
-  k_fixup<T, Q><<<grid, 256, 0, s>>>(skeys, E, kp, stat, headbuf, tailbuf, nchunks, map);
+  k_fixup<T, Q><<<grid, 256, 0, s>>>(skeys, E, kp, stat, headbuf, tailbuf, nchunks, map, stamp, sid);
   KERNEL_CHECK();
 }
 
 template <typename T>
 void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, int64_t E,
-                   const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf, const StatMap& map) {
+                   const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf, const StatMap& map,
+                   int32_t* stamp, int32_t sid) {
   if (E == 0) return;
+  if (stamp && map.sub >= 0) throw Error(STC_ERR_INVALID_ARG, "sstats: row stamps with a sub-chunk map");
   if (kp > 4096) throw Error(STC_ERR_INVALID_ARG, "k > 4096 topics is not supported");
   if (map.sub >= 0 && (map.vs == 0 || map.vsj == 0 || map.nsub < 1 || map.sub >= map.nsub ||
                        (uint64_t)(map.nsub - 1) * map.vsj >= map.vs))
@@ -651,10 +662,10 @@ void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, 
   // slab width: ≤ 4 (fp64) / 8 (fp32) columns per lane — the whole row when it is that narrow
   const int q = (kp + 63) / 64;
   constexpr int QMAX = sizeof(T) == 8 ? 4 : 8;
-  if (q <= 1) sstats_q<T, 1>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, map);
-  else if (q <= 2) sstats_q<T, 2>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, map);
-  else if (q <= 4 || QMAX == 4) sstats_q<T, 4>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, map);
-  else sstats_q<T, QMAX>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, map);
+  if (q <= 1) sstats_q<T, 1>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, map, stamp, sid);
+  else if (q <= 2) sstats_q<T, 2>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, map, stamp, sid);
+  else if (q <= 4 || QMAX == 4) sstats_q<T, 4>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, map, stamp, sid);
+  else sstats_q<T, QMAX>(s, skeys, svals, E, r, eth, kp, stat, headbuf, tailbuf, map, stamp, sid);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -696,7 +707,8 @@ __global__ __launch_bounds__(256, 5) void k_lambda_eeb(double* __restrict__ lam,
                                                     T* __restrict__ Bp, double* __restrict__ logscale,
                                                     int64_t V, int k, int kp, double rho, double scale,
                                                     double eta, const double* __restrict__ gate,
-                                                    double* __restrict__ colpart, double* __restrict__ Bp64) {
+                                                    double* __restrict__ colpart, double* __restrict__ Bp64,
+                                                    const int32_t* __restrict__ stamp, int32_t sid) {
   if (gate && !(gate[0] > 0.0)) return;  // Spark: no non-empty docs ⇒ no update
   __shared__ double s_acc[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -710,6 +722,9 @@ __global__ __launch_bounds__(256, 5) void k_lambda_eeb(double* __restrict__ lam,
     if (v >= V) break;
     double e[Q];
     double m = -INFINITY;
+    // a row no sstats launch of this step wrote (stamp ≠ sid) holds stale sums: read as 0, as the cleared
+    // stat row was (0·Bp·scale + η = η bit for bit), and its stat / Bp bytes are not fetched
+    const bool live = !UPDATE || !stamp || stamp[v] == sid;
 #pragma unroll
     for (int q0 = 0; q0 < Q; q0 += QC) {
       double lv[QC], sv[QC], bv[QC];
@@ -718,8 +733,8 @@ __global__ __launch_bounds__(256, 5) void k_lambda_eeb(double* __restrict__ lam,
         const int t = lane + 64 * (q0 + j);
         lv[j] = t < k ? lam[v * k + t] : 1.0;
         if (UPDATE) {
-          sv[j] = t < k ? (double)stat[v * kp + t] : 0.0;
-          bv[j] = t < k ? (double)Bp[v * kp + t] : 0.0;
+          sv[j] = live && t < k ? (double)stat[v * kp + t] : 0.0;
+          bv[j] = live && t < k ? (double)Bp[v * kp + t] : 0.0;
         }
       }
 #pragma unroll
@@ -774,7 +789,8 @@ __global__ __launch_bounds__(256) void k_lambda_eeb_wide(double* __restrict__ la
                                                          T* __restrict__ Bp, double* __restrict__ logscale,
                                                          int64_t V, int k, int kp, double rho, double scale,
                                                          double eta, const double* __restrict__ gate,
-                                                         double* __restrict__ colpart, double* __restrict__ Bp64) {
+                                                         double* __restrict__ colpart, double* __restrict__ Bp64,
+                                                         const int32_t* __restrict__ stamp, int32_t sid) {
   if (gate && !(gate[0] > 0.0)) return;
   __shared__ double s_max[2][4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -784,13 +800,14 @@ __global__ __launch_bounds__(256) void k_lambda_eeb_wide(double* __restrict__ la
 #pragma unroll
   for (int q = 0; q < Q; ++q) acc[q] = 0.0;
   auto load = [&](int64_t v) {
+    const bool live = !UPDATE || !stamp || stamp[v] == sid;  // (as k_lambda_eeb)
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int t = tid + 256 * q;
       lv[q] = t < k ? lam[v * k + t] : 1.0;
       if (UPDATE) {
-        sv[q] = t < k ? (double)stat[v * kp + t] : 0.0;
-        bv[q] = t < k ? (double)Bp[v * kp + t] : 0.0;
+        sv[q] = live && t < k ? (double)stat[v * kp + t] : 0.0;
+        bv[q] = live && t < k ? (double)Bp[v * kp + t] : 0.0;
       }
     }
   };
@@ -848,7 +865,7 @@ __global__ __launch_bounds__(256) void k_lambda_eeb_wide(double* __restrict__ la
 template <typename T>
 void launch_lambda_eeb(hipStream_t s, bool update, double* lam, const T* stat, T* Bp, double* logscale,
                        int64_t V, int k, int kp, double rho, double scale, double eta, const double* gate,
-                       double* colpart, int64_t nblocks, double* Bp64) {
+                       double* colpart, int64_t nblocks, double* Bp64, const int32_t* stamp, int32_t sid) {
   if (nblocks <= 0) return;
   if (kp > 256) {  // a row per workgroup
     const int qw = (kp + 255) / 256;
@@ -857,11 +874,11 @@ void launch_lambda_eeb(hipStream_t s, bool update, double* lam, const T* stat, T
     if (update)                                                                                          \
       k_lambda_eeb_wide<T, QQ, true><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, logscale, V, k, kp, \
                                                                         rho, scale, eta, gate, colpart,   \
-                                                                        Bp64);                           \
+                                                                        Bp64, stamp, sid);               \
     else                                                                                                 \
       k_lambda_eeb_wide<T, QQ, false><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, logscale, V, k,    \
                                                                          kp, rho, scale, eta, gate, colpart, \
-                                                                         Bp64);                          \
+                                                                         Bp64, stamp, sid);              \
   } while (0)
     if (qw <= 2) STC_LEEBW(2);
     else if (qw <= 4) STC_LEEBW(4);
@@ -877,10 +894,10 @@ void launch_lambda_eeb(hipStream_t s, bool update, double* lam, const T* stat, T
   do {                                                                                                  \
     if (update)                                                                                         \
       k_lambda_eeb<T, QQ, true><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, logscale, V, k, kp,   \
-                                                                   rho, scale, eta, gate, colpart, Bp64); \
+                                                                   rho, scale, eta, gate, colpart, Bp64, stamp, sid); \
     else                                                                                                \
       k_lambda_eeb<T, QQ, false><<<(unsigned)nblocks, 256, 0, s>>>(lam, stat, Bp, logscale, V, k, kp,  \
-                                                                    rho, scale, eta, gate, colpart, Bp64); \
+                                                                    rho, scale, eta, gate, colpart, Bp64, stamp, sid); \
   } while (0)
   if (q <= 1) STC_LEEB(1);
   else if (q <= 2) STC_LEEB(2);
@@ -1473,9 +1490,10 @@ void launch_to_f32(hipStream_t s, const double* in, float* out, int64_t n) {
   template int estep_lds_rows<T>(int, int, int);                                                  \
   template void launch_estep<T>(hipStream_t, const EStepArgs<T>&, bool, bool);                    \
   template void launch_sstats<T>(hipStream_t, const uint32_t*, const uint64_t*, int64_t, const T*, \
-                                 const T*, int, T*, T*, T*, const StatMap&);                      \
+                                 const T*, int, T*, T*, T*, const StatMap&, int32_t*, int32_t);   \
   template void launch_lambda_eeb<T>(hipStream_t, bool, double*, const T*, T*, double*, int64_t, int, \
-                                     int, double, double, double, const double*, double*, int64_t, double*); \
+                                     int, double, double, double, const double*, double*, int64_t, double*, \
+                                     const int32_t*, int32_t);                                    \
   template void launch_logphat<T>(hipStream_t, const T*, const int32_t*, int64_t, int, double*, double*);  \
   template void launch_topics_bound<T>(hipStream_t, const double*, const double*, int64_t, int,   \
                                        double, double*, int64_t);                                 \

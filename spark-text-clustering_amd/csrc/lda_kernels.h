@@ -167,10 +167,12 @@ __host__ __device__ __forceinline__ int64_t stat_row(const StatMap& m, uint32_t 
   return (int64_t)m.n * j * m.vsj + (int64_t)r * w + (rem - (int64_t)j * m.vsj);
 }
 
+// stamp (one rank, canonical rows only; may be null): stamp[v] = sid for every row v this launch writes, so
+// the M-step can tell this step's rows from stale ones and stat needs no clearing (launch_lambda_eeb)
 template <typename T>
 void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, int64_t E,
                    const T* r, const T* eth, int kp, T* stat, T* headbuf, T* tailbuf,
-                   const StatMap& map = StatMap{});
+                   const StatMap& map = StatMap{}, int32_t* stamp = nullptr, int32_t sid = 0);
 
 // γ₀ of n slots' members (gamma_sample, keyed as the E-step kernels key it) into out[member·k + t]
 template <typename T>
@@ -178,11 +180,13 @@ void launch_gamma0(hipStream_t s, const int32_t* batch, const int32_t* orig, int
                    int64_t iteration, int rank, int key_mode, int64_t doc_id_base, double shape, T* out);
 
 // the fused M-step pass (update = true: λ update; both: expElogβ' rows, logscale, colsum partials)
-// Bp64 (STC_MIXED, T = float only; may be null): the same rows in fp64 at the same m_v, for the re-solve
+// Bp64 (STC_MIXED, T = float only; may be null): the same rows in fp64 at the same m_v, for the re-solve.
+// stamp (may be null): rows with stamp[v] ≠ sid take stat = 0 without reading stat / Bp (launch_sstats)
 template <typename T>
 void launch_lambda_eeb(hipStream_t s, bool update, double* lam, const T* stat, T* Bp, double* logscale,
                        int64_t V, int k, int kp, double rho, double scale, double eta, const double* gate,
-                       double* colpart, int64_t nblocks, double* Bp64 = nullptr);
+                       double* colpart, int64_t nblocks, double* Bp64 = nullptr, const int32_t* stamp = nullptr,
+                       int32_t sid = 0);
 // colsum (block order), psic[0, k) = ψ(colsum), psic[k, 2k) = exp(−ψ(colsum))
 void launch_colsum_reduce(hipStream_t s, const double* colpart, int64_t nblocks, int k,
                           const double* gate, double* colsum, double* psic);
