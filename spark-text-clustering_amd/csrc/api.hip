@@ -279,7 +279,7 @@ void poll_wait(Ctx& c, Query query, Block block, const char* what) {
   }
   check_comm(c);
   const auto t0 = std::chrono::steady_clock::now();
-  for (int spin = 0;; ++spin) {
+  for (;;) {
     const hipError_t e = query();
     if (e == hipSuccess) return;
     if (e != hipErrorNotReady) HIP_CHECK(e);
@@ -297,9 +297,10 @@ void poll_wait(Ctx& c, Query query, Block block, const char* what) {
                                     " ms (STC_COLL_TIMEOUT_MS = " + std::to_string(c.coll_timeout_ms) +
                                     "): a collective's peer never arrived; communicator aborted");
     }
-    // spin first (a step's wait is usually short), then sleep in 20 µs steps
-    if (spin < 2000) std::this_thread::yield();
-    else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    // yield for the first 20 ms (a step's wait is milliseconds, and a sleep costs its timer slack — ≈ 50 µs
+    // on Linux — per wait), then sleep in 100 µs steps
+    if (ms < 20) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(100));
   }
 }
 void wait_stream(Ctx& c, hipStream_t s) {
