@@ -25,7 +25,7 @@ import org.apache.spark.sql.{DataFrame, Dataset, Row, SparkSession}
 class HipLDA(override val uid: String) extends LDA(uid) {
   def this() = this(Identifiable.randomUID("hipLDA"))
 
-  /** "f64" (default: Spark's Double E-step) or "f32" */
+  /** "f64" (default: Spark's Double E-step), "mixed" (fp32 E-step + fp64 re-solve of the slow documents) or "f32" */
   private var dtype: String = "f64"
   def setDtype(d: String): this.type = { dtype = d; this }
 

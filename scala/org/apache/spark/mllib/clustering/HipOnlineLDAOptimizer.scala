@@ -82,12 +82,14 @@ final class HipOnlineLDAOptimizer extends LDAOptimizer {
 
   def setSampleWithReplacement(b: Boolean): this.type = { this.sampleWithReplacement = b; this }
 
-  /** "f64" (default, Spark's Double arithmetic) or "f32" */
+  /** "f64" (default, Spark's Double arithmetic), "mixed" (the fp32 E-step with its slowly converging
+   *  documents re-solved in fp64: the north-star parity bars at ≈ 1.9× the f64 rate) or "f32" */
   def setDtype(d: String): this.type = {
     dtype = d.toLowerCase match {
       case "f64" | "double" => StcNative.F64
+      case "mixed" => StcNative.MIXED
       case "f32" | "float" => StcNative.F32
-      case other => throw new IllegalArgumentException(s"dtype must be f64 or f32 but got $other")
+      case other => throw new IllegalArgumentException(s"dtype must be f64, mixed or f32 but got $other")
     }
     this
   }

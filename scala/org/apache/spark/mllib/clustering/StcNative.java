@@ -16,6 +16,8 @@ public final class StcNative {
   private StcNative() {}
 
   public static final int F32 = 0, F64 = 1;
+  /** LDA dtype only: the fp32 E-step with the documents past 500 fp32 iterations re-solved in fp64 (stc.h STC_MIXED) */
+  public static final int MIXED = 2;
   public static final int HASH_STANDARD = 0, HASH_SPARK24 = 1;
   public static final int LAYOUT_VK = 0, LAYOUT_KV = 1;
 
