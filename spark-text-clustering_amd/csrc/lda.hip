@@ -678,7 +678,10 @@ void launch_sstats(hipStream_t s, const uint32_t* skeys, const uint64_t* svals, 
 // E-step (EStepArgs::psic), so a row needs only its own λ and the pass fuses with the λ update.
 // m_v only has to be common to the row and to logscale, not the exact maximum: the fp32 build takes
 // it from an fp32 DPP max and evaluates the exponential as 2^n · 2^f with the integer/fraction split
-// done in fp64, so the fp32 argument never loses the bits of a large |ψ(λ)|.
+// done in fp64, so the fp32 argument never loses the bits of a large |ψ(λ)|.  The fp64 build takes
+// m_v = ψ(max_t λ_vt) (ψ is increasing: one ψ per row instead of one per element) and evaluates
+// exp(ψ(λ) − m_v) as exp_digamma_minus_d, without a logarithm per element (round 6: config 5's
+// M-step was fp64-VALU-bound, 2,934 → 2,337 instructions per row at k = 2000).
 __device__ __forceinline__ float exp_scaled(double x, float) {
   const double y = x * 1.4426950408889634;  // log2 e
   const double n = floor(y);
@@ -746,16 +749,30 @@ __global__ __launch_bounds__(256, 5) void k_lambda_eeb(double* __restrict__ lam,
           if (UPDATE) lam[v * k + t] = nl;
           acc[q] += nl;
         }
-        e[q] = t < k ? digamma_fast_d(nl) : -INFINITY;
-        m = fmax(m, e[q]);
+        if constexpr (sizeof(T) == 8) {  // ψ is increasing: max_t ψ(λ_vt) = ψ(max_t λ_vt)
+          e[q] = nl;
+          if (t < k) m = fmax(m, nl);
+        } else {
+          e[q] = t < k ? digamma_fast_d(nl) : -INFINITY;
+          m = fmax(m, e[q]);
+        }
       }
     }
     m = row_max(m, T());
     T* br = Bp + v * kp;
+    if constexpr (sizeof(T) == 8) {  // one ψ per row, and exp(ψ(λ) − m_v) without a logarithm per element
+      m = digamma_fast_d(m);
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int t = lane + 64 * q;
-      if (t < kp) br[t] = t < k ? exp_scaled(e[q] - m, T()) : T(0);
+      for (int q = 0; q < Q; ++q) {
+        const int t = lane + 64 * q;
+        if (t < kp) br[t] = t < k ? exp_digamma_minus_d(e[q], m) : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int t = lane + 64 * q;
+        if (t < kp) br[t] = t < k ? exp_scaled(e[q] - m, T()) : T(0);
+      }
     }
     if constexpr (sizeof(T) == 4) {  // STC_MIXED: the fp64 rows of the re-solve, at the same m_v
       if (Bp64) {
@@ -785,7 +802,7 @@ __global__ __launch_bounds__(256, 5) void k_lambda_eeb(double* __restrict__ lam,
 // waves through LDS (double-buffered by row parity: one barrier per row).  Each topic's colsum partial
 // is one thread's running sum over the block's rows in row order.
 template <typename T, int Q, bool UPDATE>
-__global__ __launch_bounds__(256) void k_lambda_eeb_wide(double* __restrict__ lam, const T* __restrict__ stat,
+__global__ __launch_bounds__(256, Q <= 8 ? 3 : 1) void k_lambda_eeb_wide(double* __restrict__ lam, const T* __restrict__ stat,
                                                          T* __restrict__ Bp, double* __restrict__ logscale,
                                                          int64_t V, int k, int kp, double rho, double scale,
                                                          double eta, const double* __restrict__ gate,
@@ -831,18 +848,31 @@ __global__ __launch_bounds__(256) void k_lambda_eeb_wide(double* __restrict__ la
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const int t = tid + 256 * q;
-      e[q] = t < k ? digamma_fast_d(e[q]) : -INFINITY;
-      m = fmax(m, e[q]);
+      if constexpr (sizeof(T) == 8) {  // (as k_lambda_eeb) the row max of λ, one ψ per row
+        if (t < k) m = fmax(m, e[q]);
+      } else {
+        e[q] = t < k ? digamma_fast_d(e[q]) : -INFINITY;
+        m = fmax(m, e[q]);
+      }
     }
     m = row_max(m, T());
     if (lane == 0) s_max[i & 1][w] = m;
     __syncthreads();
     m = fmax(fmax(s_max[i & 1][0], s_max[i & 1][1]), fmax(s_max[i & 1][2], s_max[i & 1][3]));
     T* br = Bp + v * kp;
+    if constexpr (sizeof(T) == 8) {
+      m = digamma_fast_d(m);
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int t = tid + 256 * q;
-      if (t < kp) br[t] = t < k ? exp_scaled(e[q] - m, T()) : T(0);
+      for (int q = 0; q < Q; ++q) {
+        const int t = tid + 256 * q;
+        if (t < kp) br[t] = t < k ? exp_digamma_minus_d(e[q], m) : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int t = tid + 256 * q;
+        if (t < kp) br[t] = t < k ? exp_scaled(e[q] - m, T()) : T(0);
+      }
     }
     if constexpr (sizeof(T) == 4) {  // STC_MIXED: the fp64 rows of the re-solve, at the same m_v
       if (Bp64) {

@@ -45,6 +45,9 @@ constexpr int kTMaxP = 8;               // members at most (k ≤ 832)
 #ifndef TG_MIRROR
 #define TG_MIRROR 1  // the ψ wave's Σ|Δγ| reduction moved to the idle wave of its topic set (0: on the ψ wave)
 #endif
+// s_sleep units (64 cycles) between the exchange's poll rounds (config 4, 8-step A/B: 1 → E-step 147.5 ms,
+// 3 → 148.8 ms)
+constexpr int kTPollSleep = 1;
 #ifndef TG_LOAD_BATCH
 #define TG_LOAD_BATCH 2                 // row sets whose block loads are in flight together
 #endif
@@ -334,30 +337,41 @@ __device__ __forceinline__ int tg_iterate(const EStepArgs<double>& a, TLds<KL>& 
     double phi = 0.0, dsum = 0.0;
     {
       const int base = (int)(epoch & 1) * t.P * t.xstride;
-      double vr[kTMaxP], vd[kTMaxP];
-      for (unsigned spins = 0;; ++spins) {
-        bool ok = true;
+      // rows: each worker lane polls its row's granule of every partner; the Σ|Δγ| granules: lane m polls
+      // partner m's only and the wave takes the values by readlane (every lane polling every partner's D
+      // granule was most of the poll traffic queued at this CU — the hand-off's price, MI355X_MICROARCH.md
+      // handoff-1to1 — for values that are the same in every lane)
+      // A granule already received is not requested again (got: one bit per partner, and bit kTMaxP for the
+      // lane's D granule): every poll round re-requesting the partners that had arrived kept the queue full.
+      double vr[kTMaxP], vdl = 0.0;
+      const bool dl = lane < t.P && lane != t.member;
+      unsigned need = dl ? 1u << kTMaxP : 0u;
 #pragma unroll
-        for (int m = 0; m < kTMaxP; ++m) {
-          vr[m] = 0.0;
-          vd[m] = 0.0;
-          if (m < t.P && m != t.member) {
-            if (wv) ok &= get_granule<double>(t.rs, base + m * t.xstride + qn, epoch, vr[m]);
-            ok &= get_granule<double>(t.rs, base + m * t.xstride + kTSlotD, epoch, vd[m]);
+      for (int m = 0; m < kTMaxP; ++m) {
+        vr[m] = 0.0;
+        if (m < t.P && m != t.member && wv) need |= 1u << m;
+      }
+      for (unsigned spins = 0;; ++spins) {
+#pragma unroll
+        for (int m = 0; m < kTMaxP; ++m)
+          if (need & (1u << m)) {
+            if (get_granule<double>(t.rs, base + m * t.xstride + qn, epoch, vr[m])) need &= ~(1u << m);
           }
+        if (need & (1u << kTMaxP)) {
+          if (get_granule<double>(t.rs, base + lane * t.xstride + kTSlotD, epoch, vdl)) need &= ~(1u << kTMaxP);
         }
-        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        if (__builtin_amdgcn_ballot_w64(need != 0) == 0) break;
         if (spin_give_up(spins, t.tmo, t.spin_limit)) {
           *s_abort = 1;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(kTPollSleep);
       }
 #pragma unroll
       for (int m = 0; m < kTMaxP; ++m) {
         if (m < t.P) {
           phi += m == t.member ? part : vr[m];
-          dsum += m == t.member ? dmine : vd[m];
+          dsum += m == t.member ? dmine : readlane_t(vdl, m);
         }
       }
       if (!wv) phi = 0.0;

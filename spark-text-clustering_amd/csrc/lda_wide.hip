@@ -795,7 +795,8 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
         } else
 #endif
         for (unsigned spins = 0;; ++spins) {
-          bool ok = get_granule<T>(rs, g0 + kp, epoch, vs);
+          // the Σ r·dot granule is the same for every lane: lane 0 polls it, the wave takes it by readlane
+          bool ok = lane != 0 || get_granule<T>(rs, g0 + kp, epoch, vs);
 #pragma unroll
           for (int q = 0; q < Q; ++q) {
             v[q] = T(0);
@@ -808,6 +809,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
           }
           __builtin_amdgcn_s_sleep(1);
         }
+        vs = readlane_t(vs, 0);
 #pragma unroll
         for (int q = 0; q < Q; ++q) st[q] += v[q];
         sg += vs;
@@ -1092,7 +1094,9 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
             w = dsp;
           } else {
             for (unsigned spins = 0;; ++spins) {
-              bool ok = get_granule<T>(rs, base + m * (int)wt.xstride + GD, epoch, w);
+              // the Σ|Δγ| granule is the same for every lane: lane 0 polls it (readlane below) — 512 threads
+              // polling one granule were most of the requests queued at this CU per poll round
+              bool ok = lane != 0 || get_granule<T>(rs, base + m * (int)wt.xstride + GD, epoch, w);
               if (row) ok &= get_granule<T>(rs, base + m * (int)wt.xstride + tid, epoch, v);
               if (__all(ok)) break;
               if (spin_give_up(spins, wt.tmo, wt.spin_limit)) {
@@ -1101,6 +1105,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
               }
               __builtin_amdgcn_s_sleep(1);
             }
+            w = readlane_t(w, 0);
           }
           dot += row ? v : T(0);
           dsum += w;

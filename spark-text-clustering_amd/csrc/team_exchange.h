@@ -43,8 +43,9 @@ __device__ __forceinline__ bool get_granule(__amdgpu_buffer_rsrc_t rs, int idx, 
   return g.x == epoch && g.z == epoch;
 }
 __device__ __forceinline__ bool spin_give_up(unsigned spins, unsigned* tmo, unsigned limit) {
-  if (spins < limit &&
-      __hip_atomic_load((gu32*)tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+  // the team's timeout word is read every 32nd poll only (one request fewer per poll round)
+  if (spins < limit && ((spins & 31u) != 31u ||
+                        __hip_atomic_load((gu32*)tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u))
     return false;
   __hip_atomic_store((gu32*)tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;

@@ -10,6 +10,7 @@
 #                      (libstc_<n>.so); DTYPE=f32 for the fp32 kernels
 #   configs            BASELINE configs 4 / 5 lines, fp64 + fp32, with the CPU baseline (DTYPES narrows)
 #   c4ab / c5ab        config 4 / 5 A/B of the LIBS variants against the in-tree library (STEPS, WARMUP)
+#   c2env/c4env/c5env  config 2 / 4 / 5 lines of the in-tree library under each ENVS="name:VAR=val,…" setting
 #   feat               the featurisation line + its kernel profile + FETCH / WRITE passes
 #   prof               rocprofv3 stats + PMC passes of WORKLOADS="name:bench args;…" (each into
 #                      gpurun_out/prof_<name>; summarise with tools/pmc_summary.py --steady)
@@ -65,6 +66,10 @@ r_cab() {  # r_cab CONFIG
   for n in $LIBS; do step c$1_$n 500 env STC_LIB=$(lib $n) $B; done
   step c$1_new 500 $B
 }
+r_cenv() {  # r_cenv CONFIG: the in-tree library under each ENVS="name:VAR=val[,VAR=val] …" setting
+  local B="python bench.py --config $1 --steps ${STEPS:-6} --warmup ${WARMUP:-2} $FAST"
+  for spec in $ENVS; do step c$1_${spec%%:*} 500 env $(echo "${spec#*:}" | tr , ' ') $B; done
+}
 r_feat() {
   step feat 300 python bench.py --featurisation-only --steps 5
   rm -rf gpurun_out/featprof gpurun_out/featpmc
@@ -116,6 +121,9 @@ for r in "$@"; do
     configs) r_configs ;;
     c4ab) r_cab 4 ;;
     c5ab) r_cab 5 ;;
+    c4env) r_cenv 4 ;;
+    c5env) r_cenv 5 ;;
+    c2env) r_cenv 2 ;;
     feat) r_feat ;;
     prof) r_prof ;;
     counters) r_counters ;;
