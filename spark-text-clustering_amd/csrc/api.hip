@@ -688,7 +688,7 @@ int team_fault_member() {
 }
 
 template <typename T>
-bool launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamChoice tc) {
+bool launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamChoice tc, int64_t max_row) {
   const int P = tc.P;
   Ctx& c = *L.ctx;
   hipStream_t s = c.stream;
@@ -711,6 +711,7 @@ bool launch_wide_team(stc_lda& L, const lda::EStepArgs<T>& w, bool stats, TeamCh
   wt.tmo = L.team_words.as<unsigned>();
   wt.xbuf = L.team_x.p;
   wt.fault_member = team_fault_member();
+  wt.max_row = max_row <= INT32_MAX ? (int)max_row : -1;
   if (wt.fault_member >= 0) wt.spin_limit = 1u << 14;
   // every polled word zeroed before every launch: the timeout word, and the granules' epoch tags
   // (a tag left by an earlier launch could equal an epoch this launch waits for)
@@ -741,7 +742,7 @@ void launch_split(stc_lda& L, const DCsr& m, lda::EStepArgs<T> a, int64_t n, int
     w.n = n_short;
     const int dt = std::is_same<T, float>::value ? STC_F32 : STC_F64;  // (a mixed handle runs both)
     const TeamChoice tc = use_wide(L.k, dt) && !bound ? team_choice<T>(L, mean_rows, m.max_row) : TeamChoice{};
-    const bool team = tc.P > 1 && launch_wide_team<T>(L, w, stats, tc);
+    const bool team = tc.P > 1 && launch_wide_team<T>(L, w, stats, tc, m.max_row);
     if (team) {  // launched (a grid that could not be resident falls through to the one-CU kernel)
       L.kcount[tc.grid ? STC_KC_TGRID64 : tc.topics ? STC_KC_WIDE_TC : STC_KC_WIDE_MC] += 1;
       wait_stream(*L.ctx, s);

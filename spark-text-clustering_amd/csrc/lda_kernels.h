@@ -113,6 +113,9 @@ struct WideTeam {
                              // 512 + 2 (φ partials, Σ|Δγ|, Σγ)
   unsigned spin_limit = 1u << 22;  // polls before a member gives up (a few seconds)
   int fault_member = -1;     // debug (STC_TEAM_FAULT): this member of team 0 never publishes
+  int max_row = -1;          // the launch's longest document (< 0: unknown) — k_estep_wide_tc sizes its
+                             // per-row LDS arrays by it, so the rest of the CU's LDS holds block rows
+  int xrows = 0;             // (set by the tc launcher) rows of those arrays
 };
 // after the E-step's logphat: a timed-out team poisons the non-empty count (small[k] = −1e300, negative
 // after any all-reduce over ranks), which gates the λ / colsum / expElogβ' / α updates off

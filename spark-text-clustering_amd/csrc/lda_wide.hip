@@ -871,6 +871,25 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_estep_wide_tc's LDS: the per-row arrays sized by the launch's longest document (xr rows, ≥ NR so the
+// register rows past nnz read r = 0) instead of WLds's 512, so the CU's LDS holds more block rows — at
+// config 5 (k = 2000, ≈ 44 rows) 15 → 19 LDS rows next to the 24 register rows, and a document's rows
+// are streamed from L2 in Phase A and B of every iteration only past 43 instead of 39
+template <typename T>
+struct TcLds {
+  T red[2][kWWaves];      // [0]: Σ|Δγ| of the last update, [1]: Σ_n r_n·dot_n
+  double bd[kWWaves][4];  // Σγ partials
+};
+template <typename T>
+__host__ __device__ constexpr size_t tc_lds_head() {
+  return (sizeof(TcLds<T>) + 255) / 256 * 256;
+}
+// xs [kWWaves][xr] T, rr [xr] T, ids [xr] int
+template <typename T>
+__host__ __device__ constexpr size_t tc_lds_fixed(int xr) {
+  return (tc_lds_head<T>() + (size_t)xr * ((kWWaves + 1) * sizeof(T) + sizeof(int)) + 255) / 256 * 256;
+}
+
 // k_estep_wide_tc — a team of P workgroups per document with the TOPICS split (k > 512: config 5's
 // k = 2000 in fp64, whose 44 × 2000 × 8 B block is 4.5× what one CU keeps resident at 4 topics per
 // lane).  Member m owns topics [m·512Q, (m+1)·512Q) and every row of the document, so s = Bᵀr and the
@@ -882,8 +901,12 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_mc(EStepArgs<T> a, int
 template <typename T, int Q, int NR, bool STATS>
 __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int nl, WideTeam wt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  WLds<T>& sm = *reinterpret_cast<WLds<T>*>(smem);
-  T* const sB = reinterpret_cast<T*>(smem + wide_lds_fixed<T>());  // [nl][512·Q]
+  TcLds<T>& sm = *reinterpret_cast<TcLds<T>*>(smem);
+  const int xr = wt.xrows;                                           // ≥ every nnz of the launch, ≥ NR
+  T* const xs = reinterpret_cast<T*>(smem + tc_lds_head<T>());       // [kWWaves][xr] φ partials per wave
+  T* const rr = xs + kWWaves * xr;                                   // [xr] r_n
+  int* const ids = reinterpret_cast<int*>(rr + xr);                  // [xr] term ids
+  T* const sB = reinterpret_cast<T*>(smem + tc_lds_fixed<T>(xr));    // [nl][512·Q]
   __shared__ int s_abort;
   using Tr = WTr<T>;
   constexpr int CH = wide_chunk<T, Q>();
@@ -902,6 +925,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
   const int t0 = member * kP + Q * tid;  // this lane's first topic
   unsigned epoch = 0;
   if (tid == 0) s_abort = 0;
+  STAMP_DECL
 
   // one exchange: publish `mine` at slot `idx` (if `pub`), then the member-order sum of slot `idx`
   // over the team (every lane of a wave takes part in the poll; `need` = this lane reads the slot)
@@ -937,6 +961,10 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
     const int nnz = (int)(a.indptr[row + 1] - s0);
     const int64_t e0 = a.bptr ? a.bptr[slot] : s0;
     const int nres = NR + nl;
+    if (nnz > xr) {  // longer than the launch's max_row said: the whole launch goes to the one-CU kernel
+      if (tid == 0) __hip_atomic_store(wt.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
 
     T cts = T(0), eps = T(0);
     int any = 0;
@@ -944,7 +972,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
       const int64_t pos = s0 + (a.order ? a.order[s0 + tid] : tid);
       const int id = a.indices[pos];
       cts = a.values[pos];
-      sm.ids[tid] = id;
+      ids[tid] = id;
       eps = fmin(fmax((T)fmin(exp(kLogEps - a.logscale[id]), 1e300), Tr::eps_floor()), Tr::eps_cap());
       any = cts != T(0);
     }
@@ -977,7 +1005,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
         if (tid < nnz) {
           a.r[e0 + tid] = T(0);
           if (STATS) {
-            a.keys[e0 + tid] = (uint32_t)sm.ids[tid];
+            a.keys[e0 + tid] = (uint32_t)ids[tid];
             a.vals[e0 + tid] = entry_val<T>(slot, e0 + tid, T(0));
           }
         }
@@ -1005,23 +1033,24 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
     gs = Tr::wsum(gs);
     as = Tr::wsum(as);
     if (lane == 0) {
-      sm.xs[wave][0] = gs;
-      sm.xs[wave][1] = as;
+      xs[wave * xr] = gs;
+      xs[wave * xr + 1] = as;
     }
     __syncthreads();
-    gs = sm.xs[0][0];
-    as = sm.xs[0][1];
+    gs = xs[0];
+    as = xs[1];
 #pragma unroll
     for (int w = 1; w < kWWaves; ++w) {
-      gs += sm.xs[w][0];
-      as += sm.xs[w][1];
+      gs += xs[w * xr];
+      as += xs[w * xr + 1];
     }
     __syncthreads();
 
+    STAMP(0);  // per-document preamble: ids, ε', γ₀, Σγ₀ / Σα
     // the block of this member's topics: rows < NR in VGPRs, < NR + nl in LDS, the rest streamed
     T B[NR > 0 ? NR : 1][Q];
-    load_block<T, Q, NR>(a.Bp, sm.ids, nnz, nres, sB, kp, t0, B);
-    if (tid >= nnz) sm.rr[tid] = T(0);
+    load_block<T, Q, NR>(a.Bp, ids, nnz, nres, sB, kp, t0, B);
+    if (tid >= nnz && tid < xr) rr[tid] = T(0);
 
     T cs = Tr::psi(gs);
 #pragma unroll
@@ -1030,6 +1059,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
     int it = 0;
     const T kd = (T)k;
     T rfin = T(0);
+    STAMP(1);  // the block's loads, the first eθ
     while (true) {
       // Phase A: this member's φ partials, as k_estep_wide
 #pragma unroll
@@ -1045,7 +1075,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
           }
           const T v = rs_chunk<T, CH>(x, lane);
           const int n = CH * c + rs_row<CH>(lane);
-          if (rs_pub<CH>(lane) && n < nnz) sm.xs[wave][n] = v;
+          if (rs_pub<CH>(lane) && n < nnz) xs[wave * xr + n] = v;
         }
       }
       for (int n0 = NR; n0 < nnz; n0 += CH) {
@@ -1053,7 +1083,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
 #pragma unroll
         for (int bb = 0; bb < CH; bb += LB) {
           T y[LB][Q];
-          rows_q<T, Q, LB>(a.Bp, sm.ids, sB, kp, t0, NR, nres, nnz, n0 + bb, y);
+          rows_q<T, Q, LB>(a.Bp, ids, sB, kp, t0, NR, nres, nnz, n0 + bb, y);
 #pragma unroll
           for (int i = 0; i < LB; ++i) {
             T acc = T(0);
@@ -1064,18 +1094,19 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
         }
         const T v = rs_chunk<T, CH>(x, lane);
         const int n = n0 + rs_row<CH>(lane);
-        if (rs_pub<CH>(lane) && n < nnz) sm.xs[wave][n] = v;
+        if (rs_pub<CH>(lane) && n < nnz) xs[wave * xr + n] = v;
       }
       const T dsum_w = Tr::wsum(dg);
       if (lane == 0) sm.red[0][wave] = dsum_w;
       __syncthreads();  // (1) row sums and Σ|Δγ| published (and any wave's give-up in s_abort)
+      STAMP(2);  // Phase A + barrier 1
       if (s_abort) break;
       ++epoch;
       T dotp = T(0);
       if (tid < nnz) {
-        dotp = sm.xs[0][tid];
+        dotp = xs[tid];
 #pragma unroll
-        for (int w = 1; w < kWWaves; ++w) dotp += sm.xs[w][tid];
+        for (int w = 1; w < kWWaves; ++w) dotp += xs[w * xr + tid];
       }
       T dsp = sm.red[0][0];
 #pragma unroll
@@ -1111,17 +1142,19 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
           dsum += w;
         }
       }
+      STAMP(3);  // exchange: publish, poll, member-order sums
       const bool last = (it > 0 && dsum / kd <= T(1e-3)) || it >= a.max_iter;  // team-uniform
       T rd = T(0);
       if (tid < nnz) {
         const T r = cts * Tr::rcp(dot + eps);
-        sm.rr[tid] = r;
+        rr[tid] = r;
         rfin = r;
         rd = fma(r, dot, rd);
       }
       rd = Tr::wsum(rd);
       if (lane == 0) sm.red[1][wave] = rd;
       __syncthreads();  // (2) r and Σ r·dot published
+      STAMP(4);  // r, Σ r·φ, barrier 2
       if (last || s_abort) break;
       T sg = sm.red[1][0];
 #pragma unroll
@@ -1134,16 +1167,16 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
       for (int q = 0; q < Q; ++q) s[q] = T(0);
 #pragma unroll
       for (int n = 0; n < NR; ++n) {
-        const T r = sm.rr[n];
+        const T r = rr[n];
 #pragma unroll
         for (int q = 0; q < Q; ++q) s[q] = fma(B[n][q], r, s[q]);
       }
       for (int n0 = NR; n0 < nnz; n0 += LB) {
         T y[LB][Q];
-        rows_q<T, Q, LB>(a.Bp, sm.ids, sB, kp, t0, NR, nres, nnz, n0, y);
+        rows_q<T, Q, LB>(a.Bp, ids, sB, kp, t0, NR, nres, nnz, n0, y);
 #pragma unroll
         for (int i = 0; i < LB; ++i) {
-          const T r = n0 + i < nnz ? sm.rr[n0 + i] : T(0);
+          const T r = n0 + i < nnz ? rr[n0 + i] : T(0);
 #pragma unroll
           for (int q = 0; q < Q; ++q) s[q] = fma(y[i][q], r, s[q]);
         }
@@ -1159,6 +1192,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
         }
       }
       ++it;
+      STAMP(5);  // ψ(Σγ'), Phase B, γ / eθ
     }
     if (s_abort) return;  // a team timed out: every block leaves (the host re-runs the one-CU kernel)
 
@@ -1166,7 +1200,7 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
     if (member == 0 && tid < nnz) {
       a.r[e0 + tid] = rfin;
       if (STATS) {
-        a.keys[e0 + tid] = (uint32_t)sm.ids[tid];
+        a.keys[e0 + tid] = (uint32_t)ids[tid];
         a.vals[e0 + tid] = entry_val<T>(slot, e0 + tid, rfin);
       }
     }
@@ -1197,7 +1231,9 @@ __global__ __launch_bounds__(kWThreads) void k_estep_wide_tc(EStepArgs<T> a, int
       if (a.nonempty) a.nonempty[mem] = 1;
     }
     __syncthreads();  // LDS (ids, xs, rr, bd, sB) is rewritten by the next document
+    STAMP(6);  // outputs, the final Σγ exchange
   }
+  STAMP_FLUSH
 }
 
 // register rows per (T, Q): NR·Q·sizeof(T)/4 ≈ 128 VGPRs, so 512 threads keep two waves per SIMD
@@ -1296,10 +1332,13 @@ bool launch_q_mc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTea
 }
 
 template <typename T, int Q>
-bool launch_q_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, const WideTeam& wt) {
+bool launch_q_tc(hipStream_t s, const EStepArgs<T>& a, bool stats, WideTeam wt) {
   bool ok = true;
   constexpr int NR = wide_nr_mc<T, Q>();
-  const size_t fixed = wide_lds_fixed<T>();
+  // the per-row arrays: the launch's longest document (every one when unknown), at least the register rows
+  const int mr = wt.max_row >= 0 && wt.max_row <= kWRows ? wt.max_row : kWRows;
+  wt.xrows = (std::max(mr, std::max(NR, 2)) + 1) / 2 * 2;
+  const size_t fixed = tc_lds_fixed<T>(wt.xrows);
   const size_t row_bytes = sizeof(T) * kWThreads * Q;
   int nl = (int)((kWLds - fixed - 256) / row_bytes);
   const size_t lds = fixed + (size_t)nl * row_bytes;

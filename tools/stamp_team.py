@@ -1,5 +1,6 @@
 """Where the team E-step spends its cycles: per-phase s_memtime stamps of lda_wide.hip k_estep_wide_mc
-(--kernel mc, with STC_WIDE_TEAM=P) or lda_team64.hip k_estep_tgrid64 (--kernel tgrid, the fp64 default).
+(--kernel mc, with STC_WIDE_TEAM=P), k_estep_wide_tc (--kernel tc: config 5's, --k 2000 --tokens 50
+--vocab 262144) or lda_team64.hip k_estep_tgrid64 (--kernel tgrid, the fp64 default).
 
     make -C spark-text-clustering_amd/csrc stamp
     STC_LIB=spark-text-clustering_amd/stc/libstc_stamp.so python tools/stamp_team.py [--dtype f64 ...]
@@ -23,7 +24,10 @@ PHASES = {"mc": ["per-doc preamble + block loads", "A: phi rows + reduce", "barr
                  "exchange: publish + wait + sums", "gamma, psi/exp", "outputs"],
           "tgrid": ["block loads", "A: phi FMAs + worker sums", "exchange: publish + poll + sums", "r, eps ballot, r reads",
                     "B: s FMAs + stores", "barrier 1", "psi phase (psi waves)", "barrier 2 (psi waves)",
-                    "psi phase (others: empty)", "barrier 2 (others)"]}
+                    "psi phase (others: empty)", "barrier 2 (others)"],
+          "tc": ["per-doc preamble", "block loads + first eth", "A: phi partials + barrier 1",
+                 "exchange: publish + poll + sums", "r, sum r*phi, barrier 2", "B: s + gamma/psi/exp",
+                 "outputs + final exchange"]}
 
 
 def main():
@@ -72,7 +76,7 @@ def main():
     docs = c1["docs"] - c0["docs"]
     iters = c1["inner_iters"] - c0["inner_iters"]
     tot = cyc[:len(phases)].sum()
-    P = int(os.environ.get("STC_WIDE_TEAM", "0")) or (-(-a.k // 104) if a.kernel == "tgrid" else None)
+    P = int(os.environ.get("STC_WIDE_TEAM", "0")) or {"tgrid": -(-a.k // 104), "tc": -(-a.k // 1024)}.get(a.kernel)
     out = {"k": a.k, "dtype": a.dtype, "team": P or "auto", "docs": int(docs),
            "mean_inner_iters": iters / max(1, docs), "share": {}, "cycles_per_block_wave_iter": {}}
     waves = 8 * (P or 1)
