@@ -555,3 +555,39 @@ def test_team_timeout_falls_back_to_the_one_cu_kernel(ctx, k, monkeypatch):
     np.testing.assert_array_equal(fb[3], one[3])
     team = run(2, False)  # the healthy team agrees with the one-CU kernel to rounding
     np.testing.assert_allclose(team[0], one[0], rtol=1e-9)
+
+
+def test_topic_team_lds_layout_follows_the_longest_document(ctx, monkeypatch):
+    """k_estep_wide_tc sizes its per-row LDS arrays by the launch's longest document (WideTeam::max_row:
+    known for an uploaded CSR, unknown — 512 rows — for a device-built one), so the two layouts keep
+    different numbers of block rows in LDS and stream the rest.  The same documents through both give
+    bit-identical γ, iteration counts and sufficient statistics (the rows' values and summation order do
+    not depend on where a row is kept)."""
+    import stc
+
+    rng = np.random.default_rng(2026)
+    k, V, D = 1100, 1 << 12, 240
+    words = [f"w{i}" for i in range(3000)]
+    docs = []
+    for _ in range(D):
+        pick = rng.choice(len(words), size=int(rng.integers(30, 61)), replace=False)
+        docs.append([words[i] for i in pick for _ in range(int(rng.integers(1, 4)))])
+    d_dev = stc.HashingTF(numFeatures=V, ctx=ctx).transform_device(docs)  # max_row unknown
+    host = d_dev.download()
+    assert np.diff(host.indptr).max() > 39  # rows past 24 VGPR + 15 LDS rows: the layouts differ
+    d_up = stc.DeviceCsr.upload(ctx, host, stc.STC_F64)  # max_row known
+    lam = rng.gamma(100.0, 0.01, size=(V, k))
+    g0 = rng.gamma(100.0, 0.01, size=(D, k))
+    monkeypatch.setenv("STC_WIDE_TEAM", "2")
+    out = []
+    for d in (d_dev, d_up):
+        h = stc.LdaHandle(ctx, k, V, dtype="f64")
+        h.set_corpus(d, D)
+        h.set_topics(lam)
+        out.append(h.estep(np.arange(D), g0, want_stat=True))
+        assert h.counters()["kernels"]["k_estep_wide_tc"] >= 1
+        h.close()
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+    d_dev.free()
+    d_up.free()
