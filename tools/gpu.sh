@@ -14,6 +14,7 @@
 #   feat               the featurisation line + its kernel profile + FETCH / WRITE passes
 #   prof               rocprofv3 stats + PMC passes of WORKLOADS="name:bench args;…" (each into
 #                      gpurun_out/prof_<name>; summarise with tools/pmc_summary.py --steady)
+#   bitwise            tools/ab_bitwise.py: each LIBS variant's E-step / next() outputs vs the in-tree library's
 #   counters           one --pmc pass of $COUNTERS (those this rocprofv3 lists) over the headline E-step
 #   ubench             tools/ubench_f64 (the fp64 chain micro-benchmark)
 set -o pipefail
@@ -60,6 +61,9 @@ r_configs() {
       tail -n 1 gpurun_out/c${c}_$dt.log > gpurun_out/c${c}_$dt.json
     done
   done
+}
+r_bitwise() {
+  for n in $LIBS; do step bw_$n 400 python tools/ab_bitwise.py spark-text-clustering_amd/stc/libstc.so $(lib $n); done
 }
 r_cab() {  # r_cab CONFIG
   local B="python bench.py --config $1 --steps ${STEPS:-6} --warmup ${WARMUP:-2} $FAST"
@@ -118,6 +122,7 @@ for r in "$@"; do
     check) r_check ;;
     bench) r_bench ;;
     ab) r_ab ;;
+    bitwise) r_bitwise ;;
     configs) r_configs ;;
     c4ab) r_cab 4 ;;
     c5ab) r_cab 5 ;;
