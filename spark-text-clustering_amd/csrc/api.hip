@@ -92,6 +92,11 @@ struct stc_lda {
   DevBuf long_list;  // rows / grid kernels: the launch's long documents (count word + slot offsets)
   DevBuf o_keys, o_keys2, o_idx, o_idx2, o_batch, o_orig, o_nnz, o_tmp;  // slot ordering (order_slots)
   bool sort_docs = true;  // STC_SORT_DOCS=0 keeps sampling order
+  // fp64 rows kernels: the sstats pairs built and radix-sorted on a low-priority stream beside the E-step
+  // (estep_and_stats); STC_PRESORT=0 sorts them after the E-step
+  bool presort = true;
+  hipStream_t sort_stream = nullptr;
+  hipEvent_t ev_ps0 = nullptr, ev_sorted = nullptr;
   // many-topic kernel: per-entry row order, rarest terms first (lda_wide.hip), for `order_for`
   DevBuf order, order_df;
   const DCsr* order_for = nullptr;
@@ -166,6 +171,9 @@ struct stc_lda {
       if (ev_rs[j]) (void)hipEventDestroy(ev_rs[j]);
     }
     if (cstream) (void)hipStreamDestroy(cstream);
+    if (ev_ps0) (void)hipEventDestroy(ev_ps0);
+    if (ev_sorted) (void)hipEventDestroy(ev_sorted);
+    if (sort_stream) (void)hipStreamDestroy(sort_stream);
   }
 };
 
@@ -947,6 +955,31 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   a.iters = L.iters.as<int32_t>();
   a.nonempty = L.nonempty.as<int32_t>();
   record(L, 1);
+  // fp64 on the rows kernels (k ≤ 104, every slot on them): an entry's sort value carries its index, not r, so
+  // the (term, slot) pairs and their radix sort depend on the batch alone — they run on a low-priority stream
+  // beside the E-step, whose blocks take the CU slots the resident grid frees as it drains, instead of after it
+  bool presort = false;
+  if constexpr (std::is_same<T, double>::value)
+    presort = L.presort && !L.mixed && !use_wide(L.k, STC_F64) && n_short == n && E > 0;
+  if (presort) {
+    if (!L.sort_stream) {
+      int least = 0, greatest = 0;
+      HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIP_CHECK(hipStreamCreateWithPriority(&L.sort_stream, hipStreamNonBlocking, least));
+      HIP_CHECK(hipEventCreateWithFlags(&L.ev_ps0, hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&L.ev_sorted, hipEventDisableTiming));
+    }
+    HIP_CHECK(hipEventRecord(L.ev_ps0, s));  // the batch and its entry offsets are built; skeys / svals free
+    HIP_CHECK(hipStreamWaitEvent(L.sort_stream, L.ev_ps0, 0));
+    lda::launch_entry_pairs(L.sort_stream, L.corpus->indptr.as<int64_t>(), L.corpus->indices.as<int32_t>(),
+                            L.batch.as<int32_t>(), L.bptr.as<int64_t>(), n, L.keys.as<uint32_t>(), L.vals.as<uint64_t>());
+    size_t tb = L.sort_tmp.bytes;
+    HIP_CHECK(term_sort(L.sort_tmp.p, tb, L.keys.as<uint32_t>(), L.skeys.as<uint32_t>(), L.vals.as<uint64_t>(),
+                        L.svals.as<uint64_t>(), E, bits_for(L.V), L.sort_stream));
+    HIP_CHECK(hipEventRecord(L.ev_sorted, L.sort_stream));
+    a.keys = nullptr;  // (the E-step kernels leave the pairs alone)
+    a.vals = nullptr;
+  }
   launch_split<T>(L, *L.corpus, a, n, n_short, true, false, n > 0 ? (double)E / (double)n : 0.0);
   if constexpr (std::is_same<T, float>::value) {
     if (L.mixed) mixed_resolve(L, n, E, iteration, g0_64, want_gamma);
@@ -972,7 +1005,9 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   } else {
     HIP_CHECK(hipMemsetAsync(L.stat.p, 0, sizeof(T) * L.vpad * L.kp, s));  // padded rows stay zero
   }
-  if (E > 0) {
+  if (presort) {
+    HIP_CHECK(hipStreamWaitEvent(s, L.ev_sorted, 0));
+  } else if (E > 0) {
     size_t tb = L.sort_tmp.bytes;
     HIP_CHECK(term_sort(L.sort_tmp.p, tb, L.keys.as<uint32_t>(), L.skeys.as<uint32_t>(), L.vals.as<uint64_t>(),
                         L.svals.as<uint64_t>(), E, bits_for(L.V), s));
@@ -2141,6 +2176,8 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     L->hot_order = !(ho && ho[0] == '0');
     const char* sd = std::getenv("STC_SORT_DOCS");
     L->sort_docs = !(sd && sd[0] == '0');
+    const char* psr = std::getenv("STC_PRESORT");
+    L->presort = !(psr && psr[0] == '0');
     const char* wt = std::getenv("STC_WIDE_TEAM");
     L->team_force = wt ? std::max(0, std::min(8, std::atoi(wt))) : 0;
     const char* tg = std::getenv("STC_TGRID");

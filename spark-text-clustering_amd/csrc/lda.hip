@@ -1314,6 +1314,29 @@ void launch_permute_slots(hipStream_t s, const int32_t* idx, int64_t n, const in
   k_permute_slots<<<(unsigned)(g > 4096 ? 4096 : g), 256, 0, s>>>(idx, n, batch, orig, nnz, batch2, orig2, nnz2);
   KERNEL_CHECK();
 }
+// The sstats pairs of an fp64 launch built from the batch alone (api.hip presort): entry e = bptr[slot] + n
+// of slot `slot` is the slot's n-th CSR entry, with key its term and value entry_val(slot, e) — exactly what
+// the rows E-step kernels write in their close phase (fp64 carries the entry index, not r), so the radix sort
+// can run beside the E-step instead of after it.  One wave per slot.
+__global__ __launch_bounds__(256) void k_entry_pairs(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+                                                     const int32_t* __restrict__ batch, const int64_t* __restrict__ bptr,
+                                                     int64_t n, uint32_t* __restrict__ keys, uint64_t* __restrict__ vals) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t slot = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6; slot < n; slot += ((int64_t)gridDim.x * 256) >> 6) {
+    const int64_t row = batch[slot], s0 = indptr[row], nnz = indptr[row + 1] - s0, e0 = bptr[slot];
+    for (int64_t j = lane; j < nnz; j += 64) {
+      keys[e0 + j] = (uint32_t)indices[s0 + j];
+      vals[e0 + j] = entry_val<double>(slot, e0 + j, 0.0);
+    }
+  }
+}
+void launch_entry_pairs(hipStream_t s, const int64_t* indptr, const int32_t* indices, const int32_t* batch,
+                        const int64_t* bptr, int64_t n, uint32_t* keys, uint64_t* vals) {
+  if (n == 0) return;
+  const int64_t g = ceil_div(n, 4);
+  k_entry_pairs<<<(unsigned)(g > 8192 ? 8192 : g), 256, 0, s>>>(indptr, indices, batch, bptr, n, keys, vals);
+  KERNEL_CHECK();
+}
 void launch_iota(hipStream_t s, int32_t* x, int64_t n) {
   if (n == 0) return;
   const int64_t g = ceil_div(n, 256);

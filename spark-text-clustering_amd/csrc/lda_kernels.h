@@ -219,6 +219,8 @@ void launch_last3(hipStream_t s, const int32_t* a, const int64_t* b, const int32
 void launch_permute_slots(hipStream_t s, const int32_t* idx, int64_t n, const int32_t* batch, const int32_t* orig,
                           const int64_t* nnz, int32_t* batch2, int32_t* orig2, int64_t* nnz2);
 void launch_iota(hipStream_t s, int32_t* x, int64_t n);
+void launch_entry_pairs(hipStream_t s, const int64_t* indptr, const int32_t* indices, const int32_t* batch,
+                        const int64_t* bptr, int64_t n, uint32_t* keys, uint64_t* vals);
 void launch_fill_batch(hipStream_t s, const int64_t* indptr, int64_t D, int64_t cap,
                        const int32_t* counts, const int32_t* count_incl,
                        const int32_t* short_incl, int64_t n_short, int32_t* batch_p,

@@ -500,7 +500,7 @@ __device__ __forceinline__ void rows64_close(const EStepArgs<double>& a, RLds<S>
     const int ws = (n >> 3) & 3, q = 8 * (n >> 5) + (n & 7);  // row n = 32·set + 8·wave + row lane
     const double rv = sm.rrow[ws][q];
     a.r[e0 + n] = rv;
-    if (STATS) {
+    if (STATS && a.keys) {  // (null: the pairs were built and sorted beside the E-step, api.hip presort)
       a.keys[e0 + n] = (uint32_t)sm.rid[ws][q];
       a.vals[e0 + n] = entry_val<double>(slot, e0 + n, rv);
     }

@@ -1,6 +1,6 @@
 """A/B parity of two builds of libstc: the same E-step + a few next() steps, outputs compared bit for bit.
 
-    python tools/ab_bitwise.py LIB_A LIB_B [--docs N] [--k K] [--dtype f64]
+    python tools/ab_bitwise.py LIB_A LIB_B [--docs N] [--k K] [--dtype f64] [--env-a VAR=VAL] [--env-b VAR=VAL]
 
 Each library runs in its own child process (STC_LIB selects it); the child writes γ, stat, the iteration
 counts and λ after three next() steps to an .npz, and the parent compares the arrays with array_equal.
@@ -46,6 +46,8 @@ def main():
     p.add_argument("--k", type=int, default=100)
     p.add_argument("--dtype", default="f64")
     p.add_argument("--child", default=None)
+    p.add_argument("--env-a", action="append", default=[], help="VAR=VAL set for the first run only")
+    p.add_argument("--env-b", action="append", default=[], help="VAR=VAL set for the second run only")
     a = p.parse_args()
     if a.child:
         child(a.child, a.docs, a.k, a.dtype)
@@ -55,6 +57,7 @@ def main():
         for i, lib in enumerate(a.libs):
             out = os.path.join(td, f"{i}.npz")
             env = dict(os.environ, STC_LIB=os.path.abspath(lib))
+            env.update(kv.split("=", 1) for kv in (a.env_a if i == 0 else a.env_b))
             subprocess.run([sys.executable, __file__, *a.libs, "--docs", str(a.docs), "--k", str(a.k), "--dtype",
                             a.dtype, "--child", out], env=env, check=True)
             outs.append(dict(np.load(out)))
