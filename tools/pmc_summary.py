@@ -28,12 +28,13 @@ sys.path.insert(0, ROOT)
 
 # kernels of the E-step phase (the bench roofline's "kernel"): E-step, term sort, sstats SpMM,
 # the stat memset, and the partition scans (rocprim; tiny)
-PHASE = re.compile(r"k_estep|k_sstats|k_fixup|rocprim|fillBuffer|k_part_|k_fill_batch|k_batch_nnz|k_mixed_")
+PHASE = re.compile(r"k_estep|k_sstats|k_fixup|rocprim|fillBuffer|k_part_|k_fill_batch|k_batch_nnz|k_mixed_|k_entry_pairs")
 # bench.py's roofline window (SURVEY §8(d) K6 = gather + scatter): the training E-step launches and the
 # sstats phase after them — the stat clear, the (term, slot) radix sort, k_sstats / k_fixup, logphat and the
 # iteration statistics (HIP events 1 → 3 in api.hip estep_and_stats)
 WINDOW = re.compile(r"k_estep|k_rows64_long_list|k_sstats|k_fixup|k_logphat|k_iter_stats|fillBuffer"
-                    r"|radix_sort_onesweep|k_mixed_")  # (k_mixed_: the mixed mode's fp64 re-solve list and fixup)
+                    r"|radix_sort_onesweep|k_mixed_|k_entry_pairs")  # (k_mixed_: the mixed mode's fp64 re-solve list and
+# fixup; k_entry_pairs: the fp64 rows path's sstats pairs, built beside the E-step since round 6)
 # the dominant kernel (bench.py's roofline): the training E-step launches (STATS variant), one per
 # minibatch — the grid kernel plus the workgroup kernel for the few docs past its row capacity, the
 # same launches the bench's HIP-event "estep" phase brackets
