@@ -591,3 +591,21 @@ def test_topic_team_lds_layout_follows_the_longest_document(ctx, monkeypatch):
         np.testing.assert_array_equal(a, b)
     d_dev.free()
     d_up.free()
+
+
+@pytest.mark.parametrize("k", [20, 100])
+def test_presorted_sstats_pairs_bitwise(ctx, monkeypatch, k):
+    """fp64 rows path: the (term, slot) pairs built from the batch and radix-sorted beside the E-step
+    (STC_PRESORT, the default) give the model of the pairs the E-step writes and sorts after it —
+    bit for bit, over sampled next() steps with empty, short and 7–8-row-set documents."""
+    rng = np.random.default_rng(47 + k)
+    corpus = random_corpus(rng, 400, 4096, 0, 250, empty_every=19)
+    runs = []
+    for presort in ("0", "1"):
+        monkeypatch.setenv("STC_PRESORT", presort)
+        h, _ = _train(ctx, corpus, k, "f64", 5)
+        runs.append((h.topics(), h.alpha(), h.iteration()))
+    (l0, a0, i0), (l1, a1, i1) = runs
+    assert i0 == i1 == 5
+    np.testing.assert_array_equal(l1, l0)
+    np.testing.assert_array_equal(a1, a0)
