@@ -94,7 +94,7 @@ struct stc_lda {
   bool sort_docs = true;  // STC_SORT_DOCS=0 keeps sampling order
   // fp64 rows kernels: the sstats pairs built and radix-sorted on a low-priority stream beside the E-step
   // (estep_and_stats); STC_PRESORT=0 sorts them after the E-step
-  bool presort = true;
+  int presort = 1;
   hipStream_t sort_stream = nullptr;
   hipEvent_t ev_ps0 = nullptr, ev_sorted = nullptr;
   // many-topic kernel: per-entry row order, rarest terms first (lda_wide.hip), for `order_for`
@@ -961,6 +961,14 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   bool presort = false;
   if constexpr (std::is_same<T, double>::value)
     presort = L.presort && !L.mixed && !use_wide(L.k, STC_F64) && n_short == n && E > 0;
+  auto enqueue_presort = [&] {
+    lda::launch_entry_pairs(L.sort_stream, L.corpus->indptr.as<int64_t>(), L.corpus->indices.as<int32_t>(),
+                            L.batch.as<int32_t>(), L.bptr.as<int64_t>(), n, L.keys.as<uint32_t>(), L.vals.as<uint64_t>());
+    size_t tb = L.sort_tmp.bytes;
+    HIP_CHECK(term_sort(L.sort_tmp.p, tb, L.keys.as<uint32_t>(), L.skeys.as<uint32_t>(), L.vals.as<uint64_t>(),
+                        L.svals.as<uint64_t>(), E, bits_for(L.V), L.sort_stream));
+    HIP_CHECK(hipEventRecord(L.ev_sorted, L.sort_stream));
+  };
   if (presort) {
     if (!L.sort_stream) {
       int least = 0, greatest = 0;
@@ -971,16 +979,14 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
     }
     HIP_CHECK(hipEventRecord(L.ev_ps0, s));  // the batch and its entry offsets are built; skeys / svals free
     HIP_CHECK(hipStreamWaitEvent(L.sort_stream, L.ev_ps0, 0));
-    lda::launch_entry_pairs(L.sort_stream, L.corpus->indptr.as<int64_t>(), L.corpus->indices.as<int32_t>(),
-                            L.batch.as<int32_t>(), L.bptr.as<int64_t>(), n, L.keys.as<uint32_t>(), L.vals.as<uint64_t>());
-    size_t tb = L.sort_tmp.bytes;
-    HIP_CHECK(term_sort(L.sort_tmp.p, tb, L.keys.as<uint32_t>(), L.skeys.as<uint32_t>(), L.vals.as<uint64_t>(),
-                        L.svals.as<uint64_t>(), E, bits_for(L.V), L.sort_stream));
-    HIP_CHECK(hipEventRecord(L.ev_sorted, L.sort_stream));
+    // STC_PRESORT=2: the pairs and the sort enqueued before the E-step launch (their blocks then compete with
+    // the grid's first workgroups); default: after it, so the resident grid is dispatched first
+    if (L.presort == 2) enqueue_presort();
     a.keys = nullptr;  // (the E-step kernels leave the pairs alone)
     a.vals = nullptr;
   }
   launch_split<T>(L, *L.corpus, a, n, n_short, true, false, n > 0 ? (double)E / (double)n : 0.0);
+  if (presort && L.presort != 2) enqueue_presort();
   if constexpr (std::is_same<T, float>::value) {
     if (L.mixed) mixed_resolve(L, n, E, iteration, g0_64, want_gamma);
   }
@@ -2177,7 +2183,7 @@ int stc_lda_create(stc_ctx* ctx, const stc_lda_config* cfg, stc_lda** out) {
     const char* sd = std::getenv("STC_SORT_DOCS");
     L->sort_docs = !(sd && sd[0] == '0');
     const char* psr = std::getenv("STC_PRESORT");
-    L->presort = !(psr && psr[0] == '0');
+    L->presort = psr ? std::max(0, std::min(2, std::atoi(psr))) : 1;
     const char* wt = std::getenv("STC_WIDE_TEAM");
     L->team_force = wt ? std::max(0, std::min(8, std::atoi(wt))) : 0;
     const char* tg = std::getenv("STC_TGRID");
