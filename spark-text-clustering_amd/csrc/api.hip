@@ -961,24 +961,31 @@ void estep_and_stats(stc_lda& L, int64_t n, int64_t n_short, int64_t E, const T*
   bool presort = false;
   if constexpr (std::is_same<T, double>::value)
     presort = L.presort && !L.mixed && !use_wide(L.k, STC_F64) && n_short == n && E > 0;
+  hipStream_t ss = nullptr;  // the handle's side stream when it has one (no extra hardware queue), else its own
   auto enqueue_presort = [&] {
-    lda::launch_entry_pairs(L.sort_stream, L.corpus->indptr.as<int64_t>(), L.corpus->indices.as<int32_t>(),
+    lda::launch_entry_pairs(ss, L.corpus->indptr.as<int64_t>(), L.corpus->indices.as<int32_t>(),
                             L.batch.as<int32_t>(), L.bptr.as<int64_t>(), n, L.keys.as<uint32_t>(), L.vals.as<uint64_t>());
     size_t tb = L.sort_tmp.bytes;
     HIP_CHECK(term_sort(L.sort_tmp.p, tb, L.keys.as<uint32_t>(), L.skeys.as<uint32_t>(), L.vals.as<uint64_t>(),
-                        L.svals.as<uint64_t>(), E, bits_for(L.V), L.sort_stream));
-    HIP_CHECK(hipEventRecord(L.ev_sorted, L.sort_stream));
+                        L.svals.as<uint64_t>(), E, bits_for(L.V), ss));
+    HIP_CHECK(hipEventRecord(L.ev_sorted, ss));
   };
   if (presort) {
-    if (!L.sort_stream) {
-      int least = 0, greatest = 0;
-      HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      HIP_CHECK(hipStreamCreateWithPriority(&L.sort_stream, hipStreamNonBlocking, least));
+    if (!L.ev_ps0) {
       HIP_CHECK(hipEventCreateWithFlags(&L.ev_ps0, hipEventDisableTiming));
       HIP_CHECK(hipEventCreateWithFlags(&L.ev_sorted, hipEventDisableTiming));
     }
+    // a process with several handles runs past the device's hardware queues (GPU_MAX_HW_QUEUES) when each adds
+    // a stream, and a stream sharing a queue waits behind unrelated work: the side stream (next()'s draws,
+    // which then queue behind the sort) is used when it exists
+    if (!L.side && !L.sort_stream) {
+      int least = 0, greatest = 0;
+      HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIP_CHECK(hipStreamCreateWithPriority(&L.sort_stream, hipStreamNonBlocking, least));
+    }
+    ss = L.side ? L.side : L.sort_stream;
     HIP_CHECK(hipEventRecord(L.ev_ps0, s));  // the batch and its entry offsets are built; skeys / svals free
-    HIP_CHECK(hipStreamWaitEvent(L.sort_stream, L.ev_ps0, 0));
+    HIP_CHECK(hipStreamWaitEvent(ss, L.ev_ps0, 0));
     // STC_PRESORT=2: the pairs and the sort enqueued before the E-step launch (their blocks then compete with
     // the grid's first workgroups); default: after it, so the resident grid is dispatched first
     if (L.presort == 2) enqueue_presort();
